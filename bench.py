@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""Benchmark: ViT-B/16 224x224 bf16 training step (forward + backward + SGD) on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--model vit_b16] [--batch 256]
+    torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
+        bench.py --gpus N --steps K --warmup W
+
+One process per GPU.  Each rank trains on its own 256-image shard of one seeded synthetic stream
+(weak scaling); gradients are summed by RCCL inside libvit_hip.so (per-layer chunks on a side
+stream, overlapped with backward).  torch is used only as plumbing: the gloo process group for
+the rendezvous / barrier / max-over-ranks timing and torch.cuda.synchronize(); torch is imported
+BEFORE the library so the process has a single HIP runtime.
+
+Prints ONE JSON line (rank 0).  `value` = images/s of the whole job = N*B*K / max-over-ranks
+wall time of the K timed steps.  `roofline` describes the dominant GEMM class, timed with HIP
+events on the trainer's stream over the same timed steps.  `cpu_baseline` = the CPU oracle
+(the reference loops restated in C, single thread) timed on this host on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch  # noqa: F401  (first: owns the HIP runtime of the process)
+import torch.distributed as dist
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+from vitpkg import vit  # noqa: E402
+
+METRIC = "images/sec (train step) ViT-B/16 224² bf16 at 1/2/4/8 MI355X; % MFMA roofline"
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", default="vit_b16")
+    ap.add_argument("--batch", type=int, default=256, help="images per GPU")
+    ap.add_argument("--lr", type=float, default=1e-4)
+    ap.add_argument("--no-overlap", action="store_true", help="one all-reduce after backward")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events")
+    return ap.parse_args()
+
+
+def _block_once(o, t):
+    """One transformer block forward + backward, in train_vit.rs:236-245 / :359-368 order."""
+    B, T, C, NH, BTC = t["B"], t["T"], t["C"], t["NH"], t["BTC"]
+    a, w, bv, g, gw, gb = t["a"], t["w"], t["b"], t["g"], t["gw"], t["gb"]
+    x, lnw, lnb, m1, r1, m2, r2, dres = t["x"], t["lnw"], t["lnb"], t["m1"], t["r1"], t["m2"], t["r2"], t["dres"]
+    for arr in list(g.values()) + list(gw.values()) + list(gb.values()) + [dres]:
+        arr[:] = 0
+    g["r3"][:] = t["dr3"]
+    t0 = time.perf_counter()
+    o.call("layernorm_forward", a["ln1"], m1, r1, x, lnw, lnb, B, T, C)
+    o.call("matmul_forward", a["qkv"], a["ln1"], w["qkvw"], bv["qkvb"], B, T, C, 3 * C)
+    o.call("attention_forward", a["atty"], a["pre"], a["att"], a["qkv"], B, T, C, NH)
+    o.call("matmul_forward", a["proj"], a["atty"], w["projw"], bv["projb"], B, T, C, C)
+    o.call("residual_forward", a["r2"], x, a["proj"], BTC)
+    o.call("layernorm_forward", a["ln2"], m2, r2, a["r2"], lnw, lnb, B, T, C)
+    o.call("matmul_forward", a["fch"], a["ln2"], w["fcw"], bv["fcb"], B, T, C, 4 * C)
+    o.call("gelu_forward", a["fchg"], a["fch"], 4 * BTC)
+    o.call("matmul_forward", a["fcp"], a["fchg"], w["fcpw"], bv["fcpb"], B, T, 4 * C, C)
+    o.call("residual_forward", a["r3"], a["r2"], a["fcp"], BTC)
+    dlnw, dlnb = t["dlnw"], t["dlnb"]
+    o.call("residual_backward", g["r2"], g["fcp"], g["r3"], BTC)
+    o.call("matmul_backward", g["fchg"], gw["fcpw"], gb["fcpb"], g["fcp"], a["fchg"], w["fcpw"], B, T, 4 * C, C)
+    o.call("gelu_backward", g["fch"], a["fch"], g["fchg"], 4 * BTC)
+    o.call("matmul_backward", g["ln2"], gw["fcw"], gb["fcb"], g["fch"], a["ln2"], w["fcw"], B, T, C, 4 * C)
+    o.call("layernorm_backward", g["r2"], dlnw, dlnb, g["ln2"], a["r2"], lnw, m2, r2, B, T, C)
+    o.call("residual_backward", dres, g["proj"], g["r2"], BTC)
+    o.call("matmul_backward", g["atty"], gw["projw"], gb["projb"], g["proj"], a["atty"], w["projw"], B, T, C, C)
+    o.call("attention_backward", g["qkv"], g["pre"], g["att"], g["atty"], a["qkv"], a["att"], B, T, C, NH)
+    o.call("matmul_backward", g["ln1"], gw["qkvw"], gb["qkvb"], g["qkv"], a["ln1"], w["qkvw"], B, T, C, 3 * C)
+    o.call("layernorm_backward", dres, dlnw, dlnb, g["ln1"], x, lnw, m1, r1, B, T, C)
+    return time.perf_counter() - t0
+
+
+def cpu_baseline(cfg, reps=3):
+    """Time the CPU oracle (reference loops, C, 1 thread) on a bounded sample: one image through
+    one transformer block forward + backward (all layer ops in train_vit.rs order, mean of `reps`)
+    plus the patch embedding and head; images/s = 1 / (L * t_block + t_embed_head)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_ctypes as oc
+    o = oc.Oracle("f32")
+    rng = np.random.default_rng(0)
+    C, T, NH, NC, P, IMG = cfg.channels, cfg.T, cfg.num_heads, cfg.num_classes, cfg.patch, cfg.img
+    B = 1
+    BTC = B * T * C
+    f = lambda n, s=1.0: o.arr(rng.normal(size=n) * s)
+    z = lambda n: o.arr(np.zeros(n))
+    acts = {k: z(n) for k, n in (("ln1", BTC), ("qkv", 3 * BTC), ("atty", BTC), ("pre", B * T * NH * T),
+                                ("att", B * T * NH * T), ("proj", BTC), ("r2", BTC), ("ln2", BTC),
+                                ("fch", 4 * BTC), ("fchg", 4 * BTC), ("fcp", BTC), ("r3", BTC))}
+    w = {k: f(n, 0.02) for k, n in (("qkvw", 3 * C * C), ("projw", C * C), ("fcw", 4 * C * C), ("fcpw", 4 * C * C))}
+    bv = {k: f(n, 0.02) for k, n in (("qkvb", 3 * C), ("projb", C), ("fcb", 4 * C), ("fcpb", C))}
+    t = {"B": B, "T": T, "C": C, "NH": NH, "BTC": BTC, "a": acts, "w": w, "b": bv,
+         "g": {k: z(v.size) for k, v in acts.items()}, "gw": {k: z(v.size) for k, v in w.items()},
+         "gb": {k: z(v.size) for k, v in bv.items()}, "x": f(BTC), "lnw": o.arr(np.ones(C)), "lnb": z(C),
+         "m1": z(B * T), "r1": z(B * T), "m2": z(B * T), "r2": z(B * T), "dres": z(BTC), "dr3": f(BTC),
+         "dlnw": z(C), "dlnb": z(C)}
+    t_block = sum(_block_once(o, t) for _ in range(reps)) / reps
+    # patch embedding + head (forward + backward) for the same image
+    K = 3 * P * P
+    px = f(3 * IMG * IMG)
+    pw, pb, cls, wpe = f(C * K, 0.02), z(C), z(C), z(T * C)
+    enc = z(BTC)
+    hw, hb = f(NC * C, 0.02), z(NC)
+    logits, probs, losses = z(NC), z(NC), z(1)
+    tgt = np.zeros(1, np.int32)
+    lnw, lnb = t["lnw"], t["lnb"]
+    t0 = time.perf_counter()
+    o.call("patch_embed_forward", enc, px, pw, pb, cls, wpe, B, IMG, P, C)
+    lnf, mf, rf = z(C), z(1), z(1)
+    o.call("layernorm_forward", lnf, mf, rf, enc[:C].copy(), lnw, lnb, 1, 1, C)
+    o.call("matmul_forward", logits, lnf, hw, hb, 1, 1, C, NC)
+    o.call("softmax_forward", probs, logits, 1, 1, NC)
+    o.call("crossentropy_forward", losses, probs, tgt, 1, 1, NC)
+    dlog, dl = z(NC), o.arr(np.ones(1))
+    o.call("crossentropy_softmax_backward", dlog, dl, probs, tgt, 1, 1, NC)
+    dlnf, dhw, dhb = z(C), z(NC * C), z(NC)
+    o.call("matmul_backward", dlnf, dhw, dhb, dlog, lnf, hw, 1, 1, C, NC)
+    denc = f(BTC)
+    o.call("patch_embed_backward", z(C * K), z(C), z(C), z(T * C), denc, px, B, IMG, P, C)
+    t_rest = time.perf_counter() - t0
+    t_img = cfg.num_layers * t_block + t_rest
+    return {"value": round(1.0 / t_img, 5), "unit": "images/s", "cores": 1, "kind": "port",
+            "sample": (f"1 image: one {cfg.name} transformer block fwd+bwd (mean of {reps}: {t_block:.2f} s) "
+                       f"x {cfg.num_layers} layers + patch-embed/head fwd+bwd ({t_rest:.2f} s); "
+                       f"oracle/oracle.c -O2 -ffp-contract=off, single thread")}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    L = vit.lib()
+    if L.vit_init(local):
+        vit.check("vit_init")
+    cfg = vit.data.CONFIGS[args.model]
+    B = args.batch
+    m = vit.ViT(cfg, B, vit.VIT_BF16, device=local)
+    m.set_params(vit.data.init_params(cfg, "ref", seed=1337))
+    px, lab = vit.data.synthetic_batch(cfg, B, seed=1337, offset_images=rank * B)
+    m.set_batch(px, lab)
+    del px
+    if world > 1:
+        uid = [vit.ViT.dp_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        m.dp_init(rank, world, uid[0], overlap=not args.no_overlap)
+    b_global = B * world
+
+    for _ in range(args.warmup):
+        m.train_step(args.lr, b_global)
+    m.sync()
+    loss_w = m.forward() if args.warmup else float("nan")   # sanity: finite loss after warmup
+    m.timing_reset()
+    m.set_timing(not args.no_timing)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    m.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        m.train_step(args.lr, b_global)
+    m.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    m.set_timing(False)
+    kern = m.timing() if not args.no_timing else {}
+    ips = world * B * args.steps / dt
+    _, gflop_img = cfg.train_gflop_per_image()
+
+    out = None
+    if rank == 0:
+        gemms = {k: v for k, v in kern.items() if k.startswith("gemm_")}
+        roof = None
+        if gemms:
+            dom = max(gemms, key=lambda k: gemms[k]["ms"])
+            d = gemms[dom]
+            avg_ms = d["ms"] / d["calls"]
+            ach = d["flops"] / d["calls"] / (avg_ms * 1e-3) / 1e12
+            roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                    "avg_launch_ms": round(avg_ms, 4), "flops_per_launch": d["flops"] / d["calls"]}
+        ksum = {k: {"ms_per_step": round(v["ms"] / args.steps, 3), "calls_per_step": v["calls"] // args.steps,
+                    "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1) if v["flops"] and v["ms"] else None}
+                for k, v in sorted(kern.items(), key=lambda kv: -kv[1]["ms"])}
+        out = {
+            "metric": METRIC, "value": round(ips, 2), "unit": "images/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (seeded splitmix64: N(0,1) pixels, uniform labels; reference init U[0,1)*0.02)",
+            "config": {"workload": f"{cfg.name} 224x224 train step (fwd+bwd+SGD), batch {B}/GPU",
+                       "model": cfg.name, "global_batch": b_global, "seq_len": cfg.T,
+                       "parallelism": f"dp{world}"},
+            "mfma_roofline_frac_step": round(ips * gflop_img / world / (PEAK_BF16_TFLOPS * 1e3), 4),
+            "train_gflop_per_image": round(gflop_img, 3),
+            "loss_after_warmup": round(loss_w, 4),
+            "roofline": roof, "kernels": ksum,
+        }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cfg)
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    m.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,127 @@
+/*
+ * vit_ops.h — C ABI of libvit_hip.so: the reference's layer ops as MI355X (gfx950) HIP kernels.
+ *
+ * Drop-in boundary.  The reference's layer ops are the free functions of
+ * /root/reference/train_vit.rs:376-670 (raw *mut f32 / *const f32 + c_int dims).  Each symbol
+ * below keeps the reference's name, argument order (outputs, inputs/weights, dims) and write
+ * semantics, with DEVICE pointers:
+ *   - forward ops OVERWRITE their outputs; backward ops ACCUMULATE (+=) into dinp/dweight/dbias
+ *     (train_vit.rs:524-525, 538, 549, 552, 578-579, 587, 595-596, 626-633, 650);
+ *   - a NULL bias means "no bias" (train_vit.rs:388, 548);
+ *   - the caller owns every buffer (ops never allocate caller-visible memory);
+ *   - ops are enqueued on the calling thread's stream (vit_set_stream); with VIT_SYNC=1 in the
+ *     environment every op synchronises before returning, restoring the reference's
+ *     synchronous semantics;
+ *   - the reference ops return () and have no error channel: failures (bad shapes, HIP errors)
+ *     set a sticky thread-local error read with vit_last_error().
+ * Semantic fixes relative to the reference text (SURVEY.md §8a defect register) are applied:
+ * D1 offsets by T, D2 full normalisation, D3 non-causal attention, D4 GELU derivative,
+ * D5 LN backward, D6 -log p loss, D7 patch embedding, D10 64-bit offsets.
+ * Activation layouts are the reference's: qkv [B,T,3C] (Q|K|V, head h at h*hs),
+ * preatt/att [B,T,NH,T] (row index bth = (b*T+t)*NH+h, train_vit.rs:406-410).
+ */
+#ifndef VIT_OPS_H
+#define VIT_OPS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ context */
+int vit_init(int device);                 /* select device; 0 on success */
+void vit_set_stream(void* hip_stream);    /* hipStream_t; NULL = default stream */
+void* vit_get_stream(void);
+int vit_sync(void);                        /* hipStreamSynchronize(current stream) */
+int vit_last_error(const char** msg);      /* 0 = no error; sticky until vit_clear_error */
+void vit_clear_error(void);
+/* device memory helpers for hosts without their own device allocator (ctypes tests, C hosts) */
+void* vit_malloc(size_t bytes);
+void vit_free(void* p);
+int vit_memcpy_h2d(void* dst, const void* src, size_t bytes);
+int vit_memcpy_d2h(void* dst, const void* src, size_t bytes);
+int vit_memcpy_d2d(void* dst, const void* src, size_t bytes);
+int vit_memset(void* dst, int value, size_t bytes);
+/* events for per-kernel timing on the current stream */
+void* vit_event_create(void);
+void vit_event_destroy(void* ev);
+int vit_event_record(void* ev);
+float vit_event_elapsed_ms(void* start, void* stop);
+
+/* ------------------------------------------------------------------ reference ops (fp32) */
+/* train_vit.rs:376 */
+void residual_forward(float* out, const float* inp1, const float* inp2, int N);
+/* train_vit.rs:384 — out[BT,OC] = inp[BT,C] . weight[OC,C]^T + bias */
+void matmul_forward(float* out, const float* inp, const float* weight, const float* bias,
+                    int B, int T, int C, int OC);
+/* train_vit.rs:400 (+ attention.rs:1) — preatt/att [B,T,NH,T] are required (drop-in mode) */
+void attention_forward(float* out, float* preatt, float* att, const float* inp,
+                       int B, int T, int C, int NH);
+/* train_vit.rs:453 */
+void layernorm_forward(float* out, float* mean, float* rstd, const float* inp,
+                       const float* weight, const float* bias, int B, int T, int C);
+/* train_vit.rs:482 */
+void gelu_forward(float* out, const float* inp, int N);
+/* train_vit.rs:493 */
+void softmax_forward(float* probs, const float* logits, int B, int T, int V);
+/* rusty_vit.rs:836 (called train_vit.rs:256), D6: losses = -log probs[target] */
+void crossentropy_forward(float* losses, const float* probs, const int* targets,
+                          int B, int T, int V);
+/* train_vit.rs:521 (+=) */
+void residual_backward(float* dinp1, float* dinp2, const float* dout, int N);
+/* train_vit.rs:530 (+=); dinp NULL skips the input gradient, dbias NULL skips the bias */
+void matmul_backward(float* dinp, float* dweight, float* dbias, const float* dout,
+                     const float* inp, const float* weight, int B, int T, int C, int OC);
+/* train_vit.rs:559 (+=); dpreatt/datt: accumulated [B,T,NH,T] scratch, NULL = internal */
+void attention_backward(float* dinp, float* dpreatt, float* datt, const float* dout,
+                        const float* inp, const float* att, int B, int T, int C, int NH);
+/* train_vit.rs:603 (+=) */
+void layernorm_backward(float* dinp, float* dweight, float* dbias, const float* dout,
+                        const float* inp, const float* weight, const float* mean,
+                        const float* rstd, int B, int T, int C);
+/* train_vit.rs:639 (+=), D4 */
+void gelu_backward(float* dinp, const float* inp, const float* dout, int N);
+/* undefined in the reference, called train_vit.rs:293 (+=): dlogits += (p - 1[tgt]) * dloss */
+void crossentropy_softmax_backward(float* dlogits, const float* dlosses, const float* probs,
+                                   const int* targets, int B, int T, int V);
+/* ViT replacement of encoder_forward (train_vit.rs:196): pixels [B,3,IMG,IMG] ->
+ * encoded [B,T,C], row 0 = cls + wpe[0], row 1+p = patch_p . patch_w^T + patch_b + wpe[1+p] */
+void patch_embed_forward(float* encoded, const float* pixels, const float* patch_w,
+                         const float* patch_b, const float* cls, const float* wpe,
+                         int B, int IMG, int P, int C);
+/* ViT replacement of encoder_backward (train_vit.rs:371), (+=), no pixel gradient */
+void patch_embed_backward(float* dpatch_w, float* dpatch_b, float* dcls, float* dwpe,
+                          const float* dencoded, const float* pixels, int B, int IMG, int P,
+                          int C);
+/* optimizer_step (train_vit.rs:737): params -= lr * grads */
+void sgd_step(float* params, const float* grads, long long n, float lr);
+
+/* ------------------------------------------------------------------ bf16 fast path
+ * Build-side extensions with the same conventions; bf16 storage as raw uint16_t, fp32
+ * accumulate; LN statistics, biases, residual stream and gradients stay fp32.           */
+/* out_bf16[BT,OC] = inp . W^T + bias */
+void matmul_forward_bf16(uint16_t* out, const uint16_t* inp, const uint16_t* weight,
+                         const float* bias, int B, int T, int C, int OC);
+/* dinp_f32 += dout . W (NULL skips);  dweight_f32 += dout^T . inp (split-K, atomics) */
+void matmul_backward_bf16(float* dinp, float* dweight, float* dbias, const uint16_t* dout,
+                          const uint16_t* inp, const uint16_t* weight, int B, int T, int C,
+                          int OC);
+/* fused attention: out_bf16 [B,T,C], lse [B,NH,T] (log2 domain), no T x T HBM traffic.
+ * head size must be 64 and T <= 256. */
+void attention_forward_fused_bf16(uint16_t* out, float* lse, const uint16_t* inp,
+                                  int B, int T, int C, int NH);
+/* dinp_bf16 [B,T,3C] is OVERWRITTEN (it is produced whole); recomputes P from lse */
+void attention_backward_fused_bf16(uint16_t* dinp, const uint16_t* dout, const uint16_t* inp,
+                                   const uint16_t* out, const float* lse, int B, int T, int C,
+                                   int NH);
+void layernorm_forward_bf16(uint16_t* out, float* mean, float* rstd, const float* inp,
+                            const float* weight, const float* bias, int B, int T, int C);
+void convert_f32_to_bf16(uint16_t* out, const float* inp, long long n);
+void convert_bf16_to_f32(float* out, const uint16_t* inp, long long n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

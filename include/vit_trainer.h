@@ -1,0 +1,83 @@
+/*
+ * vit_trainer.h — C ABI of the native host trainer in libvit_hip.so.
+ *
+ * Mirrors the reference's model-level interface (/root/reference/train_vit.rs):
+ *   struct ViT + build_from_checkpoint (:65-186)  -> vit_trainer_create + vit_trainer_set_params
+ *   ViT::forward(inputs, targets, B, T) (:188)     -> vit_trainer_set_batch + vit_trainer_forward
+ *   ViT::backward() (:271)                         -> vit_trainer_zero_grad + vit_trainer_backward
+ *   optimizer_step(&mut ViT, lr) (:737)            -> vit_trainer_step
+ *   mean_loss field (:85, :263)                    -> vit_trainer_mean_loss
+ * Parameters cross this boundary in the reference's canonical type-major order (the 16
+ * ParameterTensors of train_vit.rs:10-27 / param_sizes :115-131, with wte -> patch_w, patch_b,
+ * cls and the tied LM head -> head_w, head_b; 20 tensors).  On the device the trainer keeps them
+ * layer-major in reverse layer order so that backward finalises one contiguous gradient range per
+ * layer (the unit of the overlapped RCCL all-reduce).
+ *
+ * Precision modes:
+ *   VIT_FP32 (0): the reference op sequence on the GPU (the fp32 C-ABI ops of vit_ops.h,
+ *                 materialised attention) — the parity path (<= 1e-4 rel vs the CPU oracle).
+ *   VIT_BF16 (1): the fast path — bf16 MFMA GEMMs with fused epilogues, fused attention,
+ *                 fp32 master weights / gradients / residual stream / LN statistics.
+ * All calls are asynchronous on the trainer's stream unless noted; functions returning int
+ * return 0 on success (details via vit_last_error()).
+ */
+#ifndef VIT_TRAINER_H
+#define VIT_TRAINER_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+    int img, patch, in_ch, channels, num_layers, num_heads, num_classes;
+} vit_config_t;
+
+enum { VIT_FP32 = 0, VIT_BF16 = 1 };
+enum { VIT_NUM_PARAM_TENSORS = 20 };
+
+typedef struct vit_trainer vit_trainer_t;
+
+vit_trainer_t* vit_trainer_create(const vit_config_t* cfg, int batch, int precision, int device);
+void vit_trainer_destroy(vit_trainer_t* t);
+long long vit_trainer_num_params(const vit_trainer_t* t);
+/* bytes of device memory held by the trainer */
+long long vit_trainer_device_bytes(const vit_trainer_t* t);
+/* canonical (type-major) fp32 host arrays of vit_trainer_num_params() elements; synchronous */
+int vit_trainer_set_params(vit_trainer_t* t, const float* host_params);
+int vit_trainer_get_params(vit_trainer_t* t, float* host_params);
+int vit_trainer_get_grads(vit_trainer_t* t, float* host_grads);
+/* pixels [batch,3,img,img] fp32, labels [batch] int32 (host); synchronous upload */
+int vit_trainer_set_batch(vit_trainer_t* t, const float* host_pixels, const int* host_labels);
+/* same from device pointers (stream-ordered device copy) */
+int vit_trainer_set_batch_device(vit_trainer_t* t, const float* dev_pixels, const int* dev_labels);
+/* forward; b_global = global batch of the data-parallel job (dloss = 1/b_global, D15) */
+int vit_trainer_forward(vit_trainer_t* t, int b_global);
+int vit_trainer_zero_grad(vit_trainer_t* t);
+int vit_trainer_backward(vit_trainer_t* t);   /* also launches the overlapped all-reduce (DP) */
+int vit_trainer_step(vit_trainer_t* t, float lr); /* waits for the all-reduce, then SGD */
+/* zero_grad + forward + backward + step */
+int vit_trainer_train_step(vit_trainer_t* t, float lr, int b_global);
+/* synchronous readbacks */
+float vit_trainer_mean_loss(vit_trainer_t* t);
+int vit_trainer_get_logits(vit_trainer_t* t, float* host_logits); /* [batch, num_classes] */
+int vit_trainer_sync(vit_trainer_t* t);
+void* vit_trainer_stream(vit_trainer_t* t);
+
+/* ---- data parallelism over RCCL (one process per GPU) ---- */
+int vit_dp_unique_id_size(void);
+int vit_dp_get_unique_id(char* out);   /* rank 0 creates; broadcast the bytes out of band */
+/* chunks: 0 = one all-reduce of the whole gradient arena after backward;
+ *         1 = per-layer chunks on a side stream overlapped with backward (default) */
+int vit_trainer_dp_init(vit_trainer_t* t, int rank, int world, const char* unique_id, int overlap);
+
+/* ---- per-kernel-class timing with HIP events on the trainer's stream ---- */
+int vit_trainer_set_timing(vit_trainer_t* t, int on);
+/* fills up to max entries; returns the number of classes. names point to static strings */
+int vit_trainer_timing(vit_trainer_t* t, const char** names, double* total_ms, long long* calls,
+                       double* flops, int max);
+void vit_trainer_timing_reset(vit_trainer_t* t);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,136 @@
+"""Model-level GPU parity: the native trainer (C ABI) vs the CPU oracle / golden fixtures.
+
+fp32 mode runs the reference op sequence on the GPU: logits, loss and every per-parameter
+gradient within 1e-4 relative (max-normalised per tensor) of the fp32 CPU oracle — the
+north-star parity bar.  bf16 mode (the benchmarked fast path) is reported against the same
+oracle with a bf16 tolerance (loss 1e-2, logits/grads 5e-2 per tensor).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, rel_err
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def oracle_step(oc, o, cfg, params, px, lab, b_global=None):
+    c = oc.VitConfig(cfg.img, cfg.patch, cfg.in_ch, cfg.channels, cfg.num_layers, cfg.num_heads,
+                     cfg.num_classes)
+    m = oc.RefViT(o, c, px.shape[0])
+    p = o.arr(params)
+    loss = m.forward(p, px, lab, b_global)
+    g = np.zeros_like(p)
+    m.backward(p, g)
+    return loss, m.logits(), g
+
+
+def per_tensor_errs(cfg, g, r):
+    return {n: rel_err(a, b) for n, a, b in zip(cfg.split(g).keys(), cfg.split(g).values(), cfg.split(r).values())}
+
+
+@pytest.mark.parametrize("name", ["test", "test_t10"])
+def test_fp32_trainer_matches_golden(gpu, name):
+    v = gpu
+    cfg = v.data.CONFIGS[name]
+    z = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    m = v.ViT.build(cfg, z["pixels"].shape[0], v.VIT_FP32, params=z["params"])
+    loss = m.forward(z["pixels"], z["labels"])
+    m.zero_grad()
+    m.forward(z["pixels"], z["labels"])
+    m.backward()
+    g = m.grads()
+    assert abs(loss - float(z["loss"])) <= 1e-4 * abs(float(z["loss"]))
+    assert rel_err(m.logits(), z["logits"]) <= 1e-4
+    errs = per_tensor_errs(cfg, g, z["grads"])
+    assert max(errs.values()) <= 1e-4, errs
+    m.close()
+
+
+@pytest.mark.parametrize("name,B", [("vit_tiny16", 2), ("test", 5)])
+def test_fp32_trainer_matches_oracle(gpu, oracle32, name, B):
+    """ViT-Tiny/16 224x224 (BASELINE config 1 shapes, T=197) through the reference op sequence."""
+    import oracle_ctypes as oc
+    v = gpu
+    cfg = v.data.CONFIGS[name]
+    params = v.data.init_params(cfg, "parity", seed=3)
+    px, lab = v.data.synthetic_batch(cfg, B, seed=5)
+    loss_r, logits_r, g_r = oracle_step(oc, oracle32, cfg, params, px, lab)
+    m = v.ViT.build(cfg, B, v.VIT_FP32, params=params)
+    m.zero_grad()
+    loss = m.forward(px, lab)
+    m.backward()
+    g = m.grads()
+    assert abs(loss - loss_r) <= 1e-4 * abs(loss_r)
+    assert rel_err(m.logits(), logits_r) <= 1e-4
+    errs = per_tensor_errs(cfg, g, g_r)
+    assert max(errs.values()) <= 1e-4, errs
+    # optimizer_step (train_vit.rs:737): p -= lr*g, bit-exact elementwise
+    m.optimizer_step(0.01)
+    p_new = m.params()
+    assert np.array_equal(p_new, (params - np.float32(0.01) * g).astype(np.float32))
+    m.close()
+
+
+@pytest.mark.parametrize("name,B", [("test_h64", 4), ("vit_tiny16", 2)])
+def test_bf16_trainer_vs_oracle(gpu, oracle32, name, B):
+    import oracle_ctypes as oc
+    v = gpu
+    cfg = v.data.CONFIGS[name]
+    params = v.data.init_params(cfg, "parity", seed=3)
+    px, lab = v.data.synthetic_batch(cfg, B, seed=5)
+    loss_r, logits_r, g_r = oracle_step(oc, oracle32, cfg, params, px, lab)
+    m = v.ViT.build(cfg, B, v.VIT_BF16, params=params)
+    m.zero_grad()
+    loss = m.forward(px, lab)
+    m.backward()
+    g = m.grads()
+    assert abs(loss - loss_r) <= 1e-2 * abs(loss_r)
+    assert rel_err(m.logits(), logits_r) <= 5e-2
+    errs = per_tensor_errs(cfg, g, g_r)
+    assert max(errs.values()) <= 5e-2, errs
+    m.close()
+
+
+def test_training_reduces_loss(gpu):
+    v = gpu
+    cfg = v.data.CONFIGS["test_h64"]
+    params = v.data.init_params(cfg, "parity", seed=1)
+    px, lab = v.data.synthetic_batch(cfg, 8, seed=2)
+    for prec in (v.VIT_FP32, v.VIT_BF16):
+        m = v.ViT.build(cfg, 8, prec, params=params)
+        m.set_batch(px, lab)
+        losses = []
+        for _ in range(40):
+            m.train_step(0.5)
+            losses.append(float(v.lib().vit_trainer_mean_loss(m.h)))
+        assert losses[-1] < 0.6 * losses[0], (prec, losses[0], losses[-1])
+        m.close()
+
+
+def test_vit_b16_full_size_step(gpu):
+    """BASELINE config 2 shapes (ViT-B/16, 224^2, B=256, bf16): size-independent properties of one
+    full-size step — finite loss near ln(1000) at init, finite grads, loss drops on a repeat."""
+    v = gpu
+    cfg = v.data.CONFIGS["vit_b16"]
+    B = 256
+    params = v.data.init_params(cfg, "parity", seed=1)
+    px, lab = v.data.synthetic_batch(cfg, B, seed=2)
+    m = v.ViT.build(cfg, B, v.VIT_BF16, params=params)
+    m.set_batch(px, lab)
+    m.zero_grad()
+    loss0 = m.forward()
+    assert np.isfinite(loss0) and abs(loss0 - np.log(1000)) < 1.5
+    m.backward()
+    g = m.grads()
+    assert np.all(np.isfinite(g))
+    gs = cfg.split(g)
+    for n in ("patch_w", "qkvw", "fcw", "head_w", "wpe"):
+        assert np.abs(gs[n]).max() > 0, n
+    m.optimizer_step(0.05)
+    m.zero_grad()
+    loss1 = m.forward()
+    assert loss1 < loss0
+    m.close()

@@ -1,0 +1,281 @@
+"""GPU parity of every C-ABI op against the CPU oracle (same seeded inputs), through the C ABI.
+
+fp32 ops: <= 1e-4 relative to the oracle's fp32 result (max-normalised), the parity bar of
+BASELINE.json.  bf16 ops: compared with the fp64 oracle run on the bf16-ROUNDED inputs, so only
+accumulation order / output rounding differ; tolerance 1e-2 (bf16 output rounding is 2^-9).
+"""
+import numpy as np
+import pytest
+
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def D(vit, a, dtype=np.float32):
+    return vit.DeviceArray.from_numpy(np.ascontiguousarray(a, dtype=dtype))
+
+
+def Z(vit, n, dtype=np.float32):
+    return vit.DeviceArray.zeros(n, dtype)
+
+
+# ------------------------------------------------------------------ fp32 reference ops
+def test_kats_on_gpu(gpu):
+    v = gpu
+    out = Z(v, 10)
+    v.call("residual_forward", out, D(v, np.ones(10)), D(v, np.full(10, 2.0)), 10)
+    assert np.array_equal(out.numpy(), np.full(10, 3.0, np.float32))
+    B, T, C, OC = 2, 3, 4, 5
+    out = Z(v, B * T * OC)
+    v.call("matmul_forward", out, D(v, np.ones(B * T * C)), D(v, np.full(OC * C, 2.0)),
+           D(v, np.full(OC, 3.0)), B, T, C, OC)
+    assert np.array_equal(out.numpy(), np.full(B * T * OC, 11.0, np.float32))
+    B, T, C, NH = 2, 3, 4, 2
+    out, pre, att = Z(v, B * T * C), Z(v, B * T * NH * T), Z(v, B * T * NH * T)
+    v.call("attention_forward", out, pre, att, D(v, np.ones(B * T * 3 * C)), B, T, C, NH)
+    assert np.allclose(out.numpy(), 1.0, atol=1e-6)
+    out, m, r = Z(v, 24), Z(v, 6), Z(v, 6)
+    v.call("layernorm_forward", out, m, r, D(v, np.ones(24)), D(v, np.full(4, 2.0)), D(v, np.full(4, 3.0)), 2, 3, 4)
+    assert np.allclose(out.numpy(), 3.0) and np.allclose(m.numpy(), 1.0)
+    assert np.allclose(r.numpy(), 1 / np.sqrt(np.float32(1e-5)), rtol=1e-5)
+    g = Z(v, 10)
+    v.call("gelu_forward", g, D(v, np.ones(10)), 10)
+    assert np.allclose(g.numpy(), 0.841192, atol=2e-6)
+    p = Z(v, 24)
+    v.call("softmax_forward", p, D(v, np.ones(24)), 2, 3, 4)
+    assert np.allclose(p.numpy(), 0.25)
+
+
+@pytest.mark.parametrize("B,T,C,OC", [(2, 3, 4, 5), (3, 17, 32, 96), (2, 197, 192, 576), (1, 50, 100, 37)])
+def test_matmul_fp32(gpu, oracle32, B, T, C, OC):
+    v, o = gpu, oracle32
+    rng = np.random.default_rng(B * 1000 + T)
+    inp, w, b = o.arr(rng.normal(size=B * T * C)), o.arr(rng.normal(size=OC * C) * 0.1), o.arr(rng.normal(size=OC))
+    dout = o.arr(rng.normal(size=B * T * OC))
+    ref = o.arr(np.zeros(B * T * OC))
+    o.call("matmul_forward", ref, inp, w, b, B, T, C, OC)
+    out = Z(v, B * T * OC)
+    v.call("matmul_forward", out, D(v, inp), D(v, w), D(v, b), B, T, C, OC)
+    assert rel_err(out.numpy(), ref) < 1e-5
+    # backward accumulates (+=) into pre-filled buffers
+    pre_i, pre_w, pre_b = rng.normal(size=B * T * C), rng.normal(size=OC * C), rng.normal(size=OC)
+    ri, rw, rb = o.arr(pre_i), o.arr(pre_w), o.arr(pre_b)
+    o.call("matmul_backward", ri, rw, rb, dout, inp, w, B, T, C, OC)
+    gi, gw, gb = D(v, pre_i), D(v, pre_w), D(v, pre_b)
+    v.call("matmul_backward", gi, gw, gb, D(v, dout), D(v, inp), D(v, w), B, T, C, OC)
+    assert rel_err(gi.numpy(), ri) < 1e-5
+    assert rel_err(gw.numpy(), rw) < 1e-5
+    assert rel_err(gb.numpy(), rb) < 1e-5
+
+
+def test_matmul_fp32_null_bias_and_dinp(gpu, oracle32):
+    v, o = gpu, oracle32
+    rng = np.random.default_rng(9)
+    B, T, C, OC = 2, 5, 8, 6
+    inp, w = o.arr(rng.normal(size=B * T * C)), o.arr(rng.normal(size=OC * C))
+    ref = o.arr(np.zeros(B * T * OC))
+    o.call("matmul_forward", ref, inp, w, None, B, T, C, OC)
+    out = Z(v, B * T * OC)
+    v.call("matmul_forward", out, D(v, inp), D(v, w), None, B, T, C, OC)
+    assert rel_err(out.numpy(), ref) < 1e-6
+    dout = o.arr(rng.normal(size=B * T * OC))
+    rw = o.arr(np.zeros(OC * C))
+    o.call("matmul_backward", None, rw, None, dout, inp, w, B, T, C, OC)
+    gw = Z(v, OC * C)
+    v.call("matmul_backward", None, gw, None, D(v, dout), D(v, inp), D(v, w), B, T, C, OC)
+    assert rel_err(gw.numpy(), rw) < 1e-6
+
+
+@pytest.mark.parametrize("B,T,C,NH", [(2, 3, 4, 2), (2, 17, 32, 2), (2, 197, 192, 3), (1, 1, 64, 1), (1, 300, 64, 4)])
+def test_attention_fp32(gpu, oracle32, B, T, C, NH):
+    v, o = gpu, oracle32
+    rng = np.random.default_rng(T)
+    inp = o.arr(rng.normal(size=B * T * 3 * C))
+    n = B * T * NH * T
+    out, pre, att = o.arr(np.zeros(B * T * C)), o.arr(np.zeros(n)), o.arr(np.zeros(n))
+    o.call("attention_forward", out, pre, att, inp, B, T, C, NH)
+    gout, gpre, gatt = Z(v, B * T * C), Z(v, n), Z(v, n)
+    gi = D(v, inp)
+    v.call("attention_forward", gout, gpre, gatt, gi, B, T, C, NH)
+    assert rel_err(gout.numpy(), out) < 1e-5
+    assert rel_err(gpre.numpy(), pre) < 1e-5
+    assert rel_err(gatt.numpy(), att) < 1e-5
+    dout = o.arr(rng.normal(size=B * T * C))
+    pre_d = rng.normal(size=B * T * 3 * C)
+    dinp, dpre, datt = o.arr(pre_d), o.arr(np.zeros(n)), o.arr(np.zeros(n))
+    o.call("attention_backward", dinp, dpre, datt, dout, inp, att, B, T, C, NH)
+    gd, gdp, gda = D(v, pre_d), Z(v, n), Z(v, n)
+    v.call("attention_backward", gd, gdp, gda, D(v, dout), gi, gatt, B, T, C, NH)
+    assert rel_err(gd.numpy(), dinp) < 1e-4
+    assert rel_err(gdp.numpy(), dpre) < 1e-4
+    assert rel_err(gda.numpy(), datt) < 1e-5
+    # NULL scratch (internal workspace) gives the same input gradient
+    gd2 = D(v, pre_d)
+    v.call("attention_backward", gd2, None, None, D(v, dout), gi, gatt, B, T, C, NH)
+    assert rel_err(gd2.numpy(), dinp) < 1e-4
+
+
+@pytest.mark.parametrize("rows,C", [(6, 4), (394, 192), (100, 768), (7, 1000)])
+def test_layernorm_fp32(gpu, oracle32, rows, C):
+    v, o = gpu, oracle32
+    rng = np.random.default_rng(C)
+    x, w, b = o.arr(rng.normal(size=rows * C) * 3 + 1), o.arr(rng.normal(size=C)), o.arr(rng.normal(size=C))
+    out, m, r = o.arr(np.zeros(rows * C)), o.arr(np.zeros(rows)), o.arr(np.zeros(rows))
+    o.call("layernorm_forward", out, m, r, x, w, b, rows, 1, C)
+    go, gm, gr = Z(v, rows * C), Z(v, rows), Z(v, rows)
+    v.call("layernorm_forward", go, gm, gr, D(v, x), D(v, w), D(v, b), rows, 1, C)
+    assert rel_err(go.numpy(), out) < 1e-5 and rel_err(gm.numpy(), m) < 1e-5 and rel_err(gr.numpy(), r) < 1e-5
+    dy = o.arr(rng.normal(size=rows * C))
+    p0 = rng.normal(size=rows * C)
+    di, dw, db = o.arr(p0), o.arr(np.ones(C)), o.arr(np.zeros(C))
+    o.call("layernorm_backward", di, dw, db, dy, x, w, m, r, rows, 1, C)
+    gdi, gdw, gdb = D(v, p0), D(v, np.ones(C)), Z(v, C)
+    v.call("layernorm_backward", gdi, gdw, gdb, D(v, dy), D(v, x), D(v, w), gm, gr, rows, 1, C)
+    assert rel_err(gdi.numpy(), di) < 1e-4 and rel_err(gdw.numpy(), dw) < 1e-5 and rel_err(gdb.numpy(), db) < 1e-5
+
+
+def test_elementwise_fp32(gpu, oracle32):
+    v, o = gpu, oracle32
+    rng = np.random.default_rng(11)
+    n = 100003
+    x, y, g = o.arr(rng.normal(size=n) * 3), o.arr(rng.normal(size=n)), o.arr(rng.normal(size=n))
+    ref = o.arr(np.zeros(n))
+    o.call("gelu_forward", ref, x, n)
+    out = Z(v, n)
+    v.call("gelu_forward", out, D(v, x), n)
+    assert rel_err(out.numpy(), ref) < 1e-6
+    p0 = rng.normal(size=n)
+    ref = o.arr(p0)
+    o.call("gelu_backward", ref, x, g, n)
+    out = D(v, p0)
+    v.call("gelu_backward", out, D(v, x), D(v, g), n)
+    assert rel_err(out.numpy(), ref) < 1e-5
+    a1, a2 = o.arr(p0), o.arr(-p0)
+    o.call("residual_backward", a1, a2, g, n)
+    b1, b2 = D(v, p0), D(v, -p0)
+    v.call("residual_backward", b1, b2, D(v, g), n)
+    assert np.array_equal(b1.numpy(), a1) and np.array_equal(b2.numpy(), a2)
+    ref = o.arr(np.zeros(n))
+    o.call("residual_forward", ref, x, y, n)
+    out = Z(v, n)
+    v.call("residual_forward", out, D(v, x), D(v, y), n)
+    assert np.array_equal(out.numpy(), ref)
+    pp = o.arr(p0)
+    o.sgd_step(pp, g, 0.01)
+    gp = D(v, p0)
+    v.call("sgd_step", gp, D(v, g), n, 0.01)
+    assert np.array_equal(gp.numpy(), pp)
+
+
+@pytest.mark.parametrize("rows,V", [(5, 10), (256, 1000), (3, 4)])
+def test_softmax_ce_fp32(gpu, oracle32, rows, V):
+    v, o = gpu, oracle32
+    rng = np.random.default_rng(V)
+    logits = o.arr(rng.normal(size=rows * V) * 4)
+    tgt = rng.integers(0, V, size=rows).astype(np.int32)
+    probs, losses = o.arr(np.zeros(rows * V)), o.arr(np.zeros(rows))
+    o.call("softmax_forward", probs, logits, rows, 1, V)
+    o.call("crossentropy_forward", losses, probs, tgt, rows, 1, V)
+    gp, gl = Z(v, rows * V), Z(v, rows)
+    gt = D(v, tgt, np.int32)
+    v.call("softmax_forward", gp, D(v, logits), rows, 1, V)
+    v.call("crossentropy_forward", gl, gp, gt, rows, 1, V)
+    assert rel_err(gp.numpy(), probs) < 1e-5 and rel_err(gl.numpy(), losses) < 1e-5
+    dl = o.arr(np.full(rows, 1.0 / rows))
+    p0 = rng.normal(size=rows * V)
+    ref = o.arr(p0)
+    o.call("crossentropy_softmax_backward", ref, dl, probs, tgt, rows, 1, V)
+    out = D(v, p0)
+    v.call("crossentropy_softmax_backward", out, D(v, dl), gp, gt, rows, 1, V)
+    assert rel_err(out.numpy(), ref) < 1e-6
+
+
+@pytest.mark.parametrize("B,IMG,P,C", [(2, 32, 8, 32), (3, 48, 16, 64), (2, 224, 16, 192)])
+def test_patch_embed_fp32(gpu, oracle32, B, IMG, P, C):
+    v, o = gpu, oracle32
+    rng = np.random.default_rng(IMG)
+    NP, K = (IMG // P) ** 2, 3 * P * P
+    T = NP + 1
+    px = o.arr(rng.normal(size=B * 3 * IMG * IMG))
+    w, b, cls, wpe = (o.arr(rng.normal(size=s) * 0.05) for s in (C * K, C, C, T * C))
+    enc = o.arr(np.zeros(B * T * C))
+    o.call("patch_embed_forward", enc, px, w, b, cls, wpe, B, IMG, P, C)
+    genc = Z(v, B * T * C)
+    gpx = D(v, px)
+    v.call("patch_embed_forward", genc, gpx, D(v, w), D(v, b), D(v, cls), D(v, wpe), B, IMG, P, C)
+    assert rel_err(genc.numpy(), enc) < 1e-5
+    denc = o.arr(rng.normal(size=B * T * C))
+    dw, db, dc, dp = (o.arr(np.zeros(s)) for s in (C * K, C, C, T * C))
+    o.call("patch_embed_backward", dw, db, dc, dp, denc, px, B, IMG, P, C)
+    gdw, gdb, gdc, gdp = (Z(v, s) for s in (C * K, C, C, T * C))
+    v.call("patch_embed_backward", gdw, gdb, gdc, gdp, D(v, denc), gpx, B, IMG, P, C)
+    for g, r in ((gdw, dw), (gdb, db), (gdc, dc), (gdp, dp)):
+        assert rel_err(g.numpy(), r) < 1e-5
+
+
+# ------------------------------------------------------------------ bf16 MFMA GEMM layouts
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (300, 200, 72), (1576, 576, 192), (50432 // 8, 768, 768), (64, 1000, 16)])
+def test_matmul_bf16(gpu, oracle64, M, N, K):
+    """forward (K-contig x K-contig), dgrad (K x N-contig) and split-K wgrad (M x N-contig)."""
+    v = gpu
+    rng = np.random.default_rng(M + N + K)
+    x = rng.normal(size=(M, K)).astype(np.float32)
+    w = (rng.normal(size=(N, K)) * 0.05).astype(np.float32)
+    b = rng.normal(size=N).astype(np.float32)
+    dy = rng.normal(size=(M, N)).astype(np.float32)
+    xb, wb, dyb = v.bf16_bits(x), v.bf16_bits(w), v.bf16_bits(dy)
+    xr, wr, dyr = (v.bf16_to_f32(a).astype(np.float64).reshape(s) for a, s in ((xb, (M, K)), (wb, (N, K)), (dyb, (M, N))))
+    out = Z(v, M * N, np.uint16)
+    v.call("matmul_forward_bf16", out, D(v, xb, np.uint16), D(v, wb, np.uint16), D(v, b), 1, M, K, N)
+    ref = xr @ wr.T + b
+    assert rel_err(v.bf16_to_f32(out.numpy()).reshape(M, N), ref) < 1e-2
+    p_in, p_w, p_b = rng.normal(size=M * K), rng.normal(size=N * K), rng.normal(size=N)
+    gi, gw, gb = D(v, p_in), D(v, p_w), D(v, p_b)
+    v.call("matmul_backward_bf16", gi, gw, gb, D(v, dyb, np.uint16), D(v, xb, np.uint16), D(v, wb, np.uint16), 1, M, K, N)
+    assert rel_err(gi.numpy().reshape(M, K), p_in.reshape(M, K) + dyr @ wr) < 2e-3
+    assert rel_err(gw.numpy().reshape(N, K), p_w.reshape(N, K) + dyr.T @ xr) < 2e-3
+    assert rel_err(gb.numpy(), p_b + dyr.sum(0)) < 2e-3
+
+
+# ------------------------------------------------------------------ fused bf16 attention
+@pytest.mark.parametrize("B,T,NH", [(2, 197, 3), (1, 1, 1), (2, 17, 2), (1, 64, 2), (1, 256, 1), (3, 33, 4)])
+def test_attention_fused_bf16(gpu, oracle64, B, T, NH):
+    v, o = gpu, oracle64
+    C = 64 * NH
+    rng = np.random.default_rng(T * 7 + NH)
+    qkv = rng.normal(size=B * T * 3 * C).astype(np.float32)
+    qb = v.bf16_bits(qkv)
+    qr = v.bf16_to_f32(qb).astype(np.float64)
+    n = B * T * NH * T
+    out, pre, att = np.zeros(B * T * C), np.zeros(n), np.zeros(n)
+    o.call("attention_forward", out, pre, att, qr, B, T, C, NH)
+    gq = D(v, qb, np.uint16)
+    gout, glse = Z(v, B * T * C, np.uint16), Z(v, B * NH * T)
+    v.call("attention_forward_fused_bf16", gout, glse, gq, B, T, C, NH)
+    o_gpu = v.bf16_to_f32(gout.numpy())
+    assert rel_err(o_gpu, out) < 1e-2
+    # lse (log2 domain) = log2(sum exp(score)) per (b,h,t)
+    s = pre.reshape(B, T, NH, T).transpose(0, 2, 1, 3)
+    lse_ref = np.log2(np.exp(s).sum(-1))
+    assert np.abs(glse.numpy().reshape(B, NH, T) - lse_ref).max() < 1e-2
+    # backward vs the oracle run on the same bf16-rounded inputs (the O fed to delta is the GPU's)
+    dy = rng.normal(size=B * T * C).astype(np.float32)
+    dyb = v.bf16_bits(dy)
+    dyr = v.bf16_to_f32(dyb).astype(np.float64)
+    dinp = np.zeros(B * T * 3 * C)
+    o.call("attention_backward", dinp, np.zeros(n), np.zeros(n), dyr, qr, att, B, T, C, NH)
+    gd = Z(v, B * T * 3 * C, np.uint16)
+    v.call("attention_backward_fused_bf16", gd, D(v, dyb, np.uint16), gq, gout, glse, B, T, C, NH)
+    g = v.bf16_to_f32(gd.numpy()).reshape(B, T, 3, C)
+    r = dinp.reshape(B, T, 3, C)
+    for k, name in enumerate("qkv"):
+        assert rel_err(g[:, :, k], r[:, :, k]) < 3e-2, name
+
+
+def test_error_channel(gpu):
+    """Unsupported shapes set the sticky error instead of launching (no silent fallback)."""
+    v = gpu
+    out = Z(v, 64, np.uint16)
+    with pytest.raises(v.VitError):
+        v.call("attention_forward_fused_bf16", out, Z(v, 64), Z(v, 3 * 64, np.uint16), 1, 1, 80, 1)

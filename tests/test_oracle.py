@@ -1,0 +1,261 @@
+"""CPU oracle pinning (no GPU): the reference's own known-answer tests, fp64 central finite
+differences of every backward op, and the committed torch-fp64 golden fixtures."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, rel_err
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+# ------------------------------------------------ reference KATs (tests/vit_tests.rs, D14-fixed)
+def test_kat_residual_forward(oracle32):
+    # vit_tests.rs:92-101 — 1 + 2 == 3
+    o = oracle32
+    a, b, out = o.arr(np.ones(10)), o.arr(np.full(10, 2.0)), o.arr(np.zeros(10))
+    o.call("residual_forward", out, a, b, 10)
+    assert np.array_equal(out, np.full(10, 3.0, np.float32))
+
+
+def test_kat_matmul_forward(oracle32):
+    # vit_tests.rs:104-132: inp=1, W=2, b=3, C=4 -> 3 + 4*1*2 = 11 (the test's 35.0 is wrong, D14)
+    o = oracle32
+    B, T, C, OC = 2, 3, 4, 5
+    inp, w, b = o.arr(np.ones(B * T * C)), o.arr(np.full(OC * C, 2.0)), o.arr(np.full(OC, 3.0))
+    out = o.arr(np.zeros(B * T * OC))
+    o.call("matmul_forward", out, inp, w, b, B, T, C, OC)
+    assert np.array_equal(out, np.full(B * T * OC, 11.0, np.float32))
+
+
+def test_kat_attention_forward_all_ones(oracle32):
+    # vit_tests.rs:135-160: all-ones input -> every output is a convex combination of ones = 1.0
+    o = oracle32
+    B, T, C, NH = 2, 3, 4, 2
+    inp = o.arr(np.ones(B * T * 3 * C))
+    out, pre, att = o.arr(np.zeros(B * T * C)), o.arr(np.zeros(B * NH * T * T)), o.arr(np.zeros(B * NH * T * T))
+    o.call("attention_forward", out, pre, att, inp, B, T, C, NH)
+    assert np.allclose(out, 1.0, atol=1e-6)
+    assert np.allclose(att, 1.0 / T, atol=1e-7)
+    assert np.allclose(pre, 2.0 / np.sqrt(2.0), atol=1e-6)  # q.k / sqrt(hs), hs = 2
+
+
+def test_kat_attention_causal_loop_structure(oracle32):
+    # D3: the reference's 0..=t loop (causal) — row t normalises over t+1 keys
+    o = oracle32
+    B, T, C, NH = 1, 3, 4, 2
+    inp = o.arr(np.ones(B * T * 3 * C))
+    out, pre, att = o.arr(np.zeros(B * T * C)), o.arr(np.zeros(B * NH * T * T)), o.arr(np.zeros(B * NH * T * T))
+    o.call("attention_forward_causal", out, pre, att, inp, B, T, C, NH)
+    a = att.reshape(B, T, NH, T)
+    for t in range(T):
+        assert np.allclose(a[0, t, :, : t + 1], 1.0 / (t + 1), atol=1e-7)
+        assert np.all(a[0, t, :, t + 1:] == 0)
+    assert np.allclose(out, 1.0, atol=1e-6)
+
+
+def test_kat_layernorm_forward(oracle32):
+    # vit_tests.rs:163-190: inp=1, w=2, b=3 -> out=3, mean=1, rstd=1/sqrt(1e-5)
+    o = oracle32
+    B, T, C = 2, 3, 4
+    out, mean, rstd = o.arr(np.zeros(B * T * C)), o.arr(np.zeros(B * T)), o.arr(np.zeros(B * T))
+    o.call("layernorm_forward", out, mean, rstd, o.arr(np.ones(B * T * C)), o.arr(np.full(C, 2.0)),
+           o.arr(np.full(C, 3.0)), B, T, C)
+    assert np.allclose(out, 3.0) and np.allclose(mean, 1.0)
+    assert np.allclose(rstd, np.float32(1.0) / np.sqrt(np.float32(1e-5)), rtol=1e-6)
+
+
+def test_kat_gelu_forward(oracle32):
+    # vit_tests.rs:193-201: gelu(1) (tanh approximation) = 0.841192
+    o = oracle32
+    out = o.arr(np.zeros(10))
+    o.call("gelu_forward", out, o.arr(np.ones(10)), 10)
+    assert np.allclose(out, 0.841192, atol=2e-6)
+
+
+def test_kat_softmax_forward(oracle32):
+    # vit_tests.rs:204-230: uniform logits -> 0.25 each, rows sum to 1
+    o = oracle32
+    B, T, V = 2, 3, 4
+    probs = o.arr(np.zeros(B * T * V))
+    o.call("softmax_forward", probs, o.arr(np.ones(B * T * V)), B, T, V)
+    assert np.allclose(probs, 0.25) and np.allclose(probs.reshape(-1, V).sum(1), 1.0, atol=1e-6)
+
+
+def test_crossentropy_is_negative_log(oracle32):
+    # D6: loss = -log p[target] (the reference wrote -p)
+    o = oracle32
+    probs = o.arr(np.array([0.1, 0.2, 0.7, 0.25, 0.25, 0.5]))
+    losses = o.arr(np.zeros(2))
+    o.call("crossentropy_forward", losses, probs, np.array([2, 0], np.int32), 2, 1, 3)
+    assert np.allclose(losses, [-np.log(0.7), -np.log(0.25)], rtol=1e-6)
+
+
+# ------------------------------------------------ fp64 central finite differences
+def _fd_check(o, f_loss, x, analytic, n_probe=12, eps=1e-6, seed=0):
+    rng = np.random.default_rng(seed)
+    idx = rng.choice(x.size, size=min(n_probe, x.size), replace=False)
+    for i in idx:
+        old = x.flat[i]
+        x.flat[i] = old + eps
+        lp = f_loss()
+        x.flat[i] = old - eps
+        lm = f_loss()
+        x.flat[i] = old
+        fd = (lp - lm) / (2 * eps)
+        assert abs(fd - analytic.flat[i]) <= 1e-6 * max(1.0, abs(fd)), (i, fd, analytic.flat[i])
+
+
+def test_fd_matmul_backward(oracle64):
+    o, rng = oracle64, np.random.default_rng(1)
+    B, T, C, OC = 2, 3, 5, 4
+    inp, w, b = rng.normal(size=B * T * C), rng.normal(size=OC * C), rng.normal(size=OC)
+    g = rng.normal(size=B * T * OC)
+
+    def loss():
+        out = np.zeros(B * T * OC)
+        o.call("matmul_forward", out, inp, w, b, B, T, C, OC)
+        return float(out @ g)
+
+    dinp, dw, db = np.zeros_like(inp), np.zeros_like(w), np.zeros_like(b)
+    o.call("matmul_backward", dinp, dw, db, g, inp, w, B, T, C, OC)
+    for x, a in ((inp, dinp), (w, dw), (b, db)):
+        _fd_check(o, loss, x, a)
+
+
+@pytest.mark.parametrize("T", [1, 4, 7])
+def test_fd_attention_backward(oracle64, T):
+    o, rng = oracle64, np.random.default_rng(2)
+    B, C, NH = 2, 8, 2
+    inp = rng.normal(size=B * T * 3 * C)
+    g = rng.normal(size=B * T * C)
+
+    def loss():
+        out, pre, att = np.zeros(B * T * C), np.zeros(B * T * NH * T), np.zeros(B * T * NH * T)
+        o.call("attention_forward", out, pre, att, inp, B, T, C, NH)
+        return float(out @ g)
+
+    out, pre, att = np.zeros(B * T * C), np.zeros(B * T * NH * T), np.zeros(B * T * NH * T)
+    o.call("attention_forward", out, pre, att, inp, B, T, C, NH)
+    dinp = np.zeros_like(inp)
+    o.call("attention_backward", dinp, np.zeros_like(pre), np.zeros_like(att), g, inp, att, B, T, C, NH)
+    _fd_check(o, loss, inp, dinp, n_probe=24)
+
+
+def test_fd_layernorm_backward(oracle64):
+    o, rng = oracle64, np.random.default_rng(3)
+    B, T, C = 2, 3, 6
+    inp, w, b = rng.normal(size=B * T * C), rng.normal(size=C), rng.normal(size=C)
+    g = rng.normal(size=B * T * C)
+
+    def fwd():
+        out, m, r = np.zeros(B * T * C), np.zeros(B * T), np.zeros(B * T)
+        o.call("layernorm_forward", out, m, r, inp, w, b, B, T, C)
+        return out, m, r
+
+    loss = lambda: float(fwd()[0] @ g)
+    _, m, r = fwd()
+    dinp, dw, db = np.zeros_like(inp), np.zeros_like(w), np.zeros_like(b)
+    o.call("layernorm_backward", dinp, dw, db, g, inp, w, m, r, B, T, C)
+    for x, a in ((inp, dinp), (w, dw), (b, db)):
+        _fd_check(o, loss, x, a)
+
+
+def test_fd_gelu_backward(oracle64):
+    # D4: the reference's cosh(2a) derivative fails this check; the fixed one passes
+    o = oracle64
+    x = np.linspace(-4, 4, 33)
+    g = np.linspace(0.5, 1.5, 33)
+    loss = lambda: float(_gelu(o, x) @ g)
+    d = np.zeros_like(x)
+    o.call("gelu_backward", d, x, g, x.size)
+    _fd_check(o, loss, x, d, n_probe=33)
+
+
+def _gelu(o, x):
+    out = np.zeros_like(x)
+    o.call("gelu_forward", out, x, x.size)
+    return out
+
+
+def test_fd_crossentropy_softmax_backward(oracle64):
+    o, rng = oracle64, np.random.default_rng(4)
+    B, V = 3, 7
+    logits = rng.normal(size=B * V)
+    tgt = np.array([1, 6, 0], np.int32)
+    dl = np.full(B, 1.0 / B)
+
+    def loss():
+        p, l = np.zeros(B * V), np.zeros(B)
+        o.call("softmax_forward", p, logits, B, 1, V)
+        o.call("crossentropy_forward", l, p, tgt, B, 1, V)
+        return float(l.mean())
+
+    p = np.zeros(B * V)
+    o.call("softmax_forward", p, logits, B, 1, V)
+    d = np.zeros(B * V)
+    o.call("crossentropy_softmax_backward", d, dl, p, tgt, B, 1, V)
+    _fd_check(o, loss, logits, d, n_probe=B * V)
+
+
+def test_fd_patch_embed_backward(oracle64):
+    o, rng = oracle64, np.random.default_rng(5)
+    B, IMG, P, C = 2, 8, 4, 3
+    NP, K = (IMG // P) ** 2, 3 * P * P
+    T = NP + 1
+    px = rng.normal(size=B * 3 * IMG * IMG)
+    w, b, cls, wpe = rng.normal(size=C * K), rng.normal(size=C), rng.normal(size=C), rng.normal(size=T * C)
+    g = rng.normal(size=B * T * C)
+
+    def loss():
+        enc = np.zeros(B * T * C)
+        o.call("patch_embed_forward", enc, px, w, b, cls, wpe, B, IMG, P, C)
+        return float(enc @ g)
+
+    dw, db, dc, dp = np.zeros_like(w), np.zeros_like(b), np.zeros_like(cls), np.zeros_like(wpe)
+    o.call("patch_embed_backward", dw, db, dc, dp, g, px, B, IMG, P, C)
+    for x, a in ((w, dw), (b, db), (cls, dc), (wpe, dp)):
+        _fd_check(o, loss, x, a)
+
+
+# ------------------------------------------------ golden fixtures (torch fp64 autograd)
+def _cfg_c(oc, cfg):
+    return oc.VitConfig(cfg.img, cfg.patch, cfg.in_ch, cfg.channels, cfg.num_layers,
+                        cfg.num_heads, cfg.num_classes)
+
+
+@pytest.mark.parametrize("name", ["test", "test_t10"])
+@pytest.mark.parametrize("prec,tol", [("f64", 1e-10), ("f32", 1e-4)])
+def test_oracle_matches_golden(vit, name, prec, tol):
+    import oracle_ctypes as oc
+    o = oc.Oracle(prec)
+    cfg = vit.data.CONFIGS[name]
+    z = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    m = oc.RefViT(o, _cfg_c(oc, cfg), z["pixels"].shape[0])
+    p = o.arr(z["params"])
+    loss = m.forward(p, z["pixels"], z["labels"])
+    g = np.zeros_like(p)
+    m.backward(p, g)
+    assert abs(loss - float(z["loss"])) <= tol * abs(float(z["loss"]))
+    assert rel_err(m.logits(), z["logits"]) <= tol
+    assert rel_err(g, z["grads"]) <= tol
+    # per tensor, too
+    for n, gv, gz in zip(vit.data.PARAM_NAMES, cfg.split(g).values(), cfg.split(z["grads"]).values()):
+        assert rel_err(gv, gz) <= 10 * tol, n
+
+
+def test_golden_fixture_inputs_are_reproducible(vit):
+    """The fixture inputs are the seeded synthetic generator's output (no hidden state)."""
+    cfg = vit.data.CONFIGS["test"]
+    z = np.load(os.path.join(GOLDEN, "test.npz"))
+    assert np.array_equal(vit.data.init_params(cfg, "parity", seed=7), z["params"])
+    px, lab = vit.data.synthetic_batch(cfg, 2, seed=11)
+    assert np.array_equal(px, z["pixels"]) and np.array_equal(lab, z["labels"])
+
+
+def test_sgd_step(oracle32):
+    o = oracle32
+    p, g = o.arr(np.arange(5.0)), o.arr(np.ones(5))
+    o.sgd_step(p, g, 0.5)
+    assert np.allclose(p, np.arange(5.0) - 0.5)

@@ -1,0 +1,348 @@
+"""vit.rs_amd — MI355X-native ViT training step: host-side mirror of the reference interface.
+
+The product is libvit_hip.so (csrc/: gfx950 HIP kernels, the C ABI of include/vit_ops.h and the
+native trainer of include/vit_trainer.h).  This module is the thin Python host over that C ABI
+(ctypes, no torch types), mirroring the reference's model interface (/root/reference/
+train_vit.rs: `ViT::build_from_checkpoint`, `forward`, `backward`, `optimizer_step`,
+`mean_loss`) so tests and the benchmark read like the reference's own code.
+
+There is no CPU fallback: if libvit_hip.so is missing or cannot be loaded, every entry point
+raises.  If torch is used in the same process, import it BEFORE this package so that the
+HIP runtime torch ships is the single runtime in the process.
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libvit_hip.so")
+
+from . import data  # noqa: E402  (configs, canonical layout, seeded synthetic inputs)
+
+VIT_FP32, VIT_BF16 = 0, 1
+_lib = None
+
+
+class VitError(RuntimeError):
+    pass
+
+
+class VitConfigC(ctypes.Structure):
+    _fields_ = [("img", ctypes.c_int), ("patch", ctypes.c_int), ("in_ch", ctypes.c_int),
+                ("channels", ctypes.c_int), ("num_layers", ctypes.c_int),
+                ("num_heads", ctypes.c_int), ("num_classes", ctypes.c_int)]
+
+
+def build(quiet=True):
+    """Compile libvit_hip.so in place (hipcc, gfx950)."""
+    import subprocess
+    jobs = str(min(8, os.cpu_count() or 1))
+    subprocess.run(["make", "-s", "-j", jobs, "-C", HERE], check=True,
+                   stdout=subprocess.DEVNULL if quiet else None)
+
+
+_VOID = [("vit_clear_error", []), ("vit_set_stream", [ctypes.c_void_p]),
+         ("vit_free", [ctypes.c_void_p]), ("vit_event_destroy", [ctypes.c_void_p]),
+         ("vit_trainer_destroy", [ctypes.c_void_p]), ("vit_trainer_timing_reset", [ctypes.c_void_p])]
+
+# name -> (restype, argtypes)
+P, I, LL, F, S = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_size_t
+_SIGS = {
+    "vit_init": (I, [I]), "vit_get_stream": (P, []), "vit_sync": (I, []),
+    "vit_last_error": (I, [ctypes.POINTER(ctypes.c_char_p)]),
+    "vit_malloc": (P, [S]), "vit_memcpy_h2d": (I, [P, P, S]), "vit_memcpy_d2h": (I, [P, P, S]),
+    "vit_memcpy_d2d": (I, [P, P, S]), "vit_memset": (I, [P, I, S]),
+    "vit_event_create": (P, []), "vit_event_record": (I, [P]), "vit_event_elapsed_ms": (F, [P, P]),
+    # reference ops (fp32)
+    "residual_forward": (None, [P, P, P, I]),
+    "matmul_forward": (None, [P, P, P, P, I, I, I, I]),
+    "attention_forward": (None, [P, P, P, P, I, I, I, I]),
+    "layernorm_forward": (None, [P, P, P, P, P, P, I, I, I]),
+    "gelu_forward": (None, [P, P, I]),
+    "softmax_forward": (None, [P, P, I, I, I]),
+    "crossentropy_forward": (None, [P, P, P, I, I, I]),
+    "residual_backward": (None, [P, P, P, I]),
+    "matmul_backward": (None, [P, P, P, P, P, P, I, I, I, I]),
+    "attention_backward": (None, [P, P, P, P, P, P, I, I, I, I]),
+    "layernorm_backward": (None, [P, P, P, P, P, P, P, P, I, I, I]),
+    "gelu_backward": (None, [P, P, P, I]),
+    "crossentropy_softmax_backward": (None, [P, P, P, P, I, I, I]),
+    "patch_embed_forward": (None, [P, P, P, P, P, P, I, I, I, I]),
+    "patch_embed_backward": (None, [P, P, P, P, P, P, I, I, I, I]),
+    "sgd_step": (None, [P, P, LL, F]),
+    # bf16 extensions
+    "matmul_forward_bf16": (None, [P, P, P, P, I, I, I, I]),
+    "matmul_backward_bf16": (None, [P, P, P, P, P, P, I, I, I, I]),
+    "attention_forward_fused_bf16": (None, [P, P, P, I, I, I, I]),
+    "attention_backward_fused_bf16": (None, [P, P, P, P, P, I, I, I, I]),
+    "layernorm_forward_bf16": (None, [P, P, P, P, P, P, I, I, I]),
+    "convert_f32_to_bf16": (None, [P, P, LL]),
+    "convert_bf16_to_f32": (None, [P, P, LL]),
+    # trainer
+    "vit_trainer_create": (P, [ctypes.POINTER(VitConfigC), I, I, I]),
+    "vit_trainer_num_params": (LL, [P]), "vit_trainer_device_bytes": (LL, [P]),
+    "vit_trainer_set_params": (I, [P, P]), "vit_trainer_get_params": (I, [P, P]),
+    "vit_trainer_get_grads": (I, [P, P]), "vit_trainer_set_batch": (I, [P, P, P]),
+    "vit_trainer_set_batch_device": (I, [P, P, P]),
+    "vit_trainer_forward": (I, [P, I]), "vit_trainer_zero_grad": (I, [P]),
+    "vit_trainer_backward": (I, [P]), "vit_trainer_step": (I, [P, F]),
+    "vit_trainer_train_step": (I, [P, F, I]), "vit_trainer_mean_loss": (F, [P]),
+    "vit_trainer_get_logits": (I, [P, P]), "vit_trainer_sync": (I, [P]),
+    "vit_trainer_stream": (P, [P]),
+    "vit_dp_unique_id_size": (I, []), "vit_dp_get_unique_id": (I, [ctypes.c_char_p]),
+    "vit_trainer_dp_init": (I, [P, I, I, ctypes.c_char_p, I]),
+    "vit_trainer_set_timing": (I, [P, I]),
+    "vit_trainer_timing": (I, [P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
+                               ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double), I]),
+}
+
+
+def exported_symbols():
+    """Every symbol include/*.h declares (used by the ABI test)."""
+    return sorted(set(_SIGS) | {n for n, _ in _VOID})
+
+
+def lib():
+    """Load libvit_hip.so (raises if absent — there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise VitError(f"{LIB_PATH} not built; run __graft_entry__.build() or make -C vit.rs_amd")
+    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in _SIGS.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    for name, args in _VOID:
+        f = getattr(L, name)
+        f.restype = None
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def check(what=""):
+    """Raise the sticky library error, if any."""
+    msg = ctypes.c_char_p()
+    if lib().vit_last_error(ctypes.byref(msg)):
+        text = msg.value.decode() if msg.value else "unknown"
+        lib().vit_clear_error()
+        raise VitError(f"{what}: {text}" if what else text)
+
+
+# --------------------------------------------------------------------------- device buffers
+class DeviceArray:
+    """Owned device allocation with numpy up/download (vit_malloc / vit_memcpy)."""
+
+    def __init__(self, shape, dtype):
+        self.shape = tuple(shape) if isinstance(shape, (tuple, list)) else (int(shape),)
+        self.dtype = np.dtype(dtype)
+        self.nbytes = int(np.prod(self.shape)) * self.dtype.itemsize
+        self.ptr = lib().vit_malloc(max(self.nbytes, 16))
+        if not self.ptr:
+            check("vit_malloc")
+            raise VitError("vit_malloc returned NULL")
+
+    @classmethod
+    def from_numpy(cls, a, dtype=None):
+        a = np.ascontiguousarray(a if dtype is None else a.astype(dtype))
+        d = cls(a.shape, a.dtype)
+        d.upload(a)
+        return d
+
+    @classmethod
+    def zeros(cls, shape, dtype):
+        d = cls(shape, dtype)
+        lib().vit_memset(d.ptr, 0, d.nbytes)
+        check("vit_memset")
+        return d
+
+    def upload(self, a):
+        a = np.ascontiguousarray(a, dtype=self.dtype)
+        assert a.nbytes == self.nbytes
+        lib().vit_memcpy_h2d(self.ptr, a.ctypes.data_as(ctypes.c_void_p), self.nbytes)
+        check("h2d")
+
+    def numpy(self):
+        out = np.empty(self.shape, dtype=self.dtype)
+        lib().vit_sync()
+        lib().vit_memcpy_d2h(out.ctypes.data_as(ctypes.c_void_p), self.ptr, self.nbytes)
+        check("d2h")
+        return out
+
+    def free(self):
+        if self.ptr:
+            lib().vit_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def bf16_bits(a):
+    """fp32 numpy -> bf16 bits (uint16), round to nearest even."""
+    u = np.ascontiguousarray(a, dtype=np.float32).view(np.uint32)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+    return r
+
+
+def bf16_to_f32(b):
+    return (np.asarray(b, dtype=np.uint16).astype(np.uint32) << 16).view(np.float32)
+
+
+def call(name, *args):
+    """Call a C-ABI op with DeviceArray / int / float arguments and raise on error."""
+    L = lib()
+    cargs = []
+    for a in args:
+        if isinstance(a, DeviceArray):
+            cargs.append(a.ptr)
+        elif a is None:
+            cargs.append(None)
+        else:
+            cargs.append(a)
+    getattr(L, name)(*cargs)
+    L.vit_sync()
+    check(name)
+
+
+# --------------------------------------------------------------------------- model
+class ViT:
+    """Mirror of the reference's `struct ViT` (train_vit.rs:65-86) over the native trainer.
+
+    build(cfg, batch, precision)      ~ ViT::build_from_checkpoint (:89) with canonical params
+    forward(pixels, targets, b_glob)  ~ ViT::forward (:188); sets .mean_loss (:263)
+    zero_grad(); backward()           ~ gradient zeroing (:272) + ViT::backward (:271)
+    optimizer_step(lr)                ~ optimizer_step (:737)
+    """
+
+    def __init__(self, cfg, batch, precision=VIT_BF16, device=0):
+        L = lib()
+        self.cfg = cfg
+        self.B = batch
+        self.precision = precision
+        c = VitConfigC(cfg.img, cfg.patch, cfg.in_ch, cfg.channels, cfg.num_layers,
+                       cfg.num_heads, cfg.num_classes)
+        self.h = L.vit_trainer_create(ctypes.byref(c), batch, precision, device)
+        if not self.h:
+            check("vit_trainer_create")
+            raise VitError("vit_trainer_create failed")
+        self.num_parameters = int(L.vit_trainer_num_params(self.h))
+        assert self.num_parameters == cfg.num_params()
+        self.mean_loss = -1.0
+
+    @classmethod
+    def build(cls, cfg, batch, precision=VIT_BF16, params=None, device=0):
+        m = cls(cfg, batch, precision, device)
+        if params is not None:
+            m.set_params(params)
+        return m
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().vit_trainer_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _ok(self, rc, what):
+        if rc:
+            check(what)
+            raise VitError(what)
+
+    def set_params(self, flat):
+        flat = np.ascontiguousarray(flat, dtype=np.float32)
+        assert flat.size == self.num_parameters
+        self._ok(lib().vit_trainer_set_params(self.h, flat.ctypes.data_as(P)), "set_params")
+
+    def params(self):
+        out = np.empty(self.num_parameters, dtype=np.float32)
+        self._ok(lib().vit_trainer_get_params(self.h, out.ctypes.data_as(P)), "get_params")
+        return out
+
+    def grads(self):
+        out = np.empty(self.num_parameters, dtype=np.float32)
+        self._ok(lib().vit_trainer_get_grads(self.h, out.ctypes.data_as(P)), "get_grads")
+        return out
+
+    def set_batch(self, pixels, labels):
+        px = np.ascontiguousarray(pixels, dtype=np.float32)
+        lb = np.ascontiguousarray(labels, dtype=np.int32)
+        assert px.shape == (self.B, 3, self.cfg.img, self.cfg.img) and lb.shape == (self.B,)
+        self._ok(lib().vit_trainer_set_batch(self.h, px.ctypes.data_as(P), lb.ctypes.data_as(P)),
+                 "set_batch")
+
+    def forward(self, pixels=None, targets=None, b_global=None):
+        if pixels is not None:
+            self.set_batch(pixels, targets)
+        self._ok(lib().vit_trainer_forward(self.h, int(b_global or self.B)), "forward")
+        self.mean_loss = float(lib().vit_trainer_mean_loss(self.h))
+        check("mean_loss")
+        return self.mean_loss
+
+    def forward_async(self, b_global=None):
+        self._ok(lib().vit_trainer_forward(self.h, int(b_global or self.B)), "forward")
+
+    def zero_grad(self):
+        self._ok(lib().vit_trainer_zero_grad(self.h), "zero_grad")
+
+    def backward(self):
+        self._ok(lib().vit_trainer_backward(self.h), "backward")
+
+    def optimizer_step(self, lr):
+        self._ok(lib().vit_trainer_step(self.h, float(lr)), "optimizer_step")
+
+    def train_step(self, lr, b_global=None):
+        self._ok(lib().vit_trainer_train_step(self.h, float(lr), int(b_global or self.B)),
+                 "train_step")
+
+    def logits(self):
+        out = np.empty((self.B, self.cfg.num_classes), dtype=np.float32)
+        self._ok(lib().vit_trainer_get_logits(self.h, out.ctypes.data_as(P)), "get_logits")
+        return out
+
+    def sync(self):
+        self._ok(lib().vit_trainer_sync(self.h), "sync")
+
+    def device_bytes(self):
+        return int(lib().vit_trainer_device_bytes(self.h))
+
+    # ---- data parallel (RCCL over xGMI), one process per GPU
+    @staticmethod
+    def dp_unique_id():
+        n = lib().vit_dp_unique_id_size()
+        buf = ctypes.create_string_buffer(n)
+        if lib().vit_dp_get_unique_id(buf):
+            check("ncclGetUniqueId")
+        return buf.raw
+
+    def dp_init(self, rank, world, unique_id, overlap=True):
+        self._ok(lib().vit_trainer_dp_init(self.h, rank, world, unique_id, int(overlap)), "dp_init")
+
+    # ---- per-kernel-class timing (HIP events on the trainer stream)
+    def set_timing(self, on=True):
+        lib().vit_trainer_set_timing(self.h, int(on))
+
+    def timing(self):
+        n = 64
+        names = (ctypes.c_char_p * n)()
+        ms = (ctypes.c_double * n)()
+        calls = (ctypes.c_longlong * n)()
+        flops = (ctypes.c_double * n)()
+        k = lib().vit_trainer_timing(self.h, names, ms, calls, flops, n)
+        check("timing")
+        return {names[i].decode(): {"ms": ms[i], "calls": calls[i], "flops": flops[i]}
+                for i in range(k)}
+
+    def timing_reset(self):
+        lib().vit_trainer_timing_reset(self.h)

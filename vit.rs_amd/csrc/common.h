@@ -1,0 +1,90 @@
+// common.h — shared device helpers and the host-side error/stream context of libvit_hip.so.
+// gfx950 (CDNA4) only: wave64, bf16 MFMA, ds_read_b64_tr_b16.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstdio>
+
+typedef uint16_t bf16_t;  // raw bf16 bits in HBM
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+#define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
+
+// ---------------------------------------------------------------- host context
+namespace vit {
+// Sticky, thread-local error (the reference ops return () — train_vit.rs:376-670 — so errors
+// are reported through vit_last_error()).
+void set_error(const char* fmt, ...);
+bool has_error();
+hipStream_t stream();
+bool sync_each_op();
+void* workspace(size_t bytes);  // per-thread device scratch, grown on demand
+void after_launch(const char* what);
+}  // namespace vit
+
+#define VIT_HIP(call)                                                                  \
+    do {                                                                               \
+        hipError_t e_ = (call);                                                        \
+        if (e_ != hipSuccess) vit::set_error("%s:%d %s: %s", __FILE__, __LINE__, #call, \
+                                             hipGetErrorString(e_));                   \
+    } while (0)
+
+#define VIT_REQUIRE(cond, ...)          \
+    do {                                \
+        if (!(cond)) {                  \
+            vit::set_error(__VA_ARGS__); \
+            return;                     \
+        }                               \
+    } while (0)
+
+// ---------------------------------------------------------------- device helpers
+__device__ __forceinline__ float bf2f(bf16_t h) { return __uint_as_float((uint32_t)h << 16); }
+__device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+    return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+__device__ __forceinline__ float warp_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float warp_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// tanh-GELU (train_vit.rs:482-491) and its derivative with the D4 fix (sech^2 of the argument)
+__device__ __forceinline__ float gelu_f(float x) {
+    const float s = 0.7978845608028654f;
+    float cube = 0.044715f * x * x * x;
+    return 0.5f * x * (1.0f + tanhf(s * (x + cube)));
+}
+__device__ __forceinline__ float gelu_grad_f(float x) {
+    const float s = 0.7978845608028654f;
+    float cube = 0.044715f * x * x * x;
+    float a = s * (x + cube);
+    float th = tanhf(a);
+    float sech2 = 1.0f - th * th;  // == 1/cosh^2(a)
+    return 0.5f * (1.0f + th) + x * 0.5f * sech2 * s * (1.0f + 3.0f * 0.044715f * x * x);
+}
+
+// optimizer_step (train_vit.rs:740): p -= lr*g with two roundings like the Rust reference
+// (no FMA contraction), so the fp32 update is bit-exact.
+__device__ __forceinline__ float sgd_update(float p, float g, float lr) {
+#pragma clang fp contract(off)
+    return p - lr * g;
+}
+
+// XCD-aware bijective remap of a linear workgroup id (cdna_hip_programming.md §5, "XCD swizzle
+// must be bijective"): blocks dealt round-robin over 8 XCDs get contiguous tile ranges per XCD.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+    const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+__host__ __device__ static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }

@@ -1,0 +1,54 @@
+// gemm.h — internal GEMM launcher API shared by the C-ABI ops and the trainer.
+//
+// C[M,N] (epilogue)= A[M,K] . B[K,N] with per-operand storage:
+//   A(m,k) = a_kcontig ? A[m*lda + k] : A[k*lda + m]
+//   B(k,n) = b_kcontig ? B[n*ldb + k] : B[k*ldb + n]
+// The three products of matmul_forward/backward (train_vit.rs:384-398, 530-557) map to
+//   forward  (out = inp . W^T):   A = inp  (K-contig), B = W (K-contig, W[n][k])
+//   dgrad    (dinp = dout . W):   A = dout (K-contig), B = W (N-contig, W[k][n])
+//   wgrad    (dW = dout^T . inp): A = dout (M-contig), B = inp (N-contig); K = B*T rows
+#pragma once
+#include "common.h"
+
+namespace vit {
+
+enum Epi {
+    EPI_F32_STORE = 0,   // C_f32 = acc (+ bias[n])
+    EPI_F32_ACC = 1,     // C_f32 += acc (+ bias[n])
+    EPI_F32_ATOMIC = 2,  // atomicAdd(C_f32, acc)   (split-K partials)
+    EPI_BF16_STORE = 3,  // C_bf16 = acc (+ bias)
+    EPI_BF16_GELU = 4,   // C_bf16 = pre = acc + bias; C2_bf16 = gelu(pre)
+    EPI_F32_RESID = 5,   // C_f32 = acc + bias + aux_f32[m*ldaux + n]
+    EPI_BF16_DGELU = 6,  // C_bf16 = acc * gelu'(aux_bf16[m*ldaux + n])
+};
+
+struct GemmArgs {
+    const void* A = nullptr;
+    long long lda = 0;
+    bool a_kcontig = true;
+    const void* B = nullptr;
+    long long ldb = 0;
+    bool b_kcontig = true;
+    void* C = nullptr;
+    long long ldc = 0;
+    void* C2 = nullptr;
+    const void* aux = nullptr;
+    long long ldaux = 0;
+    const float* bias = nullptr;
+    int M = 0, N = 0, K = 0;
+    int epi = EPI_F32_STORE;
+    int splitk = 0;  // 0 = choose automatically (only EPI_F32_ATOMIC may split)
+};
+
+// fp32 operands, exact-fp32 MFMA (v_mfma_f32_16x16x4_f32); any shape/stride. Parity path.
+void gemm_f32(const GemmArgs& a, hipStream_t s);
+// bf16 operands, fp32 accumulate (v_mfma_f32_16x16x32_bf16); requires K%8==0, 16-B aligned
+// operands, lda/ldb%8==0, the contiguous dim of an M/N-contig operand %8==0, N%4==0.
+void gemm_bf16(const GemmArgs& a, hipStream_t s);
+bool gemm_bf16_supported(const GemmArgs& a);
+
+// column sums: dbias[n] += sum_m X[m*ld + n]   (X fp32 or bf16)
+void colsum_f32(float* dbias, const float* X, int M, int N, long long ld, hipStream_t s);
+void colsum_bf16(float* dbias, const bf16_t* X, int M, int N, long long ld, hipStream_t s);
+
+}  // namespace vit

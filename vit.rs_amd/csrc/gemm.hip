@@ -1,0 +1,422 @@
+// gemm.hip — MFMA GEMMs for matmul_forward / matmul_backward (train_vit.rs:384-398, 530-557).
+//
+// gemm_bf16: 128x128x64 block tile, 256 threads = 4 waves (2x2), 64x64 per wave as 4x4
+//   v_mfma_f32_16x16x32_bf16 tiles, register-staged double-buffered LDS, one barrier per
+//   K-tile, XCD-aware bijective block remap.  Both operand kinds use one fragment scheme:
+//   a 32-deep k-step is read as two 8-byte halves at k = 4g.. and 16+4g.. (g = lane>>4), from a
+//   K-contiguous image with ds_read_b64 or from an M/N-contiguous image with
+//   ds_read_b64_tr_b16 (the gfx950 transpose read).  Because every operand uses the same k
+//   permutation the products are exact, and the padded row strides (144 B / 288 B) make both
+//   reads bank-conflict free for the 32-lane halves.  The MFMA is issued with the operands
+//   swapped (D = B^T A^T) so each lane owns 4 consecutive output columns of one row: the
+//   epilogue stores 8-16 contiguous bytes per lane.
+// gemm_f32: 64x64x16 tile on v_mfma_f32_16x16x4_f32 (exact fp32 fma chain), generic strides,
+//   bounds-checked scalar staging; the fp32 parity path.
+#include "gemm.h"
+
+namespace vit {
+
+struct GemmParams {
+    const void* A;
+    const void* B;
+    void* C;
+    void* C2;
+    const void* aux;
+    const float* bias;
+    long long lda, ldb, ldc, ldaux;
+    int M, N, K;
+    int kchunk;  // K range per split (multiple of the K tile)
+};
+
+// ============================================================================ bf16 MFMA GEMM
+namespace bf {
+constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+constexpr int SK = 72;    // K-contig image row stride (elements): 144 B
+constexpr int SMN = 144;  // M/N-contig image row stride (elements): 288 B
+constexpr int TILE = 9216;  // = 128*72 = 64*144 elements per operand image
+static_assert(BM * SK == TILE && BK * SMN == TILE, "image sizes");
+
+template <bool KC, int ROWS>
+struct Stager {
+    uint4 r[4];
+    // ROWS = rows of the operand tile along M (or N); K-tile = BK
+    __device__ __forceinline__ void load(const bf16_t* __restrict__ base, long long ld, int row0,
+                                         int rows_lim, int k0, int k_lim, int tid) {
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const int idx = c * NT + tid;
+            int row, col;
+            bool ok;
+            const bf16_t* p;
+            if constexpr (KC) {
+                row = idx >> 3;
+                col = (idx & 7) * 8;
+                ok = (row0 + row < rows_lim) && (k0 + col < k_lim);
+                p = base + (long long)(row0 + row) * ld + (k0 + col);
+            } else {
+                row = idx >> 4;  // k row
+                col = (idx & 15) * 8;
+                ok = (k0 + row < k_lim) && (row0 + col < rows_lim);
+                p = base + (long long)(k0 + row) * ld + (row0 + col);
+            }
+            r[c] = ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
+        }
+    }
+    __device__ __forceinline__ void store(bf16_t* img, int tid) const {
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const int idx = c * NT + tid;
+            int off;
+            if constexpr (KC)
+                off = (idx >> 3) * SK + (idx & 7) * 8;
+            else
+                off = (idx >> 4) * SMN + (idx & 15) * 8;
+            *reinterpret_cast<uint4*>(img + off) = r[c];
+        }
+    }
+};
+
+// fragment of rows [r0, r0+16) for k-step s (32 deep) — element j<4: k = 32s+4g+j,
+// j>=4: k = 32s+16+4g+(j-4)
+template <bool KC>
+__device__ __forceinline__ bf16x8_t frag(const bf16_t* img, int r0, int s, int lane) {
+    const int i = lane & 15, g = lane >> 4;
+    bf16x4_t lo, hi;
+    if constexpr (KC) {
+        const bf16_t* p = img + (r0 + i) * SK + 32 * s + 4 * g;
+        lo = *reinterpret_cast<const bf16x4_t*>(p);
+        hi = *reinterpret_cast<const bf16x4_t*>(p + 16);
+    } else {
+        const bf16_t* p = img + (32 * s + 4 * g + (i >> 2)) * SMN + r0 + 4 * (i & 3);
+        lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4_t, p));
+        hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4_t, p + 16 * SMN));
+    }
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+template <bool AK, bool BKC, int EPI>
+__global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmParams p) {
+    __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TILE];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int ntm = cdiv(p.M, BM), ntn = cdiv(p.N, BN);
+    const int wg = xcd_remap(blockIdx.x, ntm * ntn);
+    const int tm0 = (wg / ntn) * BM, tn0 = (wg % ntn) * BN;
+    const int kbeg = blockIdx.y * p.kchunk;
+    const int kend = min(p.K, kbeg + p.kchunk);
+    const int nk = cdiv(kend - kbeg, BK);
+    const bf16_t* A = (const bf16_t*)p.A;
+    const bf16_t* B = (const bf16_t*)p.B;
+
+    f32x4_t acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    Stager<AK, BM> sa;
+    Stager<BKC, BN> sb;
+    if (nk > 0) {
+        sa.load(A, p.lda, tm0, p.M, kbeg, kend, tid);
+        sb.load(B, p.ldb, tn0, p.N, kbeg, kend, tid);
+        sa.store(smem, tid);
+        sb.store(smem + TILE, tid);
+    }
+    __syncthreads();
+    for (int kt = 0; kt < nk; kt++) {
+        const int cur = kt & 1;
+        const bf16_t* imgA = smem + cur * 2 * TILE;
+        const bf16_t* imgB = imgA + TILE;
+        const bool more = kt + 1 < nk;
+        if (more) {
+            const int k0 = kbeg + (kt + 1) * BK;
+            sa.load(A, p.lda, tm0, p.M, k0, kend, tid);
+            sb.load(B, p.ldb, tn0, p.N, k0, kend, tid);
+        }
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            bf16x8_t af[4], bfr[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                af[t] = frag<AK>(imgA, wm * 64 + t * 16, s, lane);
+                bfr[t] = frag<BKC>(imgB, wn * 64 + t * 16, s, lane);
+            }
+#pragma unroll
+            for (int a = 0; a < 4; a++)
+#pragma unroll
+                for (int b = 0; b < 4; b++)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[b], af[a], acc[a][b],
+                                                                        0, 0, 0);
+        }
+        if (more) {
+            bf16_t* nxt = smem + (cur ^ 1) * 2 * TILE;
+            sa.store(nxt, tid);
+            sb.store(nxt + TILE, tid);
+        }
+        __syncthreads();
+    }
+
+    // epilogue: lane holds C[m][n..n+3], m = tm0 + wm*64 + a*16 + (lane&15),
+    //           n = tn0 + wn*64 + b*16 + 4*(lane>>4)
+    const int i = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int a = 0; a < 4; a++) {
+        const int m = tm0 + wm * 64 + a * 16 + i;
+        if (m >= p.M) continue;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const int n = tn0 + wn * 64 + b * 16 + 4 * g;
+            if (n >= p.N) continue;
+            f32x4_t v = acc[a][b];
+            if constexpr (EPI != EPI_F32_ATOMIC && EPI != EPI_BF16_DGELU) {
+                if (p.bias) {
+                    const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
+                    v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+                }
+            }
+            const long long off = (long long)m * p.ldc + n;
+            if constexpr (EPI == EPI_F32_STORE) {
+                *reinterpret_cast<float4*>((float*)p.C + off) = make_float4(v[0], v[1], v[2], v[3]);
+            } else if constexpr (EPI == EPI_F32_ACC) {
+                float4* q = reinterpret_cast<float4*>((float*)p.C + off);
+                float4 o = *q;
+                o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
+                *q = o;
+            } else if constexpr (EPI == EPI_F32_ATOMIC) {
+                float* q = (float*)p.C + off;
+                atomicAdd(q + 0, v[0]);
+                atomicAdd(q + 1, v[1]);
+                atomicAdd(q + 2, v[2]);
+                atomicAdd(q + 3, v[3]);
+            } else if constexpr (EPI == EPI_BF16_STORE) {
+                *reinterpret_cast<uint2*>((bf16_t*)p.C + off) =
+                    make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+            } else if constexpr (EPI == EPI_BF16_GELU) {
+                *reinterpret_cast<uint2*>((bf16_t*)p.C + off) =
+                    make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+                *reinterpret_cast<uint2*>((bf16_t*)p.C2 + off) =
+                    make_uint2(pack_bf16x2(gelu_f(v[0]), gelu_f(v[1])),
+                               pack_bf16x2(gelu_f(v[2]), gelu_f(v[3])));
+            } else if constexpr (EPI == EPI_F32_RESID) {
+                const float4 r = *reinterpret_cast<const float4*>((const float*)p.aux +
+                                                                  (long long)m * p.ldaux + n);
+                *reinterpret_cast<float4*>((float*)p.C + off) =
+                    make_float4(v[0] + r.x, v[1] + r.y, v[2] + r.z, v[3] + r.w);
+            } else if constexpr (EPI == EPI_BF16_DGELU) {
+                const uint2 h = *reinterpret_cast<const uint2*>((const bf16_t*)p.aux +
+                                                                (long long)m * p.ldaux + n);
+                const float x0 = __uint_as_float(h.x << 16), x1 = __uint_as_float(h.x & 0xffff0000u);
+                const float x2 = __uint_as_float(h.y << 16), x3 = __uint_as_float(h.y & 0xffff0000u);
+                *reinterpret_cast<uint2*>((bf16_t*)p.C + off) =
+                    make_uint2(pack_bf16x2(v[0] * gelu_grad_f(x0), v[1] * gelu_grad_f(x1)),
+                               pack_bf16x2(v[2] * gelu_grad_f(x2), v[3] * gelu_grad_f(x3)));
+            }
+        }
+    }
+}
+}  // namespace bf
+
+// ============================================================================ fp32 MFMA GEMM
+namespace f32 {
+constexpr int BM = 64, BN = 64, BK = 16, NT = 256, S = 80;  // S: LDS row stride (floats)
+
+template <int EPI>
+__global__ __launch_bounds__(NT) void gemm_f32_kernel(GemmParams p, int a_kc, int b_kc) {
+    __shared__ float As[BK * S];
+    __shared__ float Bs[BK * S];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int ntm = cdiv(p.M, BM), ntn = cdiv(p.N, BN);
+    const int wg = blockIdx.x;
+    const int tm0 = (wg / ntn) * BM, tn0 = (wg % ntn) * BN;
+    (void)ntm;
+    const int kbeg = blockIdx.y * p.kchunk;
+    const int kend = min(p.K, kbeg + p.kchunk);
+    const float* A = (const float*)p.A;
+    const float* B = (const float*)p.B;
+    f32x4_t acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    for (int k0 = kbeg; k0 < kend; k0 += BK) {
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int idx = e * NT + tid;
+            int m, k;
+            if (a_kc) { m = idx >> 4; k = idx & 15; } else { k = idx >> 6; m = idx & 63; }
+            const int gm = tm0 + m, gk = k0 + k;
+            float v = 0.f;
+            if (gm < p.M && gk < kend)
+                v = a_kc ? A[(long long)gm * p.lda + gk] : A[(long long)gk * p.lda + gm];
+            As[k * S + m] = v;
+            int n;
+            if (b_kc) { n = idx >> 4; k = idx & 15; } else { k = idx >> 6; n = idx & 63; }
+            const int gn = tn0 + n;
+            const int gk2 = k0 + k;
+            float w = 0.f;
+            if (gn < p.N && gk2 < kend)
+                w = b_kc ? B[(long long)gn * p.ldb + gk2] : B[(long long)gk2 * p.ldb + gn];
+            Bs[k * S + n] = w;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < BK / 4; kk++) {
+            const int kr = kk * 4 + (lane >> 4);
+            float af[2], bfv[2];
+#pragma unroll
+            for (int t = 0; t < 2; t++) {
+                af[t] = As[kr * S + wm * 32 + t * 16 + (lane & 15)];
+                bfv[t] = Bs[kr * S + wn * 32 + t * 16 + (lane & 15)];
+            }
+#pragma unroll
+            for (int a = 0; a < 2; a++)
+#pragma unroll
+                for (int b = 0; b < 2; b++)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[a], bfv[b], acc[a][b], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    // C layout: row = (lane>>4)*4 + r, col = lane&15
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int m = tm0 + wm * 32 + a * 16 + (lane >> 4) * 4 + r;
+                const int n = tn0 + wn * 32 + b * 16 + (lane & 15);
+                if (m >= p.M || n >= p.N) continue;
+                float v = acc[a][b][r];
+                float* q = (float*)p.C + (long long)m * p.ldc + n;
+                if constexpr (EPI == EPI_F32_STORE) {
+                    *q = p.bias ? v + p.bias[n] : v;
+                } else if constexpr (EPI == EPI_F32_ACC) {
+                    *q += p.bias ? v + p.bias[n] : v;
+                } else {
+                    atomicAdd(q, v);
+                }
+            }
+}
+}  // namespace f32
+
+// ============================================================================ column sums
+template <typename TX>
+__global__ __launch_bounds__(256) void colsum_kernel(float* __restrict__ dbias,
+                                                     const TX* __restrict__ X, int M, int N,
+                                                     long long ld, int rows_per_block) {
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    const int r0 = blockIdx.y * rows_per_block;
+    const int r1 = min(M, r0 + rows_per_block);
+    if (n >= N) return;
+    float s = 0.f;
+    for (int r = r0; r < r1; r++) {
+        if constexpr (sizeof(TX) == 2)
+            s += bf2f(X[(long long)r * ld + n]);
+        else
+            s += X[(long long)r * ld + n];
+    }
+    atomicAdd(dbias + n, s);
+}
+
+static GemmParams make_params(const GemmArgs& a, int kchunk) {
+    GemmParams p;
+    p.A = a.A; p.B = a.B; p.C = a.C; p.C2 = a.C2; p.aux = a.aux; p.bias = a.bias;
+    p.lda = a.lda; p.ldb = a.ldb; p.ldc = a.ldc; p.ldaux = a.ldaux;
+    p.M = a.M; p.N = a.N; p.K = a.K; p.kchunk = kchunk;
+    return p;
+}
+
+static int choose_split(int tiles, int K, int ktile, int want_blocks) {
+    int nk = cdiv(K, ktile);
+    int s = 1;
+    while (tiles * s < want_blocks && nk / (s * 2) >= 8) s *= 2;
+    return s;
+}
+
+void gemm_f32(const GemmArgs& a, hipStream_t s) {
+    if (a.M <= 0 || a.N <= 0) return;
+    const int tiles = cdiv(a.M, f32::BM) * cdiv(a.N, f32::BN);
+    int split = 1;
+    if (a.epi == EPI_F32_ATOMIC) split = a.splitk > 0 ? a.splitk : choose_split(tiles, a.K, f32::BK, 512);
+    int kchunk = cdiv(cdiv(a.K, split), f32::BK) * f32::BK;
+    if (kchunk <= 0) kchunk = f32::BK;
+    split = cdiv(a.K > 0 ? a.K : 1, kchunk);
+    GemmParams p = make_params(a, kchunk);
+    dim3 grid(tiles, split);
+    int akc = a.a_kcontig, bkc = a.b_kcontig;
+    switch (a.epi) {
+        case EPI_F32_STORE: f32::gemm_f32_kernel<EPI_F32_STORE><<<grid, f32::NT, 0, s>>>(p, akc, bkc); break;
+        case EPI_F32_ACC: f32::gemm_f32_kernel<EPI_F32_ACC><<<grid, f32::NT, 0, s>>>(p, akc, bkc); break;
+        case EPI_F32_ATOMIC: f32::gemm_f32_kernel<EPI_F32_ATOMIC><<<grid, f32::NT, 0, s>>>(p, akc, bkc); break;
+        default: set_error("gemm_f32: unsupported epilogue %d", a.epi); return;
+    }
+    after_launch("gemm_f32");
+}
+
+bool gemm_bf16_supported(const GemmArgs& a) {
+    auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+    if ((a.a_kcontig || a.b_kcontig) && a.K % 8) return false;  // 16-B chunks along K
+    if (a.lda % 8 || a.ldb % 8 || a.N % 4 || a.ldc % 4) return false;
+    if (!al16(a.A) || !al16(a.B)) return false;
+    if (!a.a_kcontig && a.M % 8) return false;
+    if (!a.b_kcontig && a.N % 8) return false;
+    return true;
+}
+
+template <bool AK, bool BKC>
+static void launch_bf16(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStream_t s) {
+    switch (a.epi) {
+#define VIT_CASE(E) \
+    case E: bf::gemm_bf16_kernel<AK, BKC, E><<<grid, bf::NT, 0, s>>>(p); break;
+        VIT_CASE(EPI_F32_STORE)
+        VIT_CASE(EPI_F32_ACC)
+        VIT_CASE(EPI_F32_ATOMIC)
+        VIT_CASE(EPI_BF16_STORE)
+        VIT_CASE(EPI_BF16_GELU)
+        VIT_CASE(EPI_F32_RESID)
+        VIT_CASE(EPI_BF16_DGELU)
+#undef VIT_CASE
+        default: set_error("gemm_bf16: unsupported epilogue %d", a.epi); return;
+    }
+}
+
+void gemm_bf16(const GemmArgs& a, hipStream_t s) {
+    if (a.M <= 0 || a.N <= 0) return;
+    if (!gemm_bf16_supported(a)) {
+        set_error("gemm_bf16: unsupported shape/alignment M=%d N=%d K=%d lda=%lld ldb=%lld",
+                  a.M, a.N, a.K, a.lda, a.ldb);
+        return;
+    }
+    const int tiles = cdiv(a.M, bf::BM) * cdiv(a.N, bf::BN);
+    int split = 1;
+    if (a.epi == EPI_F32_ATOMIC) split = a.splitk > 0 ? a.splitk : choose_split(tiles, a.K, bf::BK, 512);
+    int kchunk = cdiv(cdiv(a.K, split), bf::BK) * bf::BK;
+    if (kchunk <= 0) kchunk = bf::BK;
+    split = cdiv(a.K > 0 ? a.K : 1, kchunk);
+    GemmParams p = make_params(a, kchunk);
+    dim3 grid(tiles, split);
+    if (a.a_kcontig && a.b_kcontig) launch_bf16<true, true>(a, p, grid, s);
+    else if (a.a_kcontig && !a.b_kcontig) launch_bf16<true, false>(a, p, grid, s);
+    else if (!a.a_kcontig && !a.b_kcontig) launch_bf16<false, false>(a, p, grid, s);
+    else launch_bf16<false, true>(a, p, grid, s);
+    after_launch("gemm_bf16");
+}
+
+void colsum_f32(float* dbias, const float* X, int M, int N, long long ld, hipStream_t s) {
+    if (M <= 0 || N <= 0) return;
+    const int rpb = 256;
+    dim3 grid(cdiv(N, 256), cdiv(M, rpb));
+    colsum_kernel<float><<<grid, 256, 0, s>>>(dbias, X, M, N, ld, rpb);
+    after_launch("colsum_f32");
+}
+void colsum_bf16(float* dbias, const bf16_t* X, int M, int N, long long ld, hipStream_t s) {
+    if (M <= 0 || N <= 0) return;
+    const int rpb = 256;
+    dim3 grid(cdiv(N, 256), cdiv(M, rpb));
+    colsum_kernel<bf16_t><<<grid, 256, 0, s>>>(dbias, X, M, N, ld, rpb);
+    after_launch("colsum_bf16");
+}
+
+}  // namespace vit

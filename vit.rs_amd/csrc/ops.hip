@@ -1,0 +1,526 @@
+// ops.hip — the reference layer ops behind the C ABI (include/vit_ops.h), fp32 and bf16.
+//
+// Memory-bound ops (residual, GELU, LayerNorm, softmax/CE, SGD) are wave-per-row or
+// grid-stride vectorised kernels; matmul_* go to the MFMA GEMMs of gemm.hip; attention to
+// attention.hip.  Each op cites the reference function it replaces.
+#include "ops_internal.h"
+
+namespace vit {
+
+// ------------------------------------------------------------------ elementwise
+__global__ void residual_fwd_k(float* __restrict__ out, const float* __restrict__ a,
+                               const float* __restrict__ b, long long n) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        out[i] = a[i] + b[i];
+}
+__global__ void residual_bwd_k(float* __restrict__ d1, float* __restrict__ d2,
+                               const float* __restrict__ dout, long long n) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x) {
+        const float g = dout[i];
+        d1[i] += g;
+        d2[i] += g;
+    }
+}
+__global__ void gelu_fwd_k(float* __restrict__ out, const float* __restrict__ inp, long long n) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        out[i] = gelu_f(inp[i]);
+}
+__global__ void gelu_bwd_k(float* __restrict__ dinp, const float* __restrict__ inp,
+                           const float* __restrict__ dout, long long n) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        dinp[i] += gelu_grad_f(inp[i]) * dout[i];
+}
+__global__ void sgd_k(float* __restrict__ p, const float* __restrict__ g, long long n, float lr) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        p[i] = sgd_update(p[i], g[i], lr);
+}
+__global__ void f2bf_k(bf16_t* __restrict__ out, const float* __restrict__ inp, long long n) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        out[i] = f2bf(inp[i]);
+}
+__global__ void bf2f_k(float* __restrict__ out, const bf16_t* __restrict__ inp, long long n) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        out[i] = bf2f(inp[i]);
+}
+
+int grid_for(long long n, int threads) {
+    long long b = (n + threads - 1) / threads;
+    return (int)(b < 1 ? 1 : (b > 8192 ? 8192 : b));
+}
+
+// ------------------------------------------------------------------ LayerNorm
+// one wave per row (train_vit.rs:453-480): two-pass mean/variance, biased var, eps 1e-5
+template <typename TO>
+__global__ __launch_bounds__(256) void ln_fwd_k(TO* __restrict__ out, float* __restrict__ mean,
+                                                float* __restrict__ rstd,
+                                                const float* __restrict__ inp,
+                                                const float* __restrict__ w,
+                                                const float* __restrict__ b, long long rows, int C) {
+    const int lane = threadIdx.x & 63;
+    const long long row = blockIdx.x * 4LL + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const float* x = inp + row * C;
+    float s = 0.f;
+    for (int i = lane; i < C; i += 64) s += x[i];
+    const float m = warp_sum(s) / (float)C;
+    float v = 0.f;
+    for (int i = lane; i < C; i += 64) {
+        const float d = x[i] - m;
+        v += d * d;
+    }
+    v = warp_sum(v) / (float)C;
+    const float r = 1.0f / sqrtf(v + 1e-5f);
+    TO* o = out + row * C;
+    for (int i = lane; i < C; i += 64) {
+        const float y = (r * (x[i] - m)) * w[i] + b[i];
+        if constexpr (sizeof(TO) == 2)
+            o[i] = f2bf(y);
+        else
+            o[i] = y;
+    }
+    if (lane == 0) {
+        mean[row] = m;
+        rstd[row] = r;
+    }
+}
+
+// train_vit.rs:603-637 (D5).  dinp += ...; dweight/dbias accumulate through per-block LDS
+// partials and one global atomic per column per block.  TD: dout type (fp32 or bf16).
+// If dres_in != nullptr:  dinp = dres_in + ln_dinp   (fused residual_backward, bf16 path),
+// and a bf16 copy of dinp is written to dinp_bf (if non-null).
+template <typename TD>
+__global__ __launch_bounds__(256) void ln_bwd_k(float* __restrict__ dinp, bf16_t* __restrict__ dinp_bf,
+                                                const float* __restrict__ dres_in,
+                                                float* __restrict__ dweight, float* __restrict__ dbias,
+                                                const TD* __restrict__ dout,
+                                                const float* __restrict__ inp,
+                                                const float* __restrict__ weight,
+                                                const float* __restrict__ mean,
+                                                const float* __restrict__ rstd, long long rows,
+                                                int C) {
+    extern __shared__ float sm[];  // [2][C]
+    float* sdw = sm;
+    float* sdb = sm + C;
+    for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) sm[i] = 0.f;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const long long nwaves = (long long)gridDim.x * 4;
+    for (long long row = blockIdx.x * 4LL + (threadIdx.x >> 6); row < rows; row += nwaves) {
+        const TD* dy = dout + row * C;
+        const float* x = inp + row * C;
+        const float mu = mean[row], rs = rstd[row];
+        float a = 0.f, bsum = 0.f;
+        for (int i = lane; i < C; i += 64) {
+            float d;
+            if constexpr (sizeof(TD) == 2) d = bf2f(dy[i]); else d = dy[i];
+            const float nrm = (x[i] - mu) * rs;
+            const float dn = weight[i] * d;
+            a += dn;
+            bsum += dn * nrm;
+        }
+        const float dnorm_mean = warp_sum(a) / (float)C;
+        const float dnorm_norm_mean = warp_sum(bsum) / (float)C;
+        for (int i = lane; i < C; i += 64) {
+            float d;
+            if constexpr (sizeof(TD) == 2) d = bf2f(dy[i]); else d = dy[i];
+            const float nrm = (x[i] - mu) * rs;
+            const float dn = weight[i] * d;
+            atomicAdd(&sdb[i], d);
+            atomicAdd(&sdw[i], nrm * d);
+            float dval = dn;
+            dval -= dnorm_mean;
+            dval -= nrm * dnorm_norm_mean;
+            dval *= rs;
+            const long long o = row * C + i;
+            if (dres_in) {
+                const float t = dres_in[o] + dval;
+                dinp[o] = t;
+                if (dinp_bf) dinp_bf[o] = f2bf(t);
+            } else {
+                dinp[o] += dval;
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < C; i += blockDim.x) {
+        atomicAdd(dweight + i, sdw[i]);
+        atomicAdd(dbias + i, sdb[i]);
+    }
+}
+
+// ------------------------------------------------------------------ softmax / cross-entropy
+// train_vit.rs:493-517 — block per row, max init -10000 (:499)
+__global__ __launch_bounds__(256) void softmax_k(float* __restrict__ probs,
+                                                 const float* __restrict__ logits, int V) {
+    __shared__ float red[4];
+    const long long row = blockIdx.x;
+    const float* l = logits + row * V;
+    float* pr = probs + row * V;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    float m = -10000.0f;
+    for (int i = threadIdx.x; i < V; i += 256) m = fmaxf(m, l[i]);
+    m = warp_max(m);
+    if (lane == 0) red[w] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    __syncthreads();
+    float s = 0.f;
+    for (int i = threadIdx.x; i < V; i += 256) {
+        const float e = expf(l[i] - m);
+        pr[i] = e;
+        s += e;
+    }
+    s = warp_sum(s);
+    if (lane == 0) red[w] = s;
+    __syncthreads();
+    s = red[0] + red[1] + red[2] + red[3];
+    const float inv = 1.0f / s;
+    for (int i = threadIdx.x; i < V; i += 256) pr[i] = pr[i] * inv;
+}
+__global__ void ce_fwd_k(float* __restrict__ losses, const float* __restrict__ probs,
+                         const int* __restrict__ targets, long long rows, int V) {
+    const long long r = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (r < rows) losses[r] = -logf(probs[r * V + targets[r]]);
+}
+__global__ void ce_bwd_k(float* __restrict__ dlogits, const float* __restrict__ dlosses,
+                         const float* __restrict__ probs, const int* __restrict__ targets,
+                         long long rows, int V) {
+    const long long n = rows * V;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x) {
+        const long long r = i / V;
+        const int v = (int)(i - r * V);
+        const float ind = v == targets[r] ? 1.0f : 0.0f;
+        dlogits[i] += (probs[i] - ind) * dlosses[r];
+    }
+}
+
+// ------------------------------------------------------------------ patch embedding
+// im2col of [B,3,IMG,IMG] -> rows (b,p) x cols (c*P+kh)*P+kw  (Conv2d weight flatten order)
+template <typename TO>
+__global__ void im2col_k(TO* __restrict__ out, const float* __restrict__ px, int B, int IMG, int P) {
+    const int gw = IMG / P, NP = gw * gw, K = 3 * P * P;
+    const long long n = (long long)B * NP * K;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < n;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const long long row = idx / K;
+        const int k = (int)(idx - row * K);
+        const int b = (int)(row / NP), p = (int)(row - (long long)b * NP);
+        const int c = k / (P * P), r = k - c * P * P, kh = r / P, kw = r - kh * P;
+        const int y = (p / gw) * P + kh, x = (p % gw) * P + kw;
+        const float v = px[(((long long)b * 3 + c) * IMG + y) * IMG + x];
+        if constexpr (sizeof(TO) == 2) out[idx] = f2bf(v); else out[idx] = v;
+    }
+}
+// encoded[b,0] = cls + wpe[0]; encoded[b,1+p] = emb[b*NP+p] + wpe[1+p]
+__global__ void patch_assemble_k(float* __restrict__ enc, const float* __restrict__ emb,
+                                 const float* __restrict__ cls, const float* __restrict__ wpe,
+                                 int B, int NP, int C) {
+    const int T = NP + 1;
+    const long long n = (long long)B * T * C;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < n;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const long long bt = idx / C;
+        const int c = (int)(idx - bt * C);
+        const int b = (int)(bt / T), t = (int)(bt - (long long)b * T);
+        const float base = t == 0 ? cls[c] : emb[((long long)b * NP + t - 1) * C + c];
+        enc[idx] = base + wpe[(long long)t * C + c];
+    }
+}
+// gather the patch rows of dencoded into [B*NP, C] (TO = float or bf16)
+template <typename TO>
+__global__ void patch_gather_k(TO* __restrict__ out, const float* __restrict__ denc, int B, int NP,
+                               int C) {
+    const int T = NP + 1;
+    const long long n = (long long)B * NP * C;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < n;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const long long r = idx / C;
+        const int c = (int)(idx - r * C);
+        const int b = (int)(r / NP), p = (int)(r - (long long)b * NP);
+        const float v = denc[((long long)b * T + 1 + p) * C + c];
+        if constexpr (sizeof(TO) == 2) out[idx] = f2bf(v); else out[idx] = v;
+    }
+}
+// dcls[c] += sum_b denc[b,0,c];  dwpe[t,c] += sum_b denc[b,t,c];  dpatch_b[c] += sum_{b,t>0} denc
+__global__ void patch_small_grads_k(float* __restrict__ dcls, float* __restrict__ dwpe,
+                                    float* __restrict__ dpb, const float* __restrict__ denc, int B,
+                                    int T, int C) {
+    const long long n = (long long)T * C;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < n;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int t = (int)(idx / C), c = (int)(idx - (long long)t * C);
+        float s = 0.f;
+        for (int b = 0; b < B; b++) s += denc[((long long)b * T + t) * C + c];
+        dwpe[idx] += s;
+        if (t == 0) dcls[c] += s;
+        else atomicAdd(dpb + c, s);
+    }
+}
+
+// ------------------------------------------------------------------ launch helpers (internal)
+void ln_forward_f32(float* out, float* mean, float* rstd, const float* inp, const float* w,
+                    const float* b, long long rows, int C, hipStream_t s) {
+    if (rows <= 0) return;
+    ln_fwd_k<float><<<cdiv(rows, 4), 256, 0, s>>>(out, mean, rstd, inp, w, b, rows, C);
+    after_launch("layernorm_forward");
+}
+void ln_forward_bf16(bf16_t* out, float* mean, float* rstd, const float* inp, const float* w,
+                     const float* b, long long rows, int C, hipStream_t s) {
+    if (rows <= 0) return;
+    ln_fwd_k<bf16_t><<<cdiv(rows, 4), 256, 0, s>>>(out, mean, rstd, inp, w, b, rows, C);
+    after_launch("layernorm_forward_bf16");
+}
+static int ln_bwd_grid(long long rows) {
+    long long g = (rows + 31) / 32;  // ~8 rows per wave
+    return (int)(g < 1 ? 1 : (g > 2048 ? 2048 : g));
+}
+void ln_backward_f32(float* dinp, float* dw, float* db, const float* dout, const float* inp,
+                     const float* w, const float* mean, const float* rstd, long long rows, int C,
+                     hipStream_t s) {
+    if (rows <= 0) return;
+    ln_bwd_k<float><<<ln_bwd_grid(rows), 256, 2 * C * sizeof(float), s>>>(
+        dinp, nullptr, nullptr, dw, db, dout, inp, w, mean, rstd, rows, C);
+    after_launch("layernorm_backward");
+}
+void ln_backward_fused(float* dres_out, bf16_t* dres_out_bf, const float* dres_in, float* dw,
+                       float* db, const float* dout, const float* inp, const float* w,
+                       const float* mean, const float* rstd, long long rows, int C, hipStream_t s) {
+    if (rows <= 0) return;
+    ln_bwd_k<float><<<ln_bwd_grid(rows), 256, 2 * C * sizeof(float), s>>>(
+        dres_out, dres_out_bf, dres_in, dw, db, dout, inp, w, mean, rstd, rows, C);
+    after_launch("layernorm_backward_fused");
+}
+void convert_f2bf(bf16_t* out, const float* inp, long long n, hipStream_t s) {
+    if (n <= 0) return;
+    f2bf_k<<<grid_for(n, 256), 256, 0, s>>>(out, inp, n);
+    after_launch("convert_f32_to_bf16");
+}
+void sgd(float* p, const float* g, long long n, float lr, hipStream_t s) {
+    if (n <= 0) return;
+    sgd_k<<<grid_for(n, 256), 256, 0, s>>>(p, g, n, lr);
+    after_launch("sgd_step");
+}
+void softmax_rows(float* probs, const float* logits, long long rows, int V, hipStream_t s) {
+    if (rows <= 0) return;
+    softmax_k<<<(unsigned)rows, 256, 0, s>>>(probs, logits, V);
+    after_launch("softmax_forward");
+}
+void ce_forward(float* losses, const float* probs, const int* targets, long long rows, int V,
+                hipStream_t s) {
+    if (rows <= 0) return;
+    ce_fwd_k<<<cdiv(rows, 256), 256, 0, s>>>(losses, probs, targets, rows, V);
+    after_launch("crossentropy_forward");
+}
+void ce_backward(float* dlogits, const float* dlosses, const float* probs, const int* targets,
+                 long long rows, int V, hipStream_t s) {
+    if (rows <= 0) return;
+    ce_bwd_k<<<grid_for(rows * V, 256), 256, 0, s>>>(dlogits, dlosses, probs, targets, rows, V);
+    after_launch("crossentropy_softmax_backward");
+}
+void im2col_f32(float* out, const float* px, int B, int IMG, int P, hipStream_t s) {
+    const long long n = (long long)B * (IMG / P) * (IMG / P) * 3 * P * P;
+    im2col_k<float><<<grid_for(n, 256), 256, 0, s>>>(out, px, B, IMG, P);
+    after_launch("im2col");
+}
+void im2col_bf16(bf16_t* out, const float* px, int B, int IMG, int P, hipStream_t s) {
+    const long long n = (long long)B * (IMG / P) * (IMG / P) * 3 * P * P;
+    im2col_k<bf16_t><<<grid_for(n, 256), 256, 0, s>>>(out, px, B, IMG, P);
+    after_launch("im2col_bf16");
+}
+void patch_assemble(float* enc, const float* emb, const float* cls, const float* wpe, int B,
+                    int NP, int C, hipStream_t s) {
+    const long long n = (long long)B * (NP + 1) * C;
+    patch_assemble_k<<<grid_for(n, 256), 256, 0, s>>>(enc, emb, cls, wpe, B, NP, C);
+    after_launch("patch_assemble");
+}
+void patch_gather_f32(float* out, const float* denc, int B, int NP, int C, hipStream_t s) {
+    const long long n = (long long)B * NP * C;
+    patch_gather_k<float><<<grid_for(n, 256), 256, 0, s>>>(out, denc, B, NP, C);
+    after_launch("patch_gather");
+}
+void patch_gather_bf16(bf16_t* out, const float* denc, int B, int NP, int C, hipStream_t s) {
+    const long long n = (long long)B * NP * C;
+    patch_gather_k<bf16_t><<<grid_for(n, 256), 256, 0, s>>>(out, denc, B, NP, C);
+    after_launch("patch_gather_bf16");
+}
+void patch_small_grads(float* dcls, float* dwpe, float* dpb, const float* denc, int B, int T,
+                       int C, hipStream_t s) {
+    const long long n = (long long)T * C;
+    patch_small_grads_k<<<grid_for(n, 256), 256, 0, s>>>(dcls, dwpe, dpb, denc, B, T, C);
+    after_launch("patch_small_grads");
+}
+
+}  // namespace vit
+
+// ==================================================================== C ABI (fp32 reference ops)
+using namespace vit;
+extern "C" {
+
+void residual_forward(float* out, const float* inp1, const float* inp2, int N) {
+    if (N <= 0) return;
+    residual_fwd_k<<<grid_for(N, 256), 256, 0, stream()>>>(out, inp1, inp2, N);
+    after_launch("residual_forward");
+}
+void residual_backward(float* dinp1, float* dinp2, const float* dout, int N) {
+    if (N <= 0) return;
+    residual_bwd_k<<<grid_for(N, 256), 256, 0, stream()>>>(dinp1, dinp2, dout, N);
+    after_launch("residual_backward");
+}
+void gelu_forward(float* out, const float* inp, int N) {
+    if (N <= 0) return;
+    gelu_fwd_k<<<grid_for(N, 256), 256, 0, stream()>>>(out, inp, N);
+    after_launch("gelu_forward");
+}
+void gelu_backward(float* dinp, const float* inp, const float* dout, int N) {
+    if (N <= 0) return;
+    gelu_bwd_k<<<grid_for(N, 256), 256, 0, stream()>>>(dinp, inp, dout, N);
+    after_launch("gelu_backward");
+}
+void matmul_forward(float* out, const float* inp, const float* weight, const float* bias, int B,
+                    int T, int C, int OC) {
+    GemmArgs a;
+    a.A = inp; a.lda = C; a.a_kcontig = true;
+    a.B = weight; a.ldb = C; a.b_kcontig = true;
+    a.C = out; a.ldc = OC; a.bias = bias;
+    a.M = B * T; a.N = OC; a.K = C; a.epi = EPI_F32_STORE;
+    gemm_f32(a, stream());
+}
+void matmul_backward(float* dinp, float* dweight, float* dbias, const float* dout,
+                     const float* inp, const float* weight, int B, int T, int C, int OC) {
+    const int BT = B * T;
+    if (dinp) {  // dinp[BT,C] += dout[BT,OC] . W[OC,C]
+        GemmArgs a;
+        a.A = dout; a.lda = OC; a.a_kcontig = true;
+        a.B = weight; a.ldb = C; a.b_kcontig = false;
+        a.C = dinp; a.ldc = C;
+        a.M = BT; a.N = C; a.K = OC; a.epi = EPI_F32_ACC;
+        gemm_f32(a, stream());
+    }
+    {  // dweight[OC,C] += dout^T . inp   (reduction over BT, split-K atomics when large)
+        GemmArgs a;
+        a.A = dout; a.lda = OC; a.a_kcontig = false;
+        a.B = inp; a.ldb = C; a.b_kcontig = false;
+        a.C = dweight; a.ldc = C;
+        a.M = OC; a.N = C; a.K = BT;
+        a.epi = (long long)BT > 4096 ? EPI_F32_ATOMIC : EPI_F32_ACC;
+        gemm_f32(a, stream());
+    }
+    if (dbias) colsum_f32(dbias, dout, BT, OC, OC, stream());
+}
+void layernorm_forward(float* out, float* mean, float* rstd, const float* inp, const float* weight,
+                       const float* bias, int B, int T, int C) {
+    ln_forward_f32(out, mean, rstd, inp, weight, bias, (long long)B * T, C, stream());
+}
+void layernorm_backward(float* dinp, float* dweight, float* dbias, const float* dout,
+                        const float* inp, const float* weight, const float* mean, const float* rstd,
+                        int B, int T, int C) {
+    ln_backward_f32(dinp, dweight, dbias, dout, inp, weight, mean, rstd, (long long)B * T, C,
+                    stream());
+}
+void softmax_forward(float* probs, const float* logits, int B, int T, int V) {
+    softmax_rows(probs, logits, (long long)B * T, V, stream());
+}
+void crossentropy_forward(float* losses, const float* probs, const int* targets, int B, int T,
+                          int V) {
+    ce_forward(losses, probs, targets, (long long)B * T, V, stream());
+}
+void crossentropy_softmax_backward(float* dlogits, const float* dlosses, const float* probs,
+                                   const int* targets, int B, int T, int V) {
+    ce_backward(dlogits, dlosses, probs, targets, (long long)B * T, V, stream());
+}
+void patch_embed_forward(float* encoded, const float* pixels, const float* patch_w,
+                         const float* patch_b, const float* cls, const float* wpe, int B, int IMG,
+                         int P, int C) {
+    const int NP = (IMG / P) * (IMG / P), K = 3 * P * P;
+    const size_t n_patch = (size_t)B * NP * K, n_emb = (size_t)B * NP * C;
+    float* ws = (float*)workspace((n_patch + n_emb) * sizeof(float) + 256);
+    if (!ws) return;
+    float* patches = ws;
+    float* emb = ws + ((n_patch + 63) & ~(size_t)63);
+    hipStream_t s = stream();
+    im2col_f32(patches, pixels, B, IMG, P, s);
+    GemmArgs a;
+    a.A = patches; a.lda = K; a.a_kcontig = true;
+    a.B = patch_w; a.ldb = K; a.b_kcontig = true;
+    a.C = emb; a.ldc = C; a.bias = patch_b;
+    a.M = B * NP; a.N = C; a.K = K; a.epi = EPI_F32_STORE;
+    gemm_f32(a, s);
+    patch_assemble(encoded, emb, cls, wpe, B, NP, C, s);
+}
+void patch_embed_backward(float* dpatch_w, float* dpatch_b, float* dcls, float* dwpe,
+                          const float* dencoded, const float* pixels, int B, int IMG, int P, int C) {
+    const int NP = (IMG / P) * (IMG / P), K = 3 * P * P, T = NP + 1;
+    const size_t n_patch = (size_t)B * NP * K, n_g = (size_t)B * NP * C;
+    float* ws = (float*)workspace((n_patch + n_g) * sizeof(float) + 256);
+    if (!ws) return;
+    float* patches = ws;
+    float* g = ws + ((n_patch + 63) & ~(size_t)63);
+    hipStream_t s = stream();
+    im2col_f32(patches, pixels, B, IMG, P, s);
+    patch_gather_f32(g, dencoded, B, NP, C, s);
+    GemmArgs a;  // dpatch_w[C,K] += g^T . patches
+    a.A = g; a.lda = C; a.a_kcontig = false;
+    a.B = patches; a.ldb = K; a.b_kcontig = false;
+    a.C = dpatch_w; a.ldc = K;
+    a.M = C; a.N = K; a.K = B * NP;
+    a.epi = (long long)B * NP > 4096 ? EPI_F32_ATOMIC : EPI_F32_ACC;
+    gemm_f32(a, s);
+    patch_small_grads(dcls, dwpe, dpatch_b, dencoded, B, T, C, s);
+}
+void sgd_step(float* params, const float* grads, long long n, float lr) {
+    sgd(params, grads, n, lr, stream());
+}
+
+// ---------------------------------------------------------------- bf16 extensions
+void matmul_forward_bf16(uint16_t* out, const uint16_t* inp, const uint16_t* weight,
+                         const float* bias, int B, int T, int C, int OC) {
+    GemmArgs a;
+    a.A = inp; a.lda = C; a.a_kcontig = true;
+    a.B = weight; a.ldb = C; a.b_kcontig = true;
+    a.C = out; a.ldc = OC; a.bias = bias;
+    a.M = B * T; a.N = OC; a.K = C; a.epi = EPI_BF16_STORE;
+    gemm_bf16(a, stream());
+}
+void matmul_backward_bf16(float* dinp, float* dweight, float* dbias, const uint16_t* dout,
+                          const uint16_t* inp, const uint16_t* weight, int B, int T, int C, int OC) {
+    const int BT = B * T;
+    if (dinp) {
+        GemmArgs a;
+        a.A = dout; a.lda = OC; a.a_kcontig = true;
+        a.B = weight; a.ldb = C; a.b_kcontig = false;
+        a.C = dinp; a.ldc = C;
+        a.M = BT; a.N = C; a.K = OC; a.epi = EPI_F32_ACC;
+        gemm_bf16(a, stream());
+    }
+    {
+        GemmArgs a;
+        a.A = dout; a.lda = OC; a.a_kcontig = false;
+        a.B = inp; a.ldb = C; a.b_kcontig = false;
+        a.C = dweight; a.ldc = C;
+        a.M = OC; a.N = C; a.K = BT; a.epi = EPI_F32_ATOMIC;
+        gemm_bf16(a, stream());
+    }
+    if (dbias) colsum_bf16(dbias, dout, BT, OC, OC, stream());
+}
+void layernorm_forward_bf16(uint16_t* out, float* mean, float* rstd, const float* inp,
+                            const float* weight, const float* bias, int B, int T, int C) {
+    ln_forward_bf16(out, mean, rstd, inp, weight, bias, (long long)B * T, C, stream());
+}
+void convert_f32_to_bf16(uint16_t* out, const float* inp, long long n) {
+    convert_f2bf(out, inp, n, stream());
+}
+void convert_bf16_to_f32(float* out, const uint16_t* inp, long long n) {
+    if (n <= 0) return;
+    bf2f_k<<<grid_for(n, 256), 256, 0, stream()>>>(out, inp, n);
+    after_launch("convert_bf16_to_f32");
+}
+
+}  // extern "C"

@@ -1,0 +1,46 @@
+// ops_internal.h — stream-explicit launchers shared by the C-ABI ops and the trainer.
+#pragma once
+#include "common.h"
+#include "gemm.h"
+#include "../../include/vit_ops.h"
+
+namespace vit {
+int grid_for(long long n, int threads);
+void ln_forward_f32(float* out, float* mean, float* rstd, const float* inp, const float* w,
+                    const float* b, long long rows, int C, hipStream_t s);
+void ln_forward_bf16(bf16_t* out, float* mean, float* rstd, const float* inp, const float* w,
+                     const float* b, long long rows, int C, hipStream_t s);
+void ln_backward_f32(float* dinp, float* dw, float* db, const float* dout, const float* inp,
+                     const float* w, const float* mean, const float* rstd, long long rows, int C,
+                     hipStream_t s);
+// dres_out = dres_in + LN_dinp(dout);  dres_out_bf = bf16(dres_out) (nullable)
+void ln_backward_fused(float* dres_out, bf16_t* dres_out_bf, const float* dres_in, float* dw,
+                       float* db, const float* dout, const float* inp, const float* w,
+                       const float* mean, const float* rstd, long long rows, int C, hipStream_t s);
+void convert_f2bf(bf16_t* out, const float* inp, long long n, hipStream_t s);
+void sgd(float* p, const float* g, long long n, float lr, hipStream_t s);
+void softmax_rows(float* probs, const float* logits, long long rows, int V, hipStream_t s);
+void ce_forward(float* losses, const float* probs, const int* targets, long long rows, int V,
+                hipStream_t s);
+void ce_backward(float* dlogits, const float* dlosses, const float* probs, const int* targets,
+                 long long rows, int V, hipStream_t s);
+void im2col_f32(float* out, const float* px, int B, int IMG, int P, hipStream_t s);
+void im2col_bf16(bf16_t* out, const float* px, int B, int IMG, int P, hipStream_t s);
+void patch_assemble(float* enc, const float* emb, const float* cls, const float* wpe, int B,
+                    int NP, int C, hipStream_t s);
+void patch_gather_f32(float* out, const float* denc, int B, int NP, int C, hipStream_t s);
+void patch_gather_bf16(bf16_t* out, const float* denc, int B, int NP, int C, hipStream_t s);
+void patch_small_grads(float* dcls, float* dwpe, float* dpb, const float* denc, int B, int T,
+                       int C, hipStream_t s);
+// attention.hip
+void attn_forward_f32(float* out, float* preatt, float* att, const float* inp, int B, int T, int C,
+                      int NH, hipStream_t s);
+void attn_backward_f32(float* dinp, float* dpreatt, float* datt, const float* dout,
+                       const float* inp, const float* att, int B, int T, int C, int NH,
+                       hipStream_t s);
+bool attn_fused_supported(int T, int C, int NH);
+void attn_forward_fused(bf16_t* out, float* lse, const bf16_t* qkv, int B, int T, int C, int NH,
+                        hipStream_t s);
+void attn_backward_fused(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t* out,
+                         const float* lse, int B, int T, int C, int NH, hipStream_t s);
+}  // namespace vit

@@ -1,0 +1,892 @@
+// trainer.hip — native ViT training step (include/vit_trainer.h).
+//
+// Host orchestration of the reference's ViT::forward / ViT::backward / optimizer_step
+// (/root/reference/train_vit.rs:188-373, 737-743) over the HIP kernels of this library, with
+//   * one device arena for params and one for grads, layer-major in REVERSE layer order
+//     [head | layer L-1 | ... | layer 0 | embed] so backward finalises one contiguous range per
+//     layer; tensors 256-B aligned;
+//   * a bf16 shadow of the params (GEMM operands), refreshed by the fused SGD kernel;
+//   * data parallelism: one process per GPU, RCCL all-reduce (sum) of each finished gradient
+//     chunk on a side stream, ordered by events, overlapped with the rest of backward;
+//   * optional per-kernel-class HIP-event timing on the compute stream.
+#include <rccl/rccl.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ops_internal.h"
+#include "../../include/vit_trainer.h"
+
+namespace vit {
+namespace {
+
+enum TIdx {
+    P_PATCH_W, P_PATCH_B, P_CLS, P_WPE, P_LN1W, P_LN1B, P_QKVW, P_QKVB, P_ATTPROJW, P_ATTPROJB,
+    P_LN2W, P_LN2B, P_FCW, P_FCB, P_FCPROJW, P_FCPROJB, P_LNFW, P_LNFB, P_HEADW, P_HEADB
+};
+
+enum TimerClass {
+    TC_PATCH, TC_LN_FWD, TC_QKV_FWD, TC_ATTN_FWD, TC_PROJ_FWD, TC_FC_FWD, TC_FCPROJ_FWD, TC_HEAD,
+    TC_FCPROJ_DGRAD, TC_FCPROJ_WGRAD, TC_FC_DGRAD, TC_FC_WGRAD, TC_PROJ_DGRAD, TC_PROJ_WGRAD,
+    TC_ATTN_BWD, TC_QKV_DGRAD, TC_QKV_WGRAD, TC_LN_BWD, TC_COLSUM, TC_PATCH_BWD, TC_SGD, TC_MISC,
+    TC_COUNT
+};
+const char* kTimerNames[TC_COUNT] = {
+    "patch_embed_fwd", "layernorm_fwd", "gemm_qkv_fwd", "attention_fwd", "gemm_proj_fwd",
+    "gemm_fc_fwd", "gemm_fcproj_fwd", "head", "gemm_fcproj_dgrad", "gemm_fcproj_wgrad",
+    "gemm_fc_dgrad", "gemm_fc_wgrad", "gemm_proj_dgrad", "gemm_proj_wgrad", "attention_bwd",
+    "gemm_qkv_dgrad", "gemm_qkv_wgrad", "layernorm_bwd", "bias_colsum", "patch_embed_bwd", "sgd",
+    "misc"};
+
+__global__ void fill_k(float* p, float v, int n) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+// p -= lr*g; pbf = bf16(p)   (optimizer_step, train_vit.rs:737-743, + bf16 shadow)
+__global__ void sgd_bf16_k(float* __restrict__ p, bf16_t* __restrict__ pbf,
+                           const float* __restrict__ g, long long n, float lr) {
+    const long long n4 = n / 4;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4;
+         i += (long long)gridDim.x * blockDim.x) {
+        float4 pv = reinterpret_cast<float4*>(p)[i];
+        const float4 gv = reinterpret_cast<const float4*>(g)[i];
+        pv.x = sgd_update(pv.x, gv.x, lr); pv.y = sgd_update(pv.y, gv.y, lr);
+        pv.z = sgd_update(pv.z, gv.z, lr); pv.w = sgd_update(pv.w, gv.w, lr);
+        reinterpret_cast<float4*>(p)[i] = pv;
+        reinterpret_cast<uint2*>(pbf)[i] = make_uint2(pack_bf16x2(pv.x, pv.y), pack_bf16x2(pv.z, pv.w));
+    }
+    for (long long i = n4 * 4 + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x) {
+        p[i] = sgd_update(p[i], g[i], lr);
+        pbf[i] = f2bf(p[i]);
+    }
+}
+__global__ void to_bf16_k(bf16_t* __restrict__ out, const float* __restrict__ in, long long n) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        out[i] = f2bf(in[i]);
+}
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace
+
+struct Trainer {
+    vit_config_t cfg{};
+    int B = 0, T = 0, NP = 0, C = 0, L = 0, NH = 0, NC = 0, KP = 0, prec = 0, device = 0;
+    long long BT = 0;
+    long long n_params = 0;       // canonical count
+    long long arena_elems = 0;    // device arena (with alignment padding)
+    long long canon_size[20]{};
+    // device offsets: tensor ti, layer l (l=0 for unlayered)
+    std::vector<long long> off;   // [20 * L]
+    long long chunk_off[64 + 2]{};  // chunk c: [chunk_off[c], chunk_off[c+1]) ; c=0 head, 1..L layers L-1..0, L+1 embed
+    int n_chunks = 0;
+
+    hipStream_t s = nullptr, s_comm = nullptr;
+    std::vector<hipEvent_t> chunk_ev;
+    hipEvent_t comm_done = nullptr;
+
+    float* params = nullptr;
+    float* grads = nullptr;
+    bf16_t* pbf = nullptr;
+    float* pixels = nullptr;
+    int* labels = nullptr;
+    std::vector<DevBuf> allocs;
+    size_t dev_bytes = 0;
+    int b_global = 0;
+
+    // ---- bf16 activations
+    struct LayerActs {
+        bf16_t *ln1, *qkv, *atty, *ln2, *fch, *fchg;
+        float *ln1_mean, *ln1_rstd, *lse, *res2, *ln2_mean, *ln2_rstd, *res3;
+        // fp32-mode extras
+        float *ln1f, *qkvf, *attyf, *preatt, *att, *attproj, *ln2f, *fchf, *fchgf, *fcproj;
+    };
+    std::vector<LayerActs> la;
+    float* encoded = nullptr;
+    bf16_t* patches_bf = nullptr;
+    float* patches_f = nullptr;
+    float* emb_tmp = nullptr;
+    float *cls_x = nullptr, *lnf = nullptr, *lnf_mean = nullptr, *lnf_rstd = nullptr;
+    float *logits = nullptr, *probs = nullptr, *losses = nullptr;
+    // grads scratch
+    float *dlosses = nullptr, *dlogits = nullptr, *dlnf = nullptr, *dcls_x = nullptr;
+    float *dres_a = nullptr, *dres_b = nullptr, *dln = nullptr;
+    bf16_t *dres_bf = nullptr, *dfch = nullptr, *datty = nullptr, *dqkv = nullptr, *dpatch_bf = nullptr;
+    float* dpatch_f = nullptr;
+    // fp32-mode per-layer grad scratch (one layer, zeroed per layer)
+    float *g_block = nullptr;
+    long long g_block_elems = 0;
+    float *g_dres2, *g_dfcproj, *g_dfchg, *g_dfch, *g_dln2, *g_dattproj, *g_datty, *g_dpreatt,
+        *g_datt, *g_dqkv, *g_dln1;
+
+    // ---- DP
+    ncclComm_t comm = nullptr;
+    int rank = 0, world = 1, overlap = 1;
+
+    // ---- timing
+    bool timing = false;
+    struct Rec { int cls; hipEvent_t a, b; };
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
+    std::vector<Rec> recs;
+    double t_ms[TC_COUNT]{};
+    long long t_calls[TC_COUNT]{};
+    double t_flops[TC_COUNT]{};
+
+    // ------------------------------------------------------------------------------
+    template <typename TT>
+    TT* alloc(long long elems) {
+        size_t bytes = (size_t)std::max<long long>(elems, 1) * sizeof(TT);
+        bytes = (bytes + 255) & ~(size_t)255;
+        void* p = nullptr;
+        if (hipMalloc(&p, bytes) != hipSuccess) {
+            set_error("trainer: hipMalloc(%zu) failed", bytes);
+            return nullptr;
+        }
+        allocs.push_back({p, bytes});
+        dev_bytes += bytes;
+        return (TT*)p;
+    }
+
+    bool layered(int ti) const { return ti >= P_LN1W && ti <= P_FCPROJB; }
+    long long per_layer(int ti) const { return canon_size[ti] / L; }
+    float* P(int ti, int l = 0) const { return params + off[ti * L + l]; }
+    float* G(int ti, int l = 0) const { return grads + off[ti * L + l]; }
+    bf16_t* W(int ti, int l = 0) const { return pbf + off[ti * L + l]; }
+
+    void build_layout() {
+        const long long C_ = C, K = KP;
+        long long sz[20] = {C_ * K, C_, C_, (long long)T * C_,
+                            L * C_, L * C_, L * 3 * C_ * C_, L * 3 * C_, L * C_ * C_, L * C_,
+                            L * C_, L * C_, L * 4 * C_ * C_, L * 4 * C_, L * C_ * 4 * C_, L * C_,
+                            C_, C_, (long long)NC * C_, NC};
+        n_params = 0;
+        for (int i = 0; i < 20; i++) {
+            canon_size[i] = sz[i];
+            n_params += sz[i];
+        }
+        off.assign(20 * L, 0);
+        long long cur = 0;
+        auto place = [&](int ti, int l, long long n) {
+            off[ti * L + l] = cur;
+            cur += (n + 63) & ~63LL;
+        };
+        n_chunks = L + 2;
+        chunk_off[0] = 0;
+        const int head[4] = {P_HEADW, P_HEADB, P_LNFW, P_LNFB};
+        for (int ti : head) place(ti, 0, canon_size[ti]);
+        chunk_off[1] = cur;
+        for (int c = 1; c <= L; c++) {
+            const int l = L - c;
+            for (int ti = P_LN1W; ti <= P_FCPROJB; ti++) place(ti, l, per_layer(ti));
+            chunk_off[c + 1] = cur;
+        }
+        const int emb[4] = {P_PATCH_W, P_PATCH_B, P_CLS, P_WPE};
+        for (int ti : emb) place(ti, 0, canon_size[ti]);
+        chunk_off[L + 2] = cur;
+        arena_elems = cur;
+    }
+
+    // canonical <-> device copies (host staging)
+    void canon_to_device(const float* host, float* dev) {
+        std::vector<float> stage((size_t)arena_elems, 0.f);
+        long long c = 0;
+        for (int ti = 0; ti < 20; ti++) {
+            if (layered(ti)) {
+                const long long n = per_layer(ti);
+                for (int l = 0; l < L; l++, c += n) memcpy(&stage[off[ti * L + l]], host + c, n * 4);
+            } else {
+                memcpy(&stage[off[ti * L]], host + c, canon_size[ti] * 4);
+                c += canon_size[ti];
+            }
+        }
+        VIT_HIP(hipMemcpyAsync(dev, stage.data(), arena_elems * 4, hipMemcpyHostToDevice, s));
+        VIT_HIP(hipStreamSynchronize(s));
+    }
+    void device_to_canon(const float* dev, float* host) {
+        std::vector<float> stage((size_t)arena_elems);
+        VIT_HIP(hipMemcpyAsync(stage.data(), dev, arena_elems * 4, hipMemcpyDeviceToHost, s));
+        VIT_HIP(hipStreamSynchronize(s));
+        long long c = 0;
+        for (int ti = 0; ti < 20; ti++) {
+            if (layered(ti)) {
+                const long long n = per_layer(ti);
+                for (int l = 0; l < L; l++, c += n) memcpy(host + c, &stage[off[ti * L + l]], n * 4);
+            } else {
+                memcpy(host + c, &stage[off[ti * L]], canon_size[ti] * 4);
+                c += canon_size[ti];
+            }
+        }
+    }
+
+    // ---- timing helpers
+    void tbeg(int cls, double flops) {
+        if (!timing) return;
+        if (ev_used + 2 > ev_pool.size()) {
+            for (int k = 0; k < 64; k++) {
+                hipEvent_t e;
+                VIT_HIP(hipEventCreate(&e));
+                ev_pool.push_back(e);
+            }
+        }
+        Rec r{cls, ev_pool[ev_used], ev_pool[ev_used + 1]};
+        ev_used += 2;
+        VIT_HIP(hipEventRecord(r.a, s));
+        recs.push_back(r);
+        t_flops[cls] += flops;
+    }
+    void tend() {
+        if (!timing) return;
+        VIT_HIP(hipEventRecord(recs.back().b, s));
+    }
+    void collect() {
+        if (recs.empty()) return;
+        VIT_HIP(hipStreamSynchronize(s));
+        for (auto& r : recs) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+                t_ms[r.cls] += ms;
+                t_calls[r.cls] += 1;
+            }
+        }
+        recs.clear();
+        ev_used = 0;
+    }
+
+    void gemm(int cls, GemmArgs a, bool bf) {
+        tbeg(cls, 2.0 * a.M * (double)a.N * a.K);
+        if (bf) gemm_bf16(a, s); else gemm_f32(a, s);
+        tend();
+    }
+
+    // ------------------------------------------------------------------------------
+    bool init(const vit_config_t* c, int batch, int precision, int dev) {
+        cfg = *c;
+        B = batch;
+        C = c->channels; L = c->num_layers; NH = c->num_heads; NC = c->num_classes;
+        NP = (c->img / c->patch) * (c->img / c->patch);
+        T = NP + 1;
+        KP = 3 * c->patch * c->patch;
+        BT = (long long)B * T;
+        prec = precision;
+        device = dev;
+        if (c->in_ch != 3 || C % NH || L < 1 || L > 64 || B < 1) {
+            set_error("trainer: unsupported config");
+            return false;
+        }
+        if (hipSetDevice(dev) != hipSuccess) { set_error("trainer: hipSetDevice(%d)", dev); return false; }
+        VIT_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        VIT_HIP(hipStreamCreateWithFlags(&s_comm, hipStreamNonBlocking));
+        chunk_ev.resize(L + 2);
+        for (auto& e : chunk_ev) VIT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        VIT_HIP(hipEventCreateWithFlags(&comm_done, hipEventDisableTiming));
+        build_layout();
+        params = alloc<float>(arena_elems);
+        grads = alloc<float>(arena_elems);
+        pixels = alloc<float>((long long)B * 3 * c->img * c->img);
+        labels = alloc<int>(B);
+        encoded = alloc<float>(BT * C);
+        cls_x = alloc<float>((long long)B * C);
+        lnf = alloc<float>((long long)B * C);
+        lnf_mean = alloc<float>(B);
+        lnf_rstd = alloc<float>(B);
+        logits = alloc<float>((long long)B * NC);
+        probs = alloc<float>((long long)B * NC);
+        losses = alloc<float>(B);
+        dlosses = alloc<float>(B);
+        dlogits = alloc<float>((long long)B * NC);
+        dlnf = alloc<float>((long long)B * C);
+        dcls_x = alloc<float>((long long)B * C);
+        dres_a = alloc<float>(BT * C);
+        dres_b = alloc<float>(BT * C);
+        emb_tmp = alloc<float>((long long)B * NP * C);
+        la.resize(L);
+        if (prec == VIT_BF16) {
+            if (!attn_fused_supported(T, C, NH) || C % 8 || KP % 8) {
+                set_error("trainer: bf16 path needs head size 64, T<=256, C%%8==0 (T=%d C=%d NH=%d)", T, C, NH);
+                return false;
+            }
+            pbf = alloc<bf16_t>(arena_elems);
+            patches_bf = alloc<bf16_t>((long long)B * NP * KP);
+            for (int l = 0; l < L; l++) {
+                LayerActs& a = la[l];
+                a.ln1 = alloc<bf16_t>(BT * C);
+                a.ln1_mean = alloc<float>(BT);
+                a.ln1_rstd = alloc<float>(BT);
+                a.qkv = alloc<bf16_t>(BT * 3 * C);
+                a.atty = alloc<bf16_t>(BT * C);
+                a.lse = alloc<float>(BT * NH);
+                a.res2 = alloc<float>(BT * C);
+                a.ln2 = alloc<bf16_t>(BT * C);
+                a.ln2_mean = alloc<float>(BT);
+                a.ln2_rstd = alloc<float>(BT);
+                a.fch = alloc<bf16_t>(BT * 4 * C);
+                a.fchg = alloc<bf16_t>(BT * 4 * C);
+                a.res3 = alloc<float>(BT * C);
+            }
+            dln = alloc<float>(BT * C);
+            dres_bf = alloc<bf16_t>(BT * C);
+            dfch = alloc<bf16_t>(BT * 4 * C);
+            datty = alloc<bf16_t>(BT * C);
+            dqkv = alloc<bf16_t>(BT * 3 * C);
+            dpatch_bf = alloc<bf16_t>((long long)B * NP * C);
+        } else {
+            patches_f = alloc<float>((long long)B * NP * KP);
+            dpatch_f = alloc<float>((long long)B * NP * C);
+            const long long att_n = BT * NH * T;
+            for (int l = 0; l < L; l++) {
+                LayerActs& a = la[l];
+                a.ln1f = alloc<float>(BT * C);
+                a.ln1_mean = alloc<float>(BT);
+                a.ln1_rstd = alloc<float>(BT);
+                a.qkvf = alloc<float>(BT * 3 * C);
+                a.attyf = alloc<float>(BT * C);
+                a.preatt = alloc<float>(att_n);
+                a.att = alloc<float>(att_n);
+                a.attproj = alloc<float>(BT * C);
+                a.res2 = alloc<float>(BT * C);
+                a.ln2f = alloc<float>(BT * C);
+                a.ln2_mean = alloc<float>(BT);
+                a.ln2_rstd = alloc<float>(BT);
+                a.fchf = alloc<float>(BT * 4 * C);
+                a.fchgf = alloc<float>(BT * 4 * C);
+                a.fcproj = alloc<float>(BT * C);
+                a.res3 = alloc<float>(BT * C);
+            }
+            // one layer of reference grads_acts (train_vit.rs:346-357), zeroed per layer
+            const long long sizes[11] = {BT * C, BT * C, BT * 4 * C, BT * 4 * C, BT * C, BT * C,
+                                         BT * C, att_n, att_n, BT * 3 * C, BT * C};
+            float** slots[11] = {&g_dres2, &g_dfcproj, &g_dfchg, &g_dfch, &g_dln2, &g_dattproj,
+                                 &g_datty, &g_dpreatt, &g_datt, &g_dqkv, &g_dln1};
+            g_block_elems = 0;
+            for (int k = 0; k < 11; k++) g_block_elems += (sizes[k] + 63) & ~63LL;
+            g_block = alloc<float>(g_block_elems);
+            long long o = 0;
+            for (int k = 0; k < 11; k++) {
+                *slots[k] = g_block ? g_block + o : nullptr;
+                o += (sizes[k] + 63) & ~63LL;
+            }
+        }
+        VIT_HIP(hipMemsetAsync(grads, 0, arena_elems * 4, s));
+        VIT_HIP(hipStreamSynchronize(s));
+        return !has_error();
+    }
+
+    void destroy() {
+        if (s) (void)hipStreamSynchronize(s);
+        if (s_comm) (void)hipStreamSynchronize(s_comm);
+        if (comm) ncclCommDestroy(comm);
+        for (auto& a : allocs) (void)hipFree(a.p);
+        for (auto e : chunk_ev) (void)hipEventDestroy(e);
+        for (auto e : ev_pool) (void)hipEventDestroy(e);
+        if (comm_done) (void)hipEventDestroy(comm_done);
+        if (s) (void)hipStreamDestroy(s);
+        if (s_comm) (void)hipStreamDestroy(s_comm);
+    }
+
+    void refresh_bf16() {
+        if (prec != VIT_BF16) return;
+        to_bf16_k<<<grid_for(arena_elems, 256), 256, 0, s>>>(pbf, params, arena_elems);
+        after_launch("params_to_bf16");
+    }
+
+    // ------------------------------------------------------------------ head (both modes)
+    void head_forward() {
+        tbeg(TC_HEAD, 2.0 * B * C * NC);
+        // lnf on the CLS row of each image (D15)
+        const float* last = la[L - 1].res3;
+        VIT_HIP(hipMemcpy2DAsync(cls_x, C * 4, last, (size_t)T * C * 4, C * 4, B, hipMemcpyDeviceToDevice, s));
+        ln_forward_f32(lnf, lnf_mean, lnf_rstd, cls_x, P(P_LNFW), P(P_LNFB), B, C, s);
+        GemmArgs a;
+        a.A = lnf; a.lda = C; a.B = P(P_HEADW); a.ldb = C; a.C = logits; a.ldc = NC;
+        a.bias = P(P_HEADB); a.M = B; a.N = NC; a.K = C; a.epi = EPI_F32_STORE;
+        gemm_f32(a, s);
+        softmax_rows(probs, logits, B, NC, s);
+        ce_forward(losses, probs, labels, B, NC, s);
+        tend();
+    }
+    // dres_cur (zeroed) <- lnf backward on CLS rows
+    void head_backward(float* dres) {
+        tbeg(TC_HEAD, 4.0 * B * C * NC);
+        fill_k<<<cdiv(B, 256), 256, 0, s>>>(dlosses, 1.0f / (float)b_global, B);
+        VIT_HIP(hipMemsetAsync(dlogits, 0, (size_t)B * NC * 4, s));
+        ce_backward(dlogits, dlosses, probs, labels, B, NC, s);
+        VIT_HIP(hipMemsetAsync(dlnf, 0, (size_t)B * C * 4, s));
+        GemmArgs a;  // dlnf += dlogits . head_w
+        a.A = dlogits; a.lda = NC; a.a_kcontig = true;
+        a.B = P(P_HEADW); a.ldb = C; a.b_kcontig = false;
+        a.C = dlnf; a.ldc = C; a.M = B; a.N = C; a.K = NC; a.epi = EPI_F32_ACC;
+        gemm_f32(a, s);
+        GemmArgs w;  // dhead_w += dlogits^T . lnf
+        w.A = dlogits; w.lda = NC; w.a_kcontig = false;
+        w.B = lnf; w.ldb = C; w.b_kcontig = false;
+        w.C = G(P_HEADW); w.ldc = C; w.M = NC; w.N = C; w.K = B; w.epi = EPI_F32_ACC;
+        gemm_f32(w, s);
+        colsum_f32(G(P_HEADB), dlogits, B, NC, NC, s);
+        VIT_HIP(hipMemsetAsync(dcls_x, 0, (size_t)B * C * 4, s));
+        ln_backward_f32(dcls_x, G(P_LNFW), G(P_LNFB), dlnf, cls_x, P(P_LNFW), lnf_mean, lnf_rstd, B, C, s);
+        VIT_HIP(hipMemsetAsync(dres, 0, (size_t)BT * C * 4, s));
+        VIT_HIP(hipMemcpy2DAsync(dres, (size_t)T * C * 4, dcls_x, C * 4, C * 4, B, hipMemcpyDeviceToDevice, s));
+        tend();
+    }
+
+    // ------------------------------------------------------------------ bf16 fast path
+    void forward_bf16() {
+        const double BTd = (double)BT;
+        // patch embedding (encoder_forward, train_vit.rs:196 -> ViT)
+        tbeg(TC_PATCH, 2.0 * B * NP * (double)KP * C);
+        im2col_bf16(patches_bf, pixels, B, cfg.img, cfg.patch, s);
+        {
+            GemmArgs a;
+            a.A = patches_bf; a.lda = KP; a.B = W(P_PATCH_W); a.ldb = KP;
+            a.C = emb_tmp; a.ldc = C; a.bias = P(P_PATCH_B);
+            a.M = B * NP; a.N = C; a.K = KP; a.epi = EPI_F32_STORE;
+            gemm_bf16(a, s);
+        }
+        patch_assemble(encoded, emb_tmp, P(P_CLS), P(P_WPE), B, NP, C, s);
+        tend();
+        for (int l = 0; l < L; l++) {
+            LayerActs& a = la[l];
+            const float* x = l == 0 ? encoded : la[l - 1].res3;
+            tbeg(TC_LN_FWD, 0);
+            ln_forward_bf16(a.ln1, a.ln1_mean, a.ln1_rstd, x, P(P_LN1W, l), P(P_LN1B, l), BT, C, s);
+            tend();
+            GemmArgs q;
+            q.A = a.ln1; q.lda = C; q.B = W(P_QKVW, l); q.ldb = C; q.C = a.qkv; q.ldc = 3 * C;
+            q.bias = P(P_QKVB, l); q.M = (int)BT; q.N = 3 * C; q.K = C; q.epi = EPI_BF16_STORE;
+            gemm(TC_QKV_FWD, q, true);
+            tbeg(TC_ATTN_FWD, 4.0 * B * (double)T * T * C);
+            attn_forward_fused(a.atty, a.lse, a.qkv, B, T, C, NH, s);
+            tend();
+            GemmArgs pr;
+            pr.A = a.atty; pr.lda = C; pr.B = W(P_ATTPROJW, l); pr.ldb = C; pr.C = a.res2; pr.ldc = C;
+            pr.bias = P(P_ATTPROJB, l); pr.aux = x; pr.ldaux = C;
+            pr.M = (int)BT; pr.N = C; pr.K = C; pr.epi = EPI_F32_RESID;
+            gemm(TC_PROJ_FWD, pr, true);
+            tbeg(TC_LN_FWD, 0);
+            ln_forward_bf16(a.ln2, a.ln2_mean, a.ln2_rstd, a.res2, P(P_LN2W, l), P(P_LN2B, l), BT, C, s);
+            tend();
+            GemmArgs f;
+            f.A = a.ln2; f.lda = C; f.B = W(P_FCW, l); f.ldb = C; f.C = a.fch; f.C2 = a.fchg;
+            f.ldc = 4 * C; f.bias = P(P_FCB, l); f.M = (int)BT; f.N = 4 * C; f.K = C; f.epi = EPI_BF16_GELU;
+            gemm(TC_FC_FWD, f, true);
+            GemmArgs fp;
+            fp.A = a.fchg; fp.lda = 4 * C; fp.B = W(P_FCPROJW, l); fp.ldb = 4 * C; fp.C = a.res3;
+            fp.ldc = C; fp.bias = P(P_FCPROJB, l); fp.aux = a.res2; fp.ldaux = C;
+            fp.M = (int)BT; fp.N = C; fp.K = 4 * C; fp.epi = EPI_F32_RESID;
+            gemm(TC_FCPROJ_FWD, fp, true);
+        }
+        (void)BTd;
+        head_forward();
+    }
+
+    void wgrad(int cls, const bf16_t* dout, int OC, const bf16_t* inp, int Cin, float* dW) {
+        GemmArgs w;  // dW[OC,Cin] += dout^T . inp   (reduction over B*T rows)
+        w.A = dout; w.lda = OC; w.a_kcontig = false;
+        w.B = inp; w.ldb = Cin; w.b_kcontig = false;
+        w.C = dW; w.ldc = Cin; w.M = OC; w.N = Cin; w.K = (int)BT; w.epi = EPI_F32_ATOMIC;
+        gemm(cls, w, true);
+    }
+
+    void backward_bf16() {
+        float* dcur = dres_a;
+        float* dnxt = dres_b;
+        head_backward(dcur);
+        chunk_done(0);
+        convert_f2bf(dres_bf, dcur, BT * C, s);
+        for (int l = L - 1; l >= 0; l--) {
+            LayerActs& a = la[l];
+            const float* x = l == 0 ? encoded : la[l - 1].res3;
+            // fcproj: dfch = (dres3 . fcprojw) * gelu'(fch)
+            GemmArgs d1;
+            d1.A = dres_bf; d1.lda = C; d1.B = W(P_FCPROJW, l); d1.ldb = 4 * C; d1.b_kcontig = false;
+            d1.C = dfch; d1.ldc = 4 * C; d1.aux = a.fch; d1.ldaux = 4 * C;
+            d1.M = (int)BT; d1.N = 4 * C; d1.K = C; d1.epi = EPI_BF16_DGELU;
+            gemm(TC_FCPROJ_DGRAD, d1, true);
+            wgrad(TC_FCPROJ_WGRAD, dres_bf, C, a.fchg, 4 * C, G(P_FCPROJW, l));
+            tbeg(TC_COLSUM, 0);
+            colsum_f32(G(P_FCPROJB, l), dcur, (int)BT, C, C, s);
+            tend();
+            // fc: dln2 = dfch . fcw
+            GemmArgs d2;
+            d2.A = dfch; d2.lda = 4 * C; d2.B = W(P_FCW, l); d2.ldb = C; d2.b_kcontig = false;
+            d2.C = dln; d2.ldc = C; d2.M = (int)BT; d2.N = C; d2.K = 4 * C; d2.epi = EPI_F32_STORE;
+            gemm(TC_FC_DGRAD, d2, true);
+            wgrad(TC_FC_WGRAD, dfch, 4 * C, a.ln2, C, G(P_FCW, l));
+            tbeg(TC_COLSUM, 0);
+            colsum_bf16(G(P_FCB, l), dfch, (int)BT, 4 * C, 4 * C, s);
+            tend();
+            // ln2 backward + residual: dres2 = dres3 + LN2'(dln2)
+            tbeg(TC_LN_BWD, 0);
+            ln_backward_fused(dnxt, dres_bf, dcur, G(P_LN2W, l), G(P_LN2B, l), dln, a.res2,
+                              P(P_LN2W, l), a.ln2_mean, a.ln2_rstd, BT, C, s);
+            tend();
+            std::swap(dcur, dnxt);
+            // attproj
+            GemmArgs d3;
+            d3.A = dres_bf; d3.lda = C; d3.B = W(P_ATTPROJW, l); d3.ldb = C; d3.b_kcontig = false;
+            d3.C = datty; d3.ldc = C; d3.M = (int)BT; d3.N = C; d3.K = C; d3.epi = EPI_BF16_STORE;
+            gemm(TC_PROJ_DGRAD, d3, true);
+            wgrad(TC_PROJ_WGRAD, dres_bf, C, a.atty, C, G(P_ATTPROJW, l));
+            tbeg(TC_COLSUM, 0);
+            colsum_f32(G(P_ATTPROJB, l), dcur, (int)BT, C, C, s);
+            tend();
+            // attention
+            tbeg(TC_ATTN_BWD, 8.0 * B * (double)T * T * C);
+            attn_backward_fused(dqkv, datty, a.qkv, a.atty, a.lse, B, T, C, NH, s);
+            tend();
+            // qkv
+            GemmArgs d4;
+            d4.A = dqkv; d4.lda = 3 * C; d4.B = W(P_QKVW, l); d4.ldb = C; d4.b_kcontig = false;
+            d4.C = dln; d4.ldc = C; d4.M = (int)BT; d4.N = C; d4.K = 3 * C; d4.epi = EPI_F32_STORE;
+            gemm(TC_QKV_DGRAD, d4, true);
+            wgrad(TC_QKV_WGRAD, dqkv, 3 * C, a.ln1, C, G(P_QKVW, l));
+            tbeg(TC_COLSUM, 0);
+            colsum_bf16(G(P_QKVB, l), dqkv, (int)BT, 3 * C, 3 * C, s);
+            tend();
+            tbeg(TC_LN_BWD, 0);
+            ln_backward_fused(dnxt, dres_bf, dcur, G(P_LN1W, l), G(P_LN1B, l), dln, x, P(P_LN1W, l),
+                              a.ln1_mean, a.ln1_rstd, BT, C, s);
+            tend();
+            std::swap(dcur, dnxt);
+            chunk_done(L - l);
+        }
+        // patch embedding backward (encoder_backward, train_vit.rs:371 -> ViT)
+        tbeg(TC_PATCH_BWD, 2.0 * B * NP * (double)KP * C);
+        patch_gather_bf16(dpatch_bf, dcur, B, NP, C, s);
+        {
+            GemmArgs w;
+            w.A = dpatch_bf; w.lda = C; w.a_kcontig = false;
+            w.B = patches_bf; w.ldb = KP; w.b_kcontig = false;
+            w.C = G(P_PATCH_W); w.ldc = KP; w.M = C; w.N = KP; w.K = B * NP; w.epi = EPI_F32_ATOMIC;
+            gemm_bf16(w, s);
+        }
+        patch_small_grads(G(P_CLS), G(P_WPE), G(P_PATCH_B), dcur, B, T, C, s);
+        tend();
+        chunk_done(L + 1);
+    }
+
+    // ------------------------------------------------------------------ fp32 reference path
+    void forward_f32() {
+        im2col_f32(patches_f, pixels, B, cfg.img, cfg.patch, s);
+        {
+            GemmArgs a;
+            a.A = patches_f; a.lda = KP; a.B = P(P_PATCH_W); a.ldb = KP; a.C = emb_tmp; a.ldc = C;
+            a.bias = P(P_PATCH_B); a.M = B * NP; a.N = C; a.K = KP; a.epi = EPI_F32_STORE;
+            gemm_f32(a, s);
+        }
+        patch_assemble(encoded, emb_tmp, P(P_CLS), P(P_WPE), B, NP, C, s);
+        for (int l = 0; l < L; l++) {
+            LayerActs& a = la[l];
+            const float* x = l == 0 ? encoded : la[l - 1].res3;
+            ln_forward_f32(a.ln1f, a.ln1_mean, a.ln1_rstd, x, P(P_LN1W, l), P(P_LN1B, l), BT, C, s);
+            mm_fwd(a.qkvf, a.ln1f, P(P_QKVW, l), P(P_QKVB, l), C, 3 * C);
+            attn_forward_f32(a.attyf, a.preatt, a.att, a.qkvf, B, T, C, NH, s);
+            mm_fwd(a.attproj, a.attyf, P(P_ATTPROJW, l), P(P_ATTPROJB, l), C, C);
+            add(a.res2, x, a.attproj, BT * C);
+            ln_forward_f32(a.ln2f, a.ln2_mean, a.ln2_rstd, a.res2, P(P_LN2W, l), P(P_LN2B, l), BT, C, s);
+            mm_fwd(a.fchf, a.ln2f, P(P_FCW, l), P(P_FCB, l), C, 4 * C);
+            gelu(a.fchgf, a.fchf, BT * 4 * C);
+            mm_fwd(a.fcproj, a.fchgf, P(P_FCPROJW, l), P(P_FCPROJB, l), 4 * C, C);
+            add(a.res3, a.res2, a.fcproj, BT * C);
+        }
+        head_forward();
+    }
+    void mm_fwd(float* out, const float* inp, const float* w, const float* b, int Cin, int OC) {
+        GemmArgs a;
+        a.A = inp; a.lda = Cin; a.B = w; a.ldb = Cin; a.C = out; a.ldc = OC; a.bias = b;
+        a.M = (int)BT; a.N = OC; a.K = Cin; a.epi = EPI_F32_STORE;
+        gemm_f32(a, s);
+    }
+    void mm_bwd(float* dinp, float* dw, float* db, const float* dout, const float* inp,
+                const float* w, int Cin, int OC) {
+        GemmArgs d;
+        d.A = dout; d.lda = OC; d.B = w; d.ldb = Cin; d.b_kcontig = false; d.C = dinp; d.ldc = Cin;
+        d.M = (int)BT; d.N = Cin; d.K = OC; d.epi = EPI_F32_ACC;
+        gemm_f32(d, s);
+        GemmArgs g;
+        g.A = dout; g.lda = OC; g.a_kcontig = false; g.B = inp; g.ldb = Cin; g.b_kcontig = false;
+        g.C = dw; g.ldc = Cin; g.M = OC; g.N = Cin; g.K = (int)BT; g.epi = EPI_F32_ATOMIC;
+        gemm_f32(g, s);
+        colsum_f32(db, dout, (int)BT, OC, OC, s);
+    }
+    void add(float* out, const float* a, const float* b, long long n);
+    void gelu(float* out, const float* in, long long n);
+    void gelu_bwd(float* dinp, const float* in, const float* dout, long long n);
+    void res_bwd(float* d1, float* d2, const float* dout, long long n);
+
+    void backward_f32() {
+        float* dcur = dres_a;
+        float* dnxt = dres_b;
+        head_backward(dcur);
+        chunk_done(0);
+        for (int l = L - 1; l >= 0; l--) {
+            LayerActs& a = la[l];
+            const float* x = l == 0 ? encoded : la[l - 1].res3;
+            VIT_HIP(hipMemsetAsync(g_block, 0, g_block_elems * 4, s));
+            VIT_HIP(hipMemsetAsync(dnxt, 0, BT * C * 4, s));
+            // train_vit.rs:359-368
+            res_bwd(g_dres2, g_dfcproj, dcur, BT * C);
+            mm_bwd(g_dfchg, G(P_FCPROJW, l), G(P_FCPROJB, l), g_dfcproj, a.fchgf, P(P_FCPROJW, l), 4 * C, C);
+            gelu_bwd(g_dfch, a.fchf, g_dfchg, BT * 4 * C);
+            mm_bwd(g_dln2, G(P_FCW, l), G(P_FCB, l), g_dfch, a.ln2f, P(P_FCW, l), C, 4 * C);
+            ln_backward_f32(g_dres2, G(P_LN2W, l), G(P_LN2B, l), g_dln2, a.res2, P(P_LN2W, l),
+                            a.ln2_mean, a.ln2_rstd, BT, C, s);
+            res_bwd(dnxt, g_dattproj, g_dres2, BT * C);
+            mm_bwd(g_datty, G(P_ATTPROJW, l), G(P_ATTPROJB, l), g_dattproj, a.attyf, P(P_ATTPROJW, l), C, C);
+            attn_backward_f32(g_dqkv, g_dpreatt, g_datt, g_datty, a.qkvf, a.att, B, T, C, NH, s);
+            mm_bwd(g_dln1, G(P_QKVW, l), G(P_QKVB, l), g_dqkv, a.ln1f, P(P_QKVW, l), C, 3 * C);
+            ln_backward_f32(dnxt, G(P_LN1W, l), G(P_LN1B, l), g_dln1, x, P(P_LN1W, l), a.ln1_mean,
+                            a.ln1_rstd, BT, C, s);
+            std::swap(dcur, dnxt);
+            chunk_done(L - l);
+        }
+        im2col_f32(patches_f, pixels, B, cfg.img, cfg.patch, s);
+        patch_gather_f32(dpatch_f, dcur, B, NP, C, s);
+        GemmArgs w;
+        w.A = dpatch_f; w.lda = C; w.a_kcontig = false; w.B = patches_f; w.ldb = KP; w.b_kcontig = false;
+        w.C = G(P_PATCH_W); w.ldc = KP; w.M = C; w.N = KP; w.K = B * NP; w.epi = EPI_F32_ATOMIC;
+        gemm_f32(w, s);
+        patch_small_grads(G(P_CLS), G(P_WPE), G(P_PATCH_B), dcur, B, T, C, s);
+        chunk_done(L + 1);
+    }
+
+    // ------------------------------------------------------------------ DP
+    void chunk_done(int c) {
+        if (!comm || world <= 1 || !overlap) return;
+        VIT_HIP(hipEventRecord(chunk_ev[c], s));
+        VIT_HIP(hipStreamWaitEvent(s_comm, chunk_ev[c], 0));
+        const long long o = chunk_off[c], n = chunk_off[c + 1] - chunk_off[c];
+        ncclResult_t r = ncclAllReduce(grads + o, grads + o, (size_t)n, ncclFloat32, ncclSum, comm, s_comm);
+        if (r != ncclSuccess) set_error("ncclAllReduce(chunk %d): %s", c, ncclGetErrorString(r));
+    }
+    void finish_allreduce() {
+        if (!comm || world <= 1) return;
+        if (!overlap) {
+            ncclResult_t r = ncclAllReduce(grads, grads, (size_t)arena_elems, ncclFloat32, ncclSum, comm, s);
+            if (r != ncclSuccess) set_error("ncclAllReduce: %s", ncclGetErrorString(r));
+            return;
+        }
+        VIT_HIP(hipEventRecord(comm_done, s_comm));
+        VIT_HIP(hipStreamWaitEvent(s, comm_done, 0));
+    }
+
+    void step(float lr) {
+        finish_allreduce();
+        tbeg(TC_SGD, 0);
+        if (prec == VIT_BF16) {
+            sgd_bf16_k<<<grid_for(arena_elems / 4, 256), 256, 0, s>>>(params, pbf, grads, arena_elems, lr);
+            after_launch("sgd_bf16");
+        } else {
+            sgd(params, grads, arena_elems, lr, s);
+        }
+        tend();
+    }
+};
+
+__global__ void add_k(float* o, const float* a, const float* b, long long n) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        o[i] = a[i] + b[i];
+}
+__global__ void gelu_k(float* o, const float* a, long long n) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        o[i] = gelu_f(a[i]);
+}
+__global__ void gelu_bwd_k2(float* d, const float* x, const float* g, long long n) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        d[i] += gelu_grad_f(x[i]) * g[i];
+}
+__global__ void resbwd_k(float* d1, float* d2, const float* g, long long n) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        d1[i] += g[i];
+        d2[i] += g[i];
+    }
+}
+void Trainer::add(float* out, const float* a, const float* b, long long n) {
+    add_k<<<grid_for(n, 256), 256, 0, s>>>(out, a, b, n);
+    after_launch("residual_forward");
+}
+void Trainer::gelu(float* out, const float* in, long long n) {
+    gelu_k<<<grid_for(n, 256), 256, 0, s>>>(out, in, n);
+    after_launch("gelu_forward");
+}
+void Trainer::gelu_bwd(float* dinp, const float* in, const float* dout, long long n) {
+    gelu_bwd_k2<<<grid_for(n, 256), 256, 0, s>>>(dinp, in, dout, n);
+    after_launch("gelu_backward");
+}
+void Trainer::res_bwd(float* d1, float* d2, const float* dout, long long n) {
+    resbwd_k<<<grid_for(n, 256), 256, 0, s>>>(d1, d2, dout, n);
+    after_launch("residual_backward");
+}
+
+}  // namespace vit
+
+// ============================================================================ C ABI
+struct vit_trainer {
+    vit::Trainer t;
+};
+using vit::set_error;
+
+extern "C" {
+vit_trainer_t* vit_trainer_create(const vit_config_t* cfg, int batch, int precision, int device) {
+    auto* h = new vit_trainer();
+    if (!h->t.init(cfg, batch, precision, device)) {
+        h->t.destroy();
+        delete h;
+        return nullptr;
+    }
+    return h;
+}
+void vit_trainer_destroy(vit_trainer_t* h) {
+    if (!h) return;
+    h->t.destroy();
+    delete h;
+}
+long long vit_trainer_num_params(const vit_trainer_t* h) { return h->t.n_params; }
+long long vit_trainer_device_bytes(const vit_trainer_t* h) { return (long long)h->t.dev_bytes; }
+int vit_trainer_set_params(vit_trainer_t* h, const float* hp) {
+    h->t.canon_to_device(hp, h->t.params);
+    h->t.refresh_bf16();
+    VIT_HIP(hipStreamSynchronize(h->t.s));
+    return vit::has_error();
+}
+int vit_trainer_get_params(vit_trainer_t* h, float* hp) {
+    h->t.device_to_canon(h->t.params, hp);
+    return vit::has_error();
+}
+int vit_trainer_get_grads(vit_trainer_t* h, float* hg) {
+    VIT_HIP(hipStreamSynchronize(h->t.s_comm));
+    h->t.device_to_canon(h->t.grads, hg);
+    return vit::has_error();
+}
+int vit_trainer_set_batch(vit_trainer_t* h, const float* px, const int* lab) {
+    auto& t = h->t;
+    VIT_HIP(hipMemcpyAsync(t.pixels, px, (size_t)t.B * 3 * t.cfg.img * t.cfg.img * 4, hipMemcpyHostToDevice, t.s));
+    VIT_HIP(hipMemcpyAsync(t.labels, lab, (size_t)t.B * 4, hipMemcpyHostToDevice, t.s));
+    VIT_HIP(hipStreamSynchronize(t.s));
+    return vit::has_error();
+}
+int vit_trainer_set_batch_device(vit_trainer_t* h, const float* px, const int* lab) {
+    auto& t = h->t;
+    VIT_HIP(hipMemcpyAsync(t.pixels, px, (size_t)t.B * 3 * t.cfg.img * t.cfg.img * 4, hipMemcpyDeviceToDevice, t.s));
+    VIT_HIP(hipMemcpyAsync(t.labels, lab, (size_t)t.B * 4, hipMemcpyDeviceToDevice, t.s));
+    return vit::has_error();
+}
+int vit_trainer_forward(vit_trainer_t* h, int b_global) {
+    auto& t = h->t;
+    t.b_global = b_global > 0 ? b_global : t.B;
+    if (t.prec == VIT_BF16) t.forward_bf16(); else t.forward_f32();
+    return vit::has_error();
+}
+int vit_trainer_zero_grad(vit_trainer_t* h) {
+    auto& t = h->t;
+    // the previous step's all-reduce must be done with the arena before it is cleared
+    if (t.comm && t.world > 1) {
+        VIT_HIP(hipEventRecord(t.comm_done, t.s_comm));
+        VIT_HIP(hipStreamWaitEvent(t.s, t.comm_done, 0));
+    }
+    VIT_HIP(hipMemsetAsync(t.grads, 0, t.arena_elems * 4, t.s));
+    return vit::has_error();
+}
+int vit_trainer_backward(vit_trainer_t* h) {
+    auto& t = h->t;
+    if (t.prec == VIT_BF16) t.backward_bf16(); else t.backward_f32();
+    return vit::has_error();
+}
+int vit_trainer_step(vit_trainer_t* h, float lr) {
+    h->t.step(lr);
+    return vit::has_error();
+}
+int vit_trainer_train_step(vit_trainer_t* h, float lr, int b_global) {
+    vit_trainer_zero_grad(h);
+    vit_trainer_forward(h, b_global);
+    vit_trainer_backward(h);
+    vit_trainer_step(h, lr);
+    return vit::has_error();
+}
+float vit_trainer_mean_loss(vit_trainer_t* h) {
+    auto& t = h->t;
+    std::vector<float> l(t.B);
+    VIT_HIP(hipMemcpyAsync(l.data(), t.losses, t.B * 4, hipMemcpyDeviceToHost, t.s));
+    VIT_HIP(hipStreamSynchronize(t.s));
+    float m = 0.f;  // train_vit.rs:258-263
+    for (float v : l) m += v;
+    return m / (float)t.B;
+}
+int vit_trainer_get_logits(vit_trainer_t* h, float* out) {
+    auto& t = h->t;
+    VIT_HIP(hipMemcpyAsync(out, t.logits, (size_t)t.B * t.NC * 4, hipMemcpyDeviceToHost, t.s));
+    VIT_HIP(hipStreamSynchronize(t.s));
+    return vit::has_error();
+}
+int vit_trainer_sync(vit_trainer_t* h) {
+    VIT_HIP(hipStreamSynchronize(h->t.s_comm));
+    VIT_HIP(hipStreamSynchronize(h->t.s));
+    return vit::has_error();
+}
+void* vit_trainer_stream(vit_trainer_t* h) { return (void*)h->t.s; }
+
+int vit_dp_unique_id_size(void) { return (int)sizeof(ncclUniqueId); }
+int vit_dp_get_unique_id(char* out) {
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) {
+        set_error("ncclGetUniqueId: %s", ncclGetErrorString(r));
+        return 1;
+    }
+    memcpy(out, &id, sizeof(id));
+    return 0;
+}
+int vit_trainer_dp_init(vit_trainer_t* h, int rank, int world, const char* uid, int overlap) {
+    auto& t = h->t;
+    t.rank = rank;
+    t.world = world;
+    t.overlap = overlap;
+    if (world <= 1) return 0;
+    ncclUniqueId id;
+    memcpy(&id, uid, sizeof(id));
+    VIT_HIP(hipSetDevice(t.device));
+    ncclResult_t r = ncclCommInitRank(&t.comm, world, id, rank);
+    if (r != ncclSuccess) {
+        set_error("ncclCommInitRank(rank %d/%d): %s", rank, world, ncclGetErrorString(r));
+        t.comm = nullptr;
+        return 1;
+    }
+    return 0;
+}
+int vit_trainer_set_timing(vit_trainer_t* h, int on) {
+    h->t.timing = on != 0;
+    return 0;
+}
+int vit_trainer_timing(vit_trainer_t* h, const char** names, double* ms, long long* calls,
+                       double* flops, int max) {
+    auto& t = h->t;
+    t.collect();
+    int n = 0;
+    for (int c = 0; c < vit::TC_COUNT && n < max; c++) {
+        if (!t.t_calls[c]) continue;
+        names[n] = vit::kTimerNames[c];
+        ms[n] = t.t_ms[c];
+        calls[n] = t.t_calls[c];
+        flops[n] = t.t_flops[c];
+        n++;
+    }
+    return n;
+}
+void vit_trainer_timing_reset(vit_trainer_t* h) {
+    auto& t = h->t;
+    t.collect();
+    for (int c = 0; c < vit::TC_COUNT; c++) {
+        t.t_ms[c] = 0;
+        t.t_calls[c] = 0;
+        t.t_flops[c] = 0;
+    }
+}
+}  // extern "C"
