@@ -118,6 +118,14 @@ void attention_backward_fused_bf16(uint16_t* dinp, const uint16_t* dout, const u
                                    int NH);
 void layernorm_forward_bf16(uint16_t* out, float* mean, float* rstd, const float* inp,
                             const float* weight, const float* bias, int B, int T, int C);
+/* generic bf16 GEMM (the engine under matmul_*_bf16), for tests and tools:
+ * C[M,N] (epilogue)= A . B with A(m,k) = a_kcontig ? A[m*lda+k] : A[k*lda+m],
+ * B(k,n) = b_kcontig ? B[n*ldb+k] : B[k*ldb+n].  epi: 0 f32 store, 1 f32 +=, 2 f32 atomic +=
+ * (split-K), 3 bf16 store; bias (nullable) is added for 0/1/3; dbias (nullable, epi 2 with an
+ * M-contig A) receives the row sums of A. */
+void gemm_bf16_ex(void* C, long long ldc, const uint16_t* A, long long lda, int a_kcontig,
+                  const uint16_t* B, long long ldb, int b_kcontig, const float* bias,
+                  float* dbias, int M, int N, int K, int epi, int splitk);
 void convert_f32_to_bf16(uint16_t* out, const float* inp, long long n);
 void convert_bf16_to_f32(float* out, const uint16_t* inp, long long n);
 

@@ -279,3 +279,32 @@ def test_error_channel(gpu):
     out = Z(v, 64, np.uint16)
     with pytest.raises(v.VitError):
         v.call("attention_forward_fused_bf16", out, Z(v, 64), Z(v, 3 * 64, np.uint16), 1, 1, 80, 1)
+
+
+# ------------------------------------------------------------------ generic bf16 GEMM engine
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (304, 520, 128), (776, 1000, 192), (512, 264, 640)])
+@pytest.mark.parametrize("ak,bk", [(1, 1), (1, 0), (0, 0), (0, 1)])
+def test_gemm_bf16_layouts(gpu, M, N, K, ak, bk):
+    """Every operand layout through both GEMM kernels (256x256 LDS-DMA and 128x128), ragged M/N."""
+    v = gpu
+    rng = np.random.default_rng(M * 7 + N * 3 + K + 10 * ak + bk)
+    a = rng.normal(size=(M, K)).astype(np.float32)
+    b = rng.normal(size=(K, N)).astype(np.float32)
+    ab, bb = v.bf16_bits(a), v.bf16_bits(b)
+    ar, br = v.bf16_to_f32(ab).reshape(M, K).astype(np.float64), v.bf16_to_f32(bb).reshape(K, N).astype(np.float64)
+    A = D(v, ab.reshape(M, K) if ak else ab.reshape(M, K).T.copy(), np.uint16)
+    Bm = D(v, bb.reshape(K, N).T.copy() if bk else bb.reshape(K, N), np.uint16)
+    bias = rng.normal(size=N).astype(np.float32)
+    ref = ar @ br
+    for epi in (0, 2, 3):
+        out = Z(v, M * N, np.uint16 if epi == 3 else np.float32)
+        dbias = Z(v, M) if (epi == 2 and not ak) else None
+        v.call("gemm_bf16_ex", out, N, A, K if ak else M, ak, Bm, K if bk else N, bk,
+               D(v, bias) if epi != 2 else None, dbias, M, N, K, epi, 0)
+        got = out.numpy().reshape(M, N)
+        if epi == 3:
+            got = v.bf16_to_f32(got)
+        want = ref + (bias if epi != 2 else 0)
+        assert rel_err(got, want) < (1e-2 if epi == 3 else 2e-3), epi
+        if dbias is not None:
+            assert rel_err(dbias.numpy(), ar.sum(1)) < 2e-3

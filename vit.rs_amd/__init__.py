@@ -78,6 +78,7 @@ _SIGS = {
     "attention_forward_fused_bf16": (None, [P, P, P, I, I, I, I]),
     "attention_backward_fused_bf16": (None, [P, P, P, P, P, I, I, I, I]),
     "layernorm_forward_bf16": (None, [P, P, P, P, P, P, I, I, I]),
+    "gemm_bf16_ex": (None, [P, LL, P, LL, I, P, LL, I, P, P, I, I, I, I, I]),
     "convert_f32_to_bf16": (None, [P, P, LL]),
     "convert_bf16_to_f32": (None, [P, P, LL]),
     # trainer

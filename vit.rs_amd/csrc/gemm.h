@@ -35,6 +35,7 @@ struct GemmArgs {
     const void* aux = nullptr;
     long long ldaux = 0;
     const float* bias = nullptr;
+    float* dbias = nullptr;  // bf16 wgrad with an M-contig A: dbias[m] += sum_k A(m,k) (fused colsum)
     int M = 0, N = 0, K = 0;
     int epi = EPI_F32_STORE;
     int splitk = 0;  // 0 = choose automatically (only EPI_F32_ATOMIC may split)

@@ -14,6 +14,8 @@
 //   bounds-checked scalar staging; the fp32 parity path.
 #include "gemm.h"
 
+#include <cstdlib>
+
 namespace vit {
 
 struct GemmParams {
@@ -23,10 +25,59 @@ struct GemmParams {
     void* C2;
     const void* aux;
     const float* bias;
+    float* dbias;
     long long lda, ldb, ldc, ldaux;
     int M, N, K;
     int kchunk;  // K range per split (multiple of the K tile)
 };
+
+// epilogue for one lane's C[m][n..n+3] (n % 4 == 0, m < M, n < N)
+template <int EPI>
+__device__ __forceinline__ void epilogue(const GemmParams& p, int m, int n, f32x4_t v) {
+    if constexpr (EPI != EPI_F32_ATOMIC && EPI != EPI_BF16_DGELU) {
+        if (p.bias) {
+            const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
+            v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+        }
+    }
+    const long long off = (long long)m * p.ldc + n;
+    if constexpr (EPI == EPI_F32_STORE) {
+        *reinterpret_cast<float4*>((float*)p.C + off) = make_float4(v[0], v[1], v[2], v[3]);
+    } else if constexpr (EPI == EPI_F32_ACC) {
+        float4* q = reinterpret_cast<float4*>((float*)p.C + off);
+        float4 o = *q;
+        o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
+        *q = o;
+    } else if constexpr (EPI == EPI_F32_ATOMIC) {
+        float* q = (float*)p.C + off;
+        atomicAdd(q + 0, v[0]);
+        atomicAdd(q + 1, v[1]);
+        atomicAdd(q + 2, v[2]);
+        atomicAdd(q + 3, v[3]);
+    } else if constexpr (EPI == EPI_BF16_STORE) {
+        *reinterpret_cast<uint2*>((bf16_t*)p.C + off) =
+            make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+    } else if constexpr (EPI == EPI_BF16_GELU) {
+        *reinterpret_cast<uint2*>((bf16_t*)p.C + off) =
+            make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        *reinterpret_cast<uint2*>((bf16_t*)p.C2 + off) =
+            make_uint2(pack_bf16x2(gelu_f(v[0]), gelu_f(v[1])),
+                       pack_bf16x2(gelu_f(v[2]), gelu_f(v[3])));
+    } else if constexpr (EPI == EPI_F32_RESID) {
+        const float4 r = *reinterpret_cast<const float4*>((const float*)p.aux +
+                                                          (long long)m * p.ldaux + n);
+        *reinterpret_cast<float4*>((float*)p.C + off) =
+            make_float4(v[0] + r.x, v[1] + r.y, v[2] + r.z, v[3] + r.w);
+    } else if constexpr (EPI == EPI_BF16_DGELU) {
+        const uint2 h = *reinterpret_cast<const uint2*>((const bf16_t*)p.aux +
+                                                        (long long)m * p.ldaux + n);
+        const float x0 = __uint_as_float(h.x << 16), x1 = __uint_as_float(h.x & 0xffff0000u);
+        const float x2 = __uint_as_float(h.y << 16), x3 = __uint_as_float(h.y & 0xffff0000u);
+        *reinterpret_cast<uint2*>((bf16_t*)p.C + off) =
+            make_uint2(pack_bf16x2(v[0] * gelu_grad_f(x0), v[1] * gelu_grad_f(x1)),
+                       pack_bf16x2(v[2] * gelu_grad_f(x2), v[3] * gelu_grad_f(x3)));
+    }
+}
 
 // ============================================================================ bf16 MFMA GEMM
 namespace bf {
@@ -60,6 +111,18 @@ struct Stager {
                 p = base + (long long)(k0 + row) * ld + (row0 + col);
             }
             r[c] = ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
+        }
+    }
+    // M/N-contig image: this thread's 8 columns ((tid&15)*8 ..) summed over its 4 rows
+    __device__ __forceinline__ void colsum(float (&acc)[8]) const {
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(&r[c]);
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                acc[2 * e] += __uint_as_float(w[e] << 16);
+                acc[2 * e + 1] += __uint_as_float(w[e] & 0xffff0000u);
+            }
         }
     }
     __device__ __forceinline__ void store(bf16_t* img, int tid) const {
@@ -116,9 +179,13 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmParams p) {
 
     Stager<AK, BM> sa;
     Stager<BKC, BN> sb;
+    // fused bias gradient (wgrad): the blocks of the first N tile sum their A tiles
+    const bool do_db = !AK && p.dbias != nullptr && tn0 == 0;
+    float dbacc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (nk > 0) {
         sa.load(A, p.lda, tm0, p.M, kbeg, kend, tid);
         sb.load(B, p.ldb, tn0, p.N, kbeg, kend, tid);
+        if constexpr (!AK) if (do_db) sa.colsum(dbacc);
         sa.store(smem, tid);
         sb.store(smem + TILE, tid);
     }
@@ -150,10 +217,26 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmParams p) {
         }
         if (more) {
             bf16_t* nxt = smem + (cur ^ 1) * 2 * TILE;
+            if constexpr (!AK) if (do_db) sa.colsum(dbacc);
             sa.store(nxt, tid);
             sb.store(nxt + TILE, tid);
         }
         __syncthreads();
+    }
+
+    if constexpr (!AK) {
+        if (do_db) {  // reduce the 16 threads sharing a column chunk, one atomic per column
+            float* red = reinterpret_cast<float*>(smem);  // [16 row groups][128 cols]
+#pragma unroll
+            for (int e = 0; e < 8; e++) red[(tid >> 4) * 128 + (tid & 15) * 8 + e] = dbacc[e];
+            __syncthreads();
+            if (tid < 128 && tm0 + tid < p.M) {
+                float t = 0.f;
+#pragma unroll
+                for (int q = 0; q < 16; q++) t += red[q * 128 + tid];
+                atomicAdd(p.dbias + tm0 + tid, t);
+            }
+        }
     }
 
     // epilogue: lane holds C[m][n..n+3], m = tm0 + wm*64 + a*16 + (lane&15),
@@ -167,54 +250,224 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmParams p) {
         for (int b = 0; b < 4; b++) {
             const int n = tn0 + wn * 64 + b * 16 + 4 * g;
             if (n >= p.N) continue;
-            f32x4_t v = acc[a][b];
-            if constexpr (EPI != EPI_F32_ATOMIC && EPI != EPI_BF16_DGELU) {
-                if (p.bias) {
-                    const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
-                    v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
-                }
-            }
-            const long long off = (long long)m * p.ldc + n;
-            if constexpr (EPI == EPI_F32_STORE) {
-                *reinterpret_cast<float4*>((float*)p.C + off) = make_float4(v[0], v[1], v[2], v[3]);
-            } else if constexpr (EPI == EPI_F32_ACC) {
-                float4* q = reinterpret_cast<float4*>((float*)p.C + off);
-                float4 o = *q;
-                o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
-                *q = o;
-            } else if constexpr (EPI == EPI_F32_ATOMIC) {
-                float* q = (float*)p.C + off;
-                atomicAdd(q + 0, v[0]);
-                atomicAdd(q + 1, v[1]);
-                atomicAdd(q + 2, v[2]);
-                atomicAdd(q + 3, v[3]);
-            } else if constexpr (EPI == EPI_BF16_STORE) {
-                *reinterpret_cast<uint2*>((bf16_t*)p.C + off) =
-                    make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-            } else if constexpr (EPI == EPI_BF16_GELU) {
-                *reinterpret_cast<uint2*>((bf16_t*)p.C + off) =
-                    make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-                *reinterpret_cast<uint2*>((bf16_t*)p.C2 + off) =
-                    make_uint2(pack_bf16x2(gelu_f(v[0]), gelu_f(v[1])),
-                               pack_bf16x2(gelu_f(v[2]), gelu_f(v[3])));
-            } else if constexpr (EPI == EPI_F32_RESID) {
-                const float4 r = *reinterpret_cast<const float4*>((const float*)p.aux +
-                                                                  (long long)m * p.ldaux + n);
-                *reinterpret_cast<float4*>((float*)p.C + off) =
-                    make_float4(v[0] + r.x, v[1] + r.y, v[2] + r.z, v[3] + r.w);
-            } else if constexpr (EPI == EPI_BF16_DGELU) {
-                const uint2 h = *reinterpret_cast<const uint2*>((const bf16_t*)p.aux +
-                                                                (long long)m * p.ldaux + n);
-                const float x0 = __uint_as_float(h.x << 16), x1 = __uint_as_float(h.x & 0xffff0000u);
-                const float x2 = __uint_as_float(h.y << 16), x3 = __uint_as_float(h.y & 0xffff0000u);
-                *reinterpret_cast<uint2*>((bf16_t*)p.C + off) =
-                    make_uint2(pack_bf16x2(v[0] * gelu_grad_f(x0), v[1] * gelu_grad_f(x1)),
-                               pack_bf16x2(v[2] * gelu_grad_f(x2), v[3] * gelu_grad_f(x3)));
-            }
+            epilogue<EPI>(p, m, n, acc[a][b]);
         }
     }
 }
 }  // namespace bf
+
+// ============================================================================ bf16 GEMM, 256x256
+// The large-shape path (every ViT-B/L/H training GEMM): 256x256x64 block tile, 512 threads =
+// 8 waves (2 M x 4 N), 128x64 per wave = 8x4 v_mfma_f32_16x16x32_bf16 tiles; operands staged by
+// global_load_lds (16 B, LDS-DMA, no VGPR round trip) into a double-buffered 128 KiB LDS ring.
+// LDS images are lane-linear (the DMA writes base + 16*lane); bank conflicts are removed by
+// XOR-permuting the 16-B chunks on the global SOURCE address and reading through the same
+// involution (cdna_hip_programming.md §5.4 rule 21), with the swizzles chosen by
+// tools/lds_banks.py:
+//   K-contig image  [256 rows][64 k]  (128 B rows): chunk' = chunk ^ (row & 7)  -> ds_read_b128
+//                                                     fragments conflict free
+//   M/N-contig image [64 k][256 cols] (512 B rows): chunk' = chunk ^ f(k),
+//       f(k) = (k&3)<<2 | ((k>>3)&1)<<1             -> ds_read_b64_tr_b16 conflict free
+// Fragments use the standard 16x16x32 map (lane (i,g): k = 8g + j); rows/cols past M/N are
+// clamped on load (they only feed masked outputs); K must be a multiple of 64.
+namespace g2 {
+constexpr int BM = 256, BN = 256, BK = 32, NT = 512;
+constexpr int NSLOT = 4;                   // LDS ring slots (prefetch distance NSLOT-1)
+constexpr int IMG_BYTES = 256 * BK * 2;    // 16 KiB per operand per slot
+constexpr int SLOT_BYTES = 2 * IMG_BYTES;  // 32 KiB (A | B)
+constexpr int KTILE = 64;                  // K granularity required of callers (and split chunks)
+
+// K-contig image: [256 rows][32 k] = 64 B rows, 4 chunks; swizzle chunk' = chunk ^ ((row>>1)&3)
+__device__ __forceinline__ int kc_swz(int row) { return (row >> 1) & 3; }
+// M/N-contig image: [32 k][256 cols] = 512 B rows; swizzle chunk' = chunk ^ f(k)
+__device__ __forceinline__ int mn_swz(int k) { return ((k & 3) << 2) | (((k >> 3) & 1) << 1); }
+
+// this thread's 2 LDS-DMA pieces of one operand image (wave w, piece j -> 1 KiB block j*8+w)
+template <bool KC>
+__device__ __forceinline__ void stage(const bf16_t* __restrict__ base, long long ld, int row0,
+                                      int rows_lim, int k0, char* img, int wave, int lane) {
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const int blk = j * 8 + wave;
+        const bf16_t* src;
+        if constexpr (KC) {
+            const int row = blk * 16 + (lane >> 2);
+            const int c = (lane & 3) ^ kc_swz(row);
+            const int gr = min(row0 + row, rows_lim - 1);
+            src = base + (long long)gr * ld + k0 + c * 8;
+        } else {
+            const int k = blk * 2 + (lane >> 5);
+            const int c = (lane & 31) ^ mn_swz(k);
+            const int gc = min(row0 + c * 8, rows_lim - 8);
+            src = base + (long long)(k0 + k) * ld + gc;
+        }
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(img + blk * 1024),
+                                         16, 0, 0);
+    }
+}
+
+// 8 bf16 of rows/cols [r0, r0+16) for the slot's 32-deep k: lane (i,g) gets k = 8g + j
+template <bool KC>
+__device__ __forceinline__ bf16x8_t frag(const char* img, int r0, int lane) {
+    const int i = lane & 15, g = lane >> 4;
+    if constexpr (KC) {
+        const int r = r0 + i;
+        return *reinterpret_cast<const bf16x8_t*>(img + r * 64 + ((g ^ kc_swz(r)) << 4));
+    } else {
+        const int q = i >> 2, p = i & 3;
+        const int ch = (r0 >> 3) + (p >> 1);
+        const int k0 = 8 * g + q, k1 = k0 + 4;
+        const char* a0 = img + k0 * 512 + ((ch ^ mn_swz(k0)) << 4) + (p & 1) * 8;
+        const char* a1 = img + k1 * 512 + ((ch ^ mn_swz(k1)) << 4) + (p & 1) * 8;
+        const bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4_t, a0));
+        const bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4_t, a1));
+        return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+}
+
+__device__ __forceinline__ void barrier_lds() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// Pipeline: NSLOT-slot LDS ring, NSLOT-1 K-steps of LDS-DMA in flight.  At step kt each wave
+// waits (counted vmcnt) until its own pieces of step kt have landed, then one barrier makes every
+// wave's pieces visible AND retires all reads of the slot about to be refilled (read at kt-1).
+template <bool AK, bool BKC, int EPI>
+__global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
+    __shared__ __attribute__((aligned(1024))) char smem[NSLOT * SLOT_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 2, wn = wave & 3;
+    const int ntm = cdiv(p.M, BM), ntn = cdiv(p.N, BN);
+    const int wg = xcd_remap(blockIdx.x, ntm * ntn);
+    const int tm0 = (wg / ntn) * BM, tn0 = (wg % ntn) * BN;
+    const int kbeg = blockIdx.y * p.kchunk;
+    const int kend = min(p.K, kbeg + p.kchunk);
+    const int nk = (kend - kbeg) / BK;
+    const bf16_t* A = (const bf16_t*)p.A;
+    const bf16_t* B = (const bf16_t*)p.B;
+    const bool do_db = !AK && p.dbias != nullptr && tn0 == 0;
+    float dbacc = 0.f;
+
+    f32x4_t acc[8][4];
+#pragma unroll
+    for (int a = 0; a < 8; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    auto issue = [&](int kt) {
+        char* slot = smem + (kt % NSLOT) * SLOT_BYTES;
+        const int k0 = kbeg + kt * BK;
+        stage<AK>(A, p.lda, tm0, p.M, k0, slot, wave, lane);
+        stage<BKC>(B, p.ldb, tn0, p.N, k0, slot + IMG_BYTES, wave, lane);
+    };
+    // step kt+1's pieces landed (this wave: counted vmcnt; every wave: the barrier), slot of
+    // step kt-1 no longer read by anyone -> refill it with step kt+3
+    auto sync_next = [&](int kt) {
+        if (kt + 1 >= nk) return;
+        if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        barrier_lds();
+        if (kt + 3 < nk) issue(kt + 3);
+    };
+    auto load_b = [&](int kt, bf16x8_t (&fb)[4]) {
+        const char* imgB = smem + (kt % NSLOT) * SLOT_BYTES + IMG_BYTES;
+#pragma unroll
+        for (int b = 0; b < 4; b++) fb[b] = frag<BKC>(imgB, wn * 64 + b * 16, lane);
+    };
+    auto load_a = [&](int kt, int half, bf16x8_t (&fa)[4]) {
+        const char* imgA = smem + (kt % NSLOT) * SLOT_BYTES;
+#pragma unroll
+        for (int a = 0; a < 4; a++) fa[a] = frag<AK>(imgA, wm * 128 + (half * 4 + a) * 16, lane);
+    };
+    auto mfmas = [&](int half, const bf16x8_t (&fa)[4], const bf16x8_t (&fb)[4]) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+                acc[half * 4 + a][b] =
+                    __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[b], fa[a], acc[half * 4 + a][b], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+    };
+    auto bias_sum = [&](int kt) {
+        if constexpr (!AK) {
+            if (do_db) {  // fused bias gradient: column sums of this A image (rows of dW)
+                const char* imgA = smem + (kt % NSLOT) * SLOT_BYTES;
+                const int m = tid & 255, kh = (tid >> 8) * 16;
+#pragma unroll
+                for (int k = kh; k < kh + 16; k++) {
+                    const int c = (m >> 3) ^ mn_swz(k);
+                    dbacc += bf2f(*reinterpret_cast<const bf16_t*>(imgA + k * 512 + c * 16 + (m & 7) * 2));
+                }
+            }
+        }
+    };
+
+    // Two phases per K-step, fragments always one phase ahead of the MFMAs:
+    //   phase 0: read A rows 64..127 of step kt      | MFMA A rows 0..63   x B  (16)
+    //   phase 1: barrier for step kt+1, refill ring; read B and A rows 0..63 of step kt+1
+    //                                                | MFMA A rows 64..127 x B  (16)
+    bf16x8_t alo[4], ahi[4], b0[4], b1[4];
+#pragma unroll
+    for (int kt = 0; kt < NSLOT - 1; kt++)
+        if (kt < nk) issue(kt);
+    if (nk > 0) {
+        if (nk >= 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if (nk == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        barrier_lds();
+        load_b(0, b0);
+        load_a(0, 0, alo);
+    }
+    for (int kt = 0; kt < nk; kt += 2) {
+        load_a(kt, 1, ahi);
+        mfmas(0, alo, b0);
+        sync_next(kt);
+        if (kt + 1 < nk) {
+            load_b(kt + 1, b1);
+            load_a(kt + 1, 0, alo);
+        }
+        mfmas(1, ahi, b0);
+        bias_sum(kt);
+        if (kt + 1 >= nk) break;
+        load_a(kt + 1, 1, ahi);
+        mfmas(0, alo, b1);
+        sync_next(kt + 1);
+        if (kt + 2 < nk) {
+            load_b(kt + 2, b0);
+            load_a(kt + 2, 0, alo);
+        }
+        mfmas(1, ahi, b1);
+        bias_sum(kt + 1);
+    }
+    if constexpr (!AK) {
+        if (do_db) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            float* red = reinterpret_cast<float*>(smem);
+            red[tid] = dbacc;
+            __syncthreads();
+            if (tid < 256 && tm0 + tid < p.M) atomicAdd(p.dbias + tm0 + tid, red[tid] + red[tid + 256]);
+        }
+    }
+
+    const int i = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int a = 0; a < 8; a++) {
+        const int m = tm0 + wm * 128 + a * 16 + i;
+        if (m >= p.M) continue;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const int n = tn0 + wn * 64 + b * 16 + 4 * g;
+            if (n >= p.N) continue;
+            epilogue<EPI>(p, m, n, acc[a][b]);
+        }
+    }
+}
+}  // namespace g2
 
 // ============================================================================ fp32 MFMA GEMM
 namespace f32 {
@@ -322,10 +575,25 @@ __global__ __launch_bounds__(256) void colsum_kernel(float* __restrict__ dbias,
 
 static GemmParams make_params(const GemmArgs& a, int kchunk) {
     GemmParams p;
-    p.A = a.A; p.B = a.B; p.C = a.C; p.C2 = a.C2; p.aux = a.aux; p.bias = a.bias;
+    p.A = a.A; p.B = a.B; p.C = a.C; p.C2 = a.C2; p.aux = a.aux; p.bias = a.bias; p.dbias = a.dbias;
     p.lda = a.lda; p.ldb = a.ldb; p.ldc = a.ldc; p.ldaux = a.ldaux;
     p.M = a.M; p.N = a.N; p.K = a.K; p.kchunk = kchunk;
     return p;
+}
+
+// split-K for one-block-per-CU kernels: the smallest split whose last wave of blocks fills
+// >= 90% of the 256 CUs (or the best fill up to 32), keeping >= 16 K-tiles per split
+static int choose_split_waves(int tiles, int nk) {
+    int best = 1;
+    double best_eff = 0.0;
+    for (int s = 1; s <= 32 && nk / s >= 16; s++) {
+        const int blocks = tiles * s;
+        const int waves = (blocks + 255) / 256;
+        const double eff = (double)blocks / (waves * 256.0) * (blocks >= 128 ? 1.0 : blocks / 128.0);
+        if (eff > best_eff + 1e-9) { best_eff = eff; best = s; }
+        if (eff >= 0.9) break;
+    }
+    return best;
 }
 
 static int choose_split(int tiles, int K, int ktile, int want_blocks) {
@@ -382,11 +650,54 @@ static void launch_bf16(const GemmArgs& a, const GemmParams& p, dim3 grid, hipSt
     }
 }
 
+template <bool AK, bool BKC>
+static void launch_g2(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStream_t s) {
+    switch (a.epi) {
+#define VIT_CASE(E) \
+    case E: g2::gemm_kernel<AK, BKC, E><<<grid, g2::NT, 0, s>>>(p); break;
+        VIT_CASE(EPI_F32_STORE)
+        VIT_CASE(EPI_F32_ACC)
+        VIT_CASE(EPI_F32_ATOMIC)
+        VIT_CASE(EPI_BF16_STORE)
+        VIT_CASE(EPI_BF16_GELU)
+        VIT_CASE(EPI_F32_RESID)
+        VIT_CASE(EPI_BF16_DGELU)
+#undef VIT_CASE
+        default: set_error("gemm_bf16: unsupported epilogue %d", a.epi); return;
+    }
+}
+
+static int gemm_variant() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("VIT_GEMM");
+        v = (e && e[0] == '1') ? 1 : 2;  // VIT_GEMM=1 forces the 128x128 register-staged kernel
+    }
+    return v;
+}
+
 void gemm_bf16(const GemmArgs& a, hipStream_t s) {
     if (a.M <= 0 || a.N <= 0) return;
     if (!gemm_bf16_supported(a)) {
         set_error("gemm_bf16: unsupported shape/alignment M=%d N=%d K=%d lda=%lld ldb=%lld",
                   a.M, a.N, a.K, a.lda, a.ldb);
+        return;
+    }
+    const bool big = a.K % g2::KTILE == 0 && a.M >= 256 && a.N >= 256 && gemm_variant() == 2 &&
+                     (a.a_kcontig && a.b_kcontig || getenv("VIT_G2_ALL"));
+    if (big) {
+        const int tiles = cdiv(a.M, g2::BM) * cdiv(a.N, g2::BN);
+        int split = 1;
+        if (a.epi == EPI_F32_ATOMIC) split = a.splitk > 0 ? a.splitk : choose_split_waves(tiles, a.K / g2::KTILE);
+        int kchunk = cdiv(cdiv(a.K, split), g2::KTILE) * g2::KTILE;
+        split = cdiv(a.K, kchunk);
+        GemmParams p = make_params(a, kchunk);
+        dim3 grid(tiles, split);
+        if (a.a_kcontig && a.b_kcontig) launch_g2<true, true>(a, p, grid, s);
+        else if (a.a_kcontig && !a.b_kcontig) launch_g2<true, false>(a, p, grid, s);
+        else if (!a.a_kcontig && !a.b_kcontig) launch_g2<false, false>(a, p, grid, s);
+        else launch_g2<false, true>(a, p, grid, s);
+        after_launch("gemm_bf16_256");
         return;
     }
     const int tiles = cdiv(a.M, bf::BM) * cdiv(a.N, bf::BN);

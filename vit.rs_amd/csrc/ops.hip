@@ -155,6 +155,127 @@ __global__ __launch_bounds__(256) void ln_bwd_k(float* __restrict__ dinp, bf16_t
     }
 }
 
+// Vectorised LayerNorm for C % 256 == 0: one wave per row, NV float4 per lane held in registers
+// (the row is read once).  Same formulas as ln_fwd_k / ln_bwd_k.
+template <int NV, typename TO>
+__global__ __launch_bounds__(256) void ln_fwd_vec_k(TO* __restrict__ out, float* __restrict__ mean,
+                                                    float* __restrict__ rstd,
+                                                    const float* __restrict__ inp,
+                                                    const float* __restrict__ w,
+                                                    const float* __restrict__ b, long long rows,
+                                                    int C) {
+    const int lane = threadIdx.x & 63;
+    const long long row = blockIdx.x * 4LL + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const float4* x4 = reinterpret_cast<const float4*>(inp + row * C);
+    float4 v[NV];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; j++) {
+        v[j] = x4[lane + 64 * j];
+        s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+    }
+    const float m = warp_sum(s) / (float)C;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; j++) {
+        const float a = v[j].x - m, bb = v[j].y - m, c = v[j].z - m, d = v[j].w - m;
+        q += (a * a + bb * bb) + (c * c + d * d);
+    }
+    const float r = 1.0f / sqrtf(warp_sum(q) / (float)C + 1e-5f);
+#pragma unroll
+    for (int j = 0; j < NV; j++) {
+        const int k = lane + 64 * j;
+        const float4 w4 = reinterpret_cast<const float4*>(w)[k];
+        const float4 b4 = reinterpret_cast<const float4*>(b)[k];
+        const float y0 = (r * (v[j].x - m)) * w4.x + b4.x, y1 = (r * (v[j].y - m)) * w4.y + b4.y;
+        const float y2 = (r * (v[j].z - m)) * w4.z + b4.z, y3 = (r * (v[j].w - m)) * w4.w + b4.w;
+        if constexpr (sizeof(TO) == 2)
+            reinterpret_cast<uint2*>(out + row * C)[k] = make_uint2(pack_bf16x2(y0, y1), pack_bf16x2(y2, y3));
+        else
+            reinterpret_cast<float4*>(out + row * C)[k] = make_float4(y0, y1, y2, y3);
+    }
+    if (lane == 0) {
+        mean[row] = m;
+        rstd[row] = r;
+    }
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void ln_bwd_vec_k(float* __restrict__ dinp, bf16_t* __restrict__ dinp_bf,
+                                                    const float* __restrict__ dres_in,
+                                                    float* __restrict__ dweight,
+                                                    float* __restrict__ dbias,
+                                                    const float* __restrict__ dout,
+                                                    const float* __restrict__ inp,
+                                                    const float* __restrict__ weight,
+                                                    const float* __restrict__ mean,
+                                                    const float* __restrict__ rstd, long long rows,
+                                                    int C) {
+    extern __shared__ float sm[];  // [4 waves][2][C]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float4 w4[NV], dw[NV], db[NV];
+#pragma unroll
+    for (int j = 0; j < NV; j++) {
+        w4[j] = reinterpret_cast<const float4*>(weight)[lane + 64 * j];
+        dw[j] = db[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const long long nwaves = (long long)gridDim.x * 4;
+    for (long long row = blockIdx.x * 4LL + wave; row < rows; row += nwaves) {
+        const float4* dy4 = reinterpret_cast<const float4*>(dout + row * C);
+        const float4* x4 = reinterpret_cast<const float4*>(inp + row * C);
+        const float mu = mean[row], rs = rstd[row];
+        float4 dy[NV], nr[NV];
+        float a = 0.f, bs = 0.f;
+#pragma unroll
+        for (int j = 0; j < NV; j++) {
+            dy[j] = dy4[lane + 64 * j];
+            const float4 x = x4[lane + 64 * j];
+            nr[j] = make_float4((x.x - mu) * rs, (x.y - mu) * rs, (x.z - mu) * rs, (x.w - mu) * rs);
+            const float d0 = w4[j].x * dy[j].x, d1 = w4[j].y * dy[j].y, d2 = w4[j].z * dy[j].z, d3 = w4[j].w * dy[j].w;
+            a += (d0 + d1) + (d2 + d3);
+            bs += (d0 * nr[j].x + d1 * nr[j].y) + (d2 * nr[j].z + d3 * nr[j].w);
+        }
+        const float dm = warp_sum(a) / (float)C, dnm = warp_sum(bs) / (float)C;
+#pragma unroll
+        for (int j = 0; j < NV; j++) {
+            const int k = lane + 64 * j;
+            db[j].x += dy[j].x; db[j].y += dy[j].y; db[j].z += dy[j].z; db[j].w += dy[j].w;
+            dw[j].x += nr[j].x * dy[j].x; dw[j].y += nr[j].y * dy[j].y;
+            dw[j].z += nr[j].z * dy[j].z; dw[j].w += nr[j].w * dy[j].w;
+            float4 dv;
+            dv.x = ((w4[j].x * dy[j].x - dm) - nr[j].x * dnm) * rs;
+            dv.y = ((w4[j].y * dy[j].y - dm) - nr[j].y * dnm) * rs;
+            dv.z = ((w4[j].z * dy[j].z - dm) - nr[j].z * dnm) * rs;
+            dv.w = ((w4[j].w * dy[j].w - dm) - nr[j].w * dnm) * rs;
+            float4* o = reinterpret_cast<float4*>(dinp + row * C) + k;
+            if (dres_in) {
+                const float4 ri = reinterpret_cast<const float4*>(dres_in + row * C)[k];
+                const float4 t = make_float4(ri.x + dv.x, ri.y + dv.y, ri.z + dv.z, ri.w + dv.w);
+                *o = t;
+                if (dinp_bf)
+                    reinterpret_cast<uint2*>(dinp_bf + row * C)[k] =
+                        make_uint2(pack_bf16x2(t.x, t.y), pack_bf16x2(t.z, t.w));
+            } else {
+                float4 t = *o;
+                t.x += dv.x; t.y += dv.y; t.z += dv.z; t.w += dv.w;
+                *o = t;
+            }
+        }
+    }
+    float* mw = sm + wave * 2 * C;
+#pragma unroll
+    for (int j = 0; j < NV; j++) {
+        reinterpret_cast<float4*>(mw)[lane + 64 * j] = dw[j];
+        reinterpret_cast<float4*>(mw + C)[lane + 64 * j] = db[j];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * C; i += 256) {
+        const float t = sm[i] + sm[2 * C + i] + sm[4 * C + i] + sm[6 * C + i];
+        atomicAdd(i < C ? dweight + i : dbias + (i - C), t);
+    }
+}
+
 // ------------------------------------------------------------------ softmax / cross-entropy
 // train_vit.rs:493-517 — block per row, max init -10000 (:499)
 __global__ __launch_bounds__(256) void softmax_k(float* __restrict__ probs,
@@ -266,37 +387,76 @@ __global__ void patch_small_grads_k(float* __restrict__ dcls, float* __restrict_
 }
 
 // ------------------------------------------------------------------ launch helpers (internal)
+template <typename TO>
+static void ln_forward_any(TO* out, float* mean, float* rstd, const float* inp, const float* w,
+                           const float* b, long long rows, int C, hipStream_t s) {
+    if (rows <= 0) return;
+    const int g = cdiv(rows, 4);
+    const bool vec = C % 256 == 0 && C <= 2048 && (((uintptr_t)inp | (uintptr_t)out | (uintptr_t)w | (uintptr_t)b) & 15) == 0;
+    switch (vec ? C / 256 : 0) {
+        case 1: ln_fwd_vec_k<1, TO><<<g, 256, 0, s>>>(out, mean, rstd, inp, w, b, rows, C); break;
+        case 2: ln_fwd_vec_k<2, TO><<<g, 256, 0, s>>>(out, mean, rstd, inp, w, b, rows, C); break;
+        case 3: ln_fwd_vec_k<3, TO><<<g, 256, 0, s>>>(out, mean, rstd, inp, w, b, rows, C); break;
+        case 4: ln_fwd_vec_k<4, TO><<<g, 256, 0, s>>>(out, mean, rstd, inp, w, b, rows, C); break;
+        case 5: ln_fwd_vec_k<5, TO><<<g, 256, 0, s>>>(out, mean, rstd, inp, w, b, rows, C); break;
+        case 6: ln_fwd_vec_k<6, TO><<<g, 256, 0, s>>>(out, mean, rstd, inp, w, b, rows, C); break;
+        case 8: ln_fwd_vec_k<8, TO><<<g, 256, 0, s>>>(out, mean, rstd, inp, w, b, rows, C); break;
+        default: ln_fwd_k<TO><<<g, 256, 0, s>>>(out, mean, rstd, inp, w, b, rows, C); break;
+    }
+    after_launch("layernorm_forward");
+}
 void ln_forward_f32(float* out, float* mean, float* rstd, const float* inp, const float* w,
                     const float* b, long long rows, int C, hipStream_t s) {
-    if (rows <= 0) return;
-    ln_fwd_k<float><<<cdiv(rows, 4), 256, 0, s>>>(out, mean, rstd, inp, w, b, rows, C);
-    after_launch("layernorm_forward");
+    ln_forward_any<float>(out, mean, rstd, inp, w, b, rows, C, s);
 }
 void ln_forward_bf16(bf16_t* out, float* mean, float* rstd, const float* inp, const float* w,
                      const float* b, long long rows, int C, hipStream_t s) {
-    if (rows <= 0) return;
-    ln_fwd_k<bf16_t><<<cdiv(rows, 4), 256, 0, s>>>(out, mean, rstd, inp, w, b, rows, C);
-    after_launch("layernorm_forward_bf16");
+    ln_forward_any<bf16_t>(out, mean, rstd, inp, w, b, rows, C, s);
 }
 static int ln_bwd_grid(long long rows) {
     long long g = (rows + 31) / 32;  // ~8 rows per wave
     return (int)(g < 1 ? 1 : (g > 2048 ? 2048 : g));
 }
+static void ln_backward_any(float* dinp, bf16_t* dinp_bf, const float* dres_in, float* dw,
+                            float* db, const float* dout, const float* inp, const float* w,
+                            const float* mean, const float* rstd, long long rows, int C,
+                            hipStream_t s) {
+    if (rows <= 0) return;
+    const bool vec = C % 256 == 0 && C <= 2048 &&
+                     (((uintptr_t)dinp | (uintptr_t)dout | (uintptr_t)inp | (uintptr_t)w |
+                       (uintptr_t)dres_in | (uintptr_t)dinp_bf) & 15) == 0;
+    if (!vec) {
+        ln_bwd_k<float><<<ln_bwd_grid(rows), 256, 2 * C * sizeof(float), s>>>(
+            dinp, dinp_bf, dres_in, dw, db, dout, inp, w, mean, rstd, rows, C);
+        after_launch("layernorm_backward");
+        return;
+    }
+    long long g = (rows + 15) / 16;  // ~4 rows per wave
+    const int grid = (int)(g < 1 ? 1 : (g > 1024 ? 1024 : g));
+    const size_t lds = 8 * (size_t)C * sizeof(float);
+#define VIT_LNB(NV) ln_bwd_vec_k<NV><<<grid, 256, lds, s>>>(dinp, dinp_bf, dres_in, dw, db, dout, inp, w, mean, rstd, rows, C)
+    switch (C / 256) {
+        case 1: VIT_LNB(1); break;
+        case 2: VIT_LNB(2); break;
+        case 3: VIT_LNB(3); break;
+        case 4: VIT_LNB(4); break;
+        case 5: VIT_LNB(5); break;
+        case 6: VIT_LNB(6); break;
+        case 7: VIT_LNB(7); break;
+        default: VIT_LNB(8); break;
+    }
+#undef VIT_LNB
+    after_launch("layernorm_backward");
+}
 void ln_backward_f32(float* dinp, float* dw, float* db, const float* dout, const float* inp,
                      const float* w, const float* mean, const float* rstd, long long rows, int C,
                      hipStream_t s) {
-    if (rows <= 0) return;
-    ln_bwd_k<float><<<ln_bwd_grid(rows), 256, 2 * C * sizeof(float), s>>>(
-        dinp, nullptr, nullptr, dw, db, dout, inp, w, mean, rstd, rows, C);
-    after_launch("layernorm_backward");
+    ln_backward_any(dinp, nullptr, nullptr, dw, db, dout, inp, w, mean, rstd, rows, C, s);
 }
 void ln_backward_fused(float* dres_out, bf16_t* dres_out_bf, const float* dres_in, float* dw,
                        float* db, const float* dout, const float* inp, const float* w,
                        const float* mean, const float* rstd, long long rows, int C, hipStream_t s) {
-    if (rows <= 0) return;
-    ln_bwd_k<float><<<ln_bwd_grid(rows), 256, 2 * C * sizeof(float), s>>>(
-        dres_out, dres_out_bf, dres_in, dw, db, dout, inp, w, mean, rstd, rows, C);
-    after_launch("layernorm_backward_fused");
+    ln_backward_any(dres_out, dres_out_bf, dres_in, dw, db, dout, inp, w, mean, rstd, rows, C, s);
 }
 void convert_f2bf(bf16_t* out, const float* inp, long long n, hipStream_t s) {
     if (n <= 0) return;
@@ -506,13 +666,24 @@ void matmul_backward_bf16(float* dinp, float* dweight, float* dbias, const uint1
         a.B = inp; a.ldb = C; a.b_kcontig = false;
         a.C = dweight; a.ldc = C;
         a.M = OC; a.N = C; a.K = BT; a.epi = EPI_F32_ATOMIC;
+        a.dbias = dbias;  // fused column sum of dout
         gemm_bf16(a, stream());
     }
-    if (dbias) colsum_bf16(dbias, dout, BT, OC, OC, stream());
 }
 void layernorm_forward_bf16(uint16_t* out, float* mean, float* rstd, const float* inp,
                             const float* weight, const float* bias, int B, int T, int C) {
     ln_forward_bf16(out, mean, rstd, inp, weight, bias, (long long)B * T, C, stream());
+}
+void gemm_bf16_ex(void* C, long long ldc, const uint16_t* A, long long lda, int a_kcontig,
+                  const uint16_t* B, long long ldb, int b_kcontig, const float* bias,
+                  float* dbias, int M, int N, int K, int epi, int splitk) {
+    VIT_REQUIRE(epi >= EPI_F32_STORE && epi <= EPI_BF16_STORE, "gemm_bf16_ex: epi %d", epi);
+    GemmArgs a;
+    a.A = A; a.lda = lda; a.a_kcontig = a_kcontig != 0;
+    a.B = B; a.ldb = ldb; a.b_kcontig = b_kcontig != 0;
+    a.C = C; a.ldc = ldc; a.bias = bias; a.dbias = dbias;
+    a.M = M; a.N = N; a.K = K; a.epi = epi; a.splitk = splitk;
+    gemm_bf16(a, stream());
 }
 void convert_f32_to_bf16(uint16_t* out, const float* inp, long long n) {
     convert_f2bf(out, inp, n, stream());

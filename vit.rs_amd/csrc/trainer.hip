@@ -487,8 +487,10 @@ struct Trainer {
         head_forward();
     }
 
-    void wgrad(int cls, const bf16_t* dout, int OC, const bf16_t* inp, int Cin, float* dW) {
-        GemmArgs w;  // dW[OC,Cin] += dout^T . inp   (reduction over B*T rows)
+    void wgrad(int cls, const bf16_t* dout, int OC, const bf16_t* inp, int Cin, float* dW,
+               float* db) {
+        GemmArgs w;  // dW[OC,Cin] += dout^T . inp, db += colsum(dout)  (reduction over B*T rows)
+        w.dbias = db;
         w.A = dout; w.lda = OC; w.a_kcontig = false;
         w.B = inp; w.ldb = Cin; w.b_kcontig = false;
         w.C = dW; w.ldc = Cin; w.M = OC; w.N = Cin; w.K = (int)BT; w.epi = EPI_F32_ATOMIC;
@@ -510,19 +512,13 @@ struct Trainer {
             d1.C = dfch; d1.ldc = 4 * C; d1.aux = a.fch; d1.ldaux = 4 * C;
             d1.M = (int)BT; d1.N = 4 * C; d1.K = C; d1.epi = EPI_BF16_DGELU;
             gemm(TC_FCPROJ_DGRAD, d1, true);
-            wgrad(TC_FCPROJ_WGRAD, dres_bf, C, a.fchg, 4 * C, G(P_FCPROJW, l));
-            tbeg(TC_COLSUM, 0);
-            colsum_f32(G(P_FCPROJB, l), dcur, (int)BT, C, C, s);
-            tend();
+            wgrad(TC_FCPROJ_WGRAD, dres_bf, C, a.fchg, 4 * C, G(P_FCPROJW, l), G(P_FCPROJB, l));
             // fc: dln2 = dfch . fcw
             GemmArgs d2;
             d2.A = dfch; d2.lda = 4 * C; d2.B = W(P_FCW, l); d2.ldb = C; d2.b_kcontig = false;
             d2.C = dln; d2.ldc = C; d2.M = (int)BT; d2.N = C; d2.K = 4 * C; d2.epi = EPI_F32_STORE;
             gemm(TC_FC_DGRAD, d2, true);
-            wgrad(TC_FC_WGRAD, dfch, 4 * C, a.ln2, C, G(P_FCW, l));
-            tbeg(TC_COLSUM, 0);
-            colsum_bf16(G(P_FCB, l), dfch, (int)BT, 4 * C, 4 * C, s);
-            tend();
+            wgrad(TC_FC_WGRAD, dfch, 4 * C, a.ln2, C, G(P_FCW, l), G(P_FCB, l));
             // ln2 backward + residual: dres2 = dres3 + LN2'(dln2)
             tbeg(TC_LN_BWD, 0);
             ln_backward_fused(dnxt, dres_bf, dcur, G(P_LN2W, l), G(P_LN2B, l), dln, a.res2,
@@ -534,10 +530,7 @@ struct Trainer {
             d3.A = dres_bf; d3.lda = C; d3.B = W(P_ATTPROJW, l); d3.ldb = C; d3.b_kcontig = false;
             d3.C = datty; d3.ldc = C; d3.M = (int)BT; d3.N = C; d3.K = C; d3.epi = EPI_BF16_STORE;
             gemm(TC_PROJ_DGRAD, d3, true);
-            wgrad(TC_PROJ_WGRAD, dres_bf, C, a.atty, C, G(P_ATTPROJW, l));
-            tbeg(TC_COLSUM, 0);
-            colsum_f32(G(P_ATTPROJB, l), dcur, (int)BT, C, C, s);
-            tend();
+            wgrad(TC_PROJ_WGRAD, dres_bf, C, a.atty, C, G(P_ATTPROJW, l), G(P_ATTPROJB, l));
             // attention
             tbeg(TC_ATTN_BWD, 8.0 * B * (double)T * T * C);
             attn_backward_fused(dqkv, datty, a.qkv, a.atty, a.lse, B, T, C, NH, s);
@@ -547,10 +540,7 @@ struct Trainer {
             d4.A = dqkv; d4.lda = 3 * C; d4.B = W(P_QKVW, l); d4.ldb = C; d4.b_kcontig = false;
             d4.C = dln; d4.ldc = C; d4.M = (int)BT; d4.N = C; d4.K = 3 * C; d4.epi = EPI_F32_STORE;
             gemm(TC_QKV_DGRAD, d4, true);
-            wgrad(TC_QKV_WGRAD, dqkv, 3 * C, a.ln1, C, G(P_QKVW, l));
-            tbeg(TC_COLSUM, 0);
-            colsum_bf16(G(P_QKVB, l), dqkv, (int)BT, 3 * C, 3 * C, s);
-            tend();
+            wgrad(TC_QKV_WGRAD, dqkv, 3 * C, a.ln1, C, G(P_QKVW, l), G(P_QKVB, l));
             tbeg(TC_LN_BWD, 0);
             ln_backward_fused(dnxt, dres_bf, dcur, G(P_LN1W, l), G(P_LN1B, l), dln, x, P(P_LN1W, l),
                               a.ln1_mean, a.ln1_rstd, BT, C, s);
