@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--C", type=int, default=768)
+    ap.add_argument("--only", default=None, help="comma-separated shape names")
     args = ap.parse_args()
     L = vit.lib()
     assert L.vit_init(0) == 0
@@ -37,6 +38,9 @@ def main():
         shapes.append((f"dgrad_{nm}", BT, ic, oc, 1, 0, 0))
         shapes.append((f"wgrad_{nm}", oc, ic, BT, 0, 0, 2))
     tot_ms, tot_fl = 0.0, 0.0
+    if args.only:
+        keep = set(args.only.split(","))
+        shapes = [sh for sh in shapes if sh[0] in keep]
     for name, M, N, K, ak, bk, epi in shapes:
         lda = K if ak else M
         ldb = K if bk else N

@@ -196,6 +196,7 @@ constexpr int TMAX = 256;
 constexpr int SK = 72;  // row-read image stride (144 B)
 constexpr int SV = 80;  // tr-read-only image stride (160 B): 8 consecutive rows hit 8 slots
 constexpr float LOG2E = 1.4426950408889634f;
+constexpr int NWB = 8;   // waves per backward workgroup (one workgroup per (b,h), LDS-bound to 1/CU)
 
 // rows r0+i, k over the head dim with the shared permutation (d = 32s+4g+j | 32s+16+4g+j-4)
 __device__ __forceinline__ bf16x8_t frag_row(const bf16_t* img, int stride, int r0, int s, int lane) {
@@ -320,23 +321,25 @@ __global__ __launch_bounds__(256) void attn_fwd_fused_k(bf16_t* __restrict__ out
 }
 
 template <int NKT>
-__global__ __launch_bounds__(256) void attn_bwd_fused_k(bf16_t* __restrict__ dqkv,
+__global__ __launch_bounds__(512) void attn_bwd_fused_k(bf16_t* __restrict__ dqkv,
                                                         const bf16_t* __restrict__ dout,
                                                         const bf16_t* __restrict__ qkv,
                                                         const bf16_t* __restrict__ out,
                                                         const float* __restrict__ lse, int T,
-                                                        int C, int NH) {
+                                                        int C, int NH, float* __restrict__ dsum) {
     __shared__ __attribute__((aligned(16))) bf16_t Qs[TMAX * SK];
     __shared__ __attribute__((aligned(16))) bf16_t Ks[TMAX * SK];
     __shared__ __attribute__((aligned(16))) bf16_t Vs[TMAX * SK];
     __shared__ __attribute__((aligned(16))) bf16_t Ds[TMAX * SK];
     __shared__ float lse_s[TMAX];
     __shared__ float del_s[TMAX];
+    __shared__ float csum_s[NWB * 3 * HS];  // fused bias gradient: per-wave column sums dQ|dK|dV
     constexpr int TP = NKT * 16;
     const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
     const long long C3 = 3LL * C;
     const bf16_t* base = qkv + (long long)b * T * C3 + h * HS;
     const bf16_t* dbase = dout + (long long)b * T * C + h * HS;
+    for (int t = threadIdx.x; t < NWB * 3 * HS; t += blockDim.x) csum_s[t] = 0.f;
     const bf16_t* obase = out + (long long)b * T * C + h * HS;
     load_rows(Qs, SK, base, C3, T, TP);
     load_rows(Ks, SK, base + C, C3, T, TP);
@@ -371,7 +374,8 @@ __global__ __launch_bounds__(256) void attn_bwd_fused_k(bf16_t* __restrict__ dqk
     const int nt_valid = (T + 15) / 16;
 
     // ---- phase 1: dK, dV for key tiles owned by this wave
-    for (int kt = w; kt < nt_valid; kt += 4) {
+    f32x4_t ck[4] = {}, cv[4] = {};  // this lane's share of the dK / dV column sums
+    for (int kt = w; kt < nt_valid; kt += NWB) {
         const int key0 = kt * 16;
         const bool key_ok = key0 + i < T;
         const bf16x8_t kf0 = frag_row(Ks, SK, key0, 0, lane), kf1 = frag_row(Ks, SK, key0, 1, lane);
@@ -379,6 +383,7 @@ __global__ __launch_bounds__(256) void attn_bwd_fused_k(bf16_t* __restrict__ dqk
         f32x4_t dv[4], dk[4];
 #pragma unroll
         for (int dt = 0; dt < 4; dt++) dv[dt] = dk[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
         for (int qs = 0; qs < TP / 32; qs++) {
             f32x4_t P[2], dS[2];
 #pragma unroll
@@ -414,10 +419,35 @@ __global__ __launch_bounds__(256) void attn_bwd_fused_k(bf16_t* __restrict__ dqk
                 store4(dst + 2 * C + 16 * dt, dv[dt], 1.0f);
             }
         }
+        if (dsum) {  // rows past T hold exact zeros (P = 0 there)
+#pragma unroll
+            for (int dt = 0; dt < 4; dt++) {
+                ck[dt] += dk[dt] * scale;
+                cv[dt] += dv[dt];
+            }
+        }
+    }
+    if (dsum) {  // reduce over the 16 key lanes once, one LDS row per wave
+#pragma unroll
+        for (int dt = 0; dt < 4; dt++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                float tk = ck[dt][r], tv = cv[dt][r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    tk += __shfl_xor(tk, o, 64);
+                    tv += __shfl_xor(tv, o, 64);
+                }
+                if (i == 0) {
+                    csum_s[(w * 3 + 1) * HS + 16 * dt + 4 * g + r] = tk;
+                    csum_s[(w * 3 + 2) * HS + 16 * dt + 4 * g + r] = tv;
+                }
+            }
     }
 
     // ---- phase 2: dQ for query tiles owned by this wave
-    for (int qt = w; qt < nt_valid; qt += 4) {
+    f32x4_t cq[4] = {};
+    for (int qt = w; qt < nt_valid; qt += NWB) {
         const int q0 = qt * 16;
         const bf16x8_t qf0 = frag_row(Qs, SK, q0, 0, lane), qf1 = frag_row(Qs, SK, q0, 1, lane);
         const bf16x8_t df0 = frag_row(Ds, SK, q0, 0, lane), df1 = frag_row(Ds, SK, q0, 1, lane);
@@ -425,6 +455,7 @@ __global__ __launch_bounds__(256) void attn_bwd_fused_k(bf16_t* __restrict__ dqk
         f32x4_t dq[4];
 #pragma unroll
         for (int dt = 0; dt < 4; dt++) dq[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
         for (int ks = 0; ks < TP / 32; ks++) {
             f32x4_t dS[2];
 #pragma unroll
@@ -452,7 +483,42 @@ __global__ __launch_bounds__(256) void attn_bwd_fused_k(bf16_t* __restrict__ dqk
 #pragma unroll
             for (int dt = 0; dt < 4; dt++) store4(dst + 16 * dt, dq[dt], scale);
         }
+        if (dsum) {
+#pragma unroll
+            for (int dt = 0; dt < 4; dt++) cq[dt] += dq[dt] * scale;
+        }
     }
+    if (dsum) {
+#pragma unroll
+        for (int dt = 0; dt < 4; dt++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                float tq = cq[dt][r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) tq += __shfl_xor(tq, o, 64);
+                if (i == 0) csum_s[(w * 3 + 0) * HS + 16 * dt + 4 * g + r] = tq;
+            }
+    }
+    if (dsum) {  // per-(b,h) partial column sums -> dsum[bh][3*64] (reduced over b by a second kernel)
+        __syncthreads();
+        for (int t = threadIdx.x; t < 3 * HS; t += blockDim.x) {
+            float acc = 0.f;
+#pragma unroll
+            for (int ww = 0; ww < NWB; ww++) acc += csum_s[ww * 3 * HS + t];
+            dsum[(long long)bh * 3 * HS + t] = acc;
+        }
+    }
+}
+
+// out[s*C + h*64 + d] += sum_b part[(b*NH + h)][s*64 + d]
+__global__ void attn_colsum_reduce_k(float* __restrict__ out, const float* __restrict__ part, int B,
+                                     int NH, int C) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // over 3*C
+    if (idx >= 3 * C) return;
+    const int sct = idx / C, c = idx - sct * C, h = c / HS, d = c - h * HS;
+    float t = 0.f;
+    for (int b = 0; b < B; b++) t += part[((long long)b * NH + h) * 3 * HS + sct * HS + d];
+    out[idx] += t;
 }
 }  // namespace fa
 
@@ -473,6 +539,19 @@ bool attn_fused_supported(int T, int C, int NH) {
         default: set_error("fused attention: unsupported key tile count %d", nkt); return; \
     }
 
+#define VIT_NKT_DISPATCH_T(KERNEL, NTHR, ...)                                          \
+    switch (nkt) {                                                                      \
+        case 2: KERNEL<2><<<grid, NTHR, 0, s>>>(__VA_ARGS__); break;                    \
+        case 4: KERNEL<4><<<grid, NTHR, 0, s>>>(__VA_ARGS__); break;                    \
+        case 6: KERNEL<6><<<grid, NTHR, 0, s>>>(__VA_ARGS__); break;                    \
+        case 8: KERNEL<8><<<grid, NTHR, 0, s>>>(__VA_ARGS__); break;                    \
+        case 10: KERNEL<10><<<grid, NTHR, 0, s>>>(__VA_ARGS__); break;                  \
+        case 12: KERNEL<12><<<grid, NTHR, 0, s>>>(__VA_ARGS__); break;                  \
+        case 14: KERNEL<14><<<grid, NTHR, 0, s>>>(__VA_ARGS__); break;                  \
+        case 16: KERNEL<16><<<grid, NTHR, 0, s>>>(__VA_ARGS__); break;                  \
+        default: set_error("fused attention: unsupported key tile count %d", nkt); return; \
+    }
+
 void attn_forward_fused(bf16_t* out, float* lse, const bf16_t* qkv, int B, int T, int C, int NH,
                         hipStream_t s) {
     if (!attn_fused_supported(T, C, NH)) {
@@ -486,15 +565,26 @@ void attn_forward_fused(bf16_t* out, float* lse, const bf16_t* qkv, int B, int T
 }
 
 void attn_backward_fused(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t* out,
-                         const float* lse, int B, int T, int C, int NH, hipStream_t s) {
+                         const float* lse, int B, int T, int C, int NH, hipStream_t s,
+                         float* dqkv_colsum, float* part_ws) {
     if (!attn_fused_supported(T, C, NH)) {
         set_error("attention_backward_fused: needs head size 64 and T<=256 (T=%d C=%d NH=%d)", T, C, NH);
         return;
     }
     const int nkt = cdiv(T, 32) * 2;
     dim3 grid(B * NH);
-    VIT_NKT_DISPATCH(fa::attn_bwd_fused_k, dqkv, dout, qkv, out, lse, T, C, NH)
+#define VIT_BWD_THREADS 512
+    if (dqkv_colsum && !part_ws) {
+        set_error("attention_backward_fused: column sums need a [B*NH*192] workspace");
+        return;
+    }
+    VIT_NKT_DISPATCH_T(fa::attn_bwd_fused_k, VIT_BWD_THREADS, dqkv, dout, qkv, out, lse, T, C, NH,
+                       dqkv_colsum ? part_ws : nullptr)
     after_launch("attention_backward_fused");
+    if (dqkv_colsum) {
+        fa::attn_colsum_reduce_k<<<cdiv(3 * C, 256), 256, 0, s>>>(dqkv_colsum, part_ws, B, NH, C);
+        after_launch("attention_colsum_reduce");
+    }
 }
 
 }  // namespace vit

@@ -20,6 +20,7 @@ enum Epi {
     EPI_BF16_GELU = 4,   // C_bf16 = pre = acc + bias; C2_bf16 = gelu(pre)
     EPI_F32_RESID = 5,   // C_f32 = acc + bias + aux_f32[m*ldaux + n]
     EPI_BF16_DGELU = 6,  // C_bf16 = acc * gelu'(aux_bf16[m*ldaux + n])
+    EPI_F32_SLAB = 7,    // internal: split-K partial -> workspace slab[split][M][N] (float4 stores)
 };
 
 struct GemmArgs {
@@ -36,9 +37,15 @@ struct GemmArgs {
     long long ldaux = 0;
     const float* bias = nullptr;
     float* dbias = nullptr;  // bf16 wgrad with an M-contig A: dbias[m] += sum_k A(m,k) (fused colsum)
+    float* colsum_out = nullptr;  // 256x256 kernel, EPI_BF16_DGELU: += column sums of the output
     int M = 0, N = 0, K = 0;
     int epi = EPI_F32_STORE;
     int splitk = 0;  // 0 = choose automatically (only EPI_F32_ATOMIC may split)
+    // split-K workspace for EPI_F32_ATOMIC on the 256x256 kernel: partials go to fp32 slabs and
+    // one reduce kernel adds them into C (no atomics).  nullptr = the calling thread's workspace
+    // (ordered on the context stream); the trainer passes its own buffer for its stream.
+    float* ws = nullptr;
+    size_t ws_bytes = 0;
 };
 
 // fp32 operands, exact-fp32 MFMA (v_mfma_f32_16x16x4_f32); any shape/stride. Parity path.

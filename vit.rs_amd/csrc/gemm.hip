@@ -26,15 +26,17 @@ struct GemmParams {
     const void* aux;
     const float* bias;
     float* dbias;
+    float* colsum_out;
     long long lda, ldb, ldc, ldaux;
     int M, N, K;
     int kchunk;  // K range per split (multiple of the K tile)
+    int debug_same_tile;
 };
 
 // epilogue for one lane's C[m][n..n+3] (n % 4 == 0, m < M, n < N)
 template <int EPI>
-__device__ __forceinline__ void epilogue(const GemmParams& p, int m, int n, f32x4_t v) {
-    if constexpr (EPI != EPI_F32_ATOMIC && EPI != EPI_BF16_DGELU) {
+__device__ __forceinline__ void epilogue(const GemmParams& p, int m, int n, f32x4_t& v) {
+    if constexpr (EPI != EPI_F32_ATOMIC && EPI != EPI_BF16_DGELU && EPI != EPI_F32_SLAB) {
         if (p.bias) {
             const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
             v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
@@ -68,14 +70,18 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, int m, int n, f32x
                                                           (long long)m * p.ldaux + n);
         *reinterpret_cast<float4*>((float*)p.C + off) =
             make_float4(v[0] + r.x, v[1] + r.y, v[2] + r.z, v[3] + r.w);
+    } else if constexpr (EPI == EPI_F32_SLAB) {
+        float* slab = (float*)p.C + (long long)blockIdx.y * p.M * p.ldc;
+        *reinterpret_cast<float4*>(slab + off) = make_float4(v[0], v[1], v[2], v[3]);
     } else if constexpr (EPI == EPI_BF16_DGELU) {
         const uint2 h = *reinterpret_cast<const uint2*>((const bf16_t*)p.aux +
                                                         (long long)m * p.ldaux + n);
         const float x0 = __uint_as_float(h.x << 16), x1 = __uint_as_float(h.x & 0xffff0000u);
         const float x2 = __uint_as_float(h.y << 16), x3 = __uint_as_float(h.y & 0xffff0000u);
+        v[0] *= gelu_grad_f(x0); v[1] *= gelu_grad_f(x1);
+        v[2] *= gelu_grad_f(x2); v[3] *= gelu_grad_f(x3);
         *reinterpret_cast<uint2*>((bf16_t*)p.C + off) =
-            make_uint2(pack_bf16x2(v[0] * gelu_grad_f(x0), v[1] * gelu_grad_f(x1)),
-                       pack_bf16x2(v[2] * gelu_grad_f(x2), v[3] * gelu_grad_f(x3)));
+            make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
     }
 }
 
@@ -272,7 +278,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmParams p) {
 // clamped on load (they only feed masked outputs); K must be a multiple of 64.
 namespace g2 {
 constexpr int BM = 256, BN = 256, BK = 32, NT = 512;
-constexpr int NSLOT = 4;                   // LDS ring slots (prefetch distance NSLOT-1)
+constexpr int NSLOT = 4;                   // LDS ring slots (DMA 2 steps ahead)
 constexpr int IMG_BYTES = 256 * BK * 2;    // 16 KiB per operand per slot
 constexpr int SLOT_BYTES = 2 * IMG_BYTES;  // 32 KiB (A | B)
 constexpr int KTILE = 64;                  // K granularity required of callers (and split chunks)
@@ -326,23 +332,46 @@ __device__ __forceinline__ bf16x8_t frag(const char* img, int r0, int lane) {
     }
 }
 
+// instruction interleave hints (LLVM SchedGroupMask: MFMA 0x8, VMEM_READ 0x20, DS_READ 0x100)
+__device__ __forceinline__ void sched_phase0() {  // 4 A-fragment reads among 16 MFMAs
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
+    }
+}
+__device__ __forceinline__ void sched_phase1() {  // 4 LDS-DMA pieces + 8 fragment reads among 16 MFMAs
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
+    }
+}
+
 __device__ __forceinline__ void barrier_lds() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 }
 
-// Pipeline: NSLOT-slot LDS ring, NSLOT-1 K-steps of LDS-DMA in flight.  At step kt each wave
-// waits (counted vmcnt) until its own pieces of step kt have landed, then one barrier makes every
-// wave's pieces visible AND retires all reads of the slot about to be refilled (read at kt-1).
-template <bool AK, bool BKC, int EPI>
+// Pipeline (cdna_hip_programming.md §5 8-phase template, adapted): each 32-deep K-step is two
+// phases of 16 MFMAs per wave; every phase is [A: LDS fragment reads + 2 LDS-DMA pieces] barrier
+// [B: MFMAs] barrier.  Waves 4-7 (the SIMD partners of waves 0-3) run one barrier behind, so on
+// every SIMD one wave is in its MFMA region while its partner issues reads and DMA.  Ring of
+// NSLOT slots, DMA two steps ahead; a wave retires its own pieces of step s+1 (vmcnt) in phase 1
+// of step s, two barriers (three with the stagger) before anyone reads them; a slot is refilled
+// >= 6 barriers after its last read; every barrier is preceded by lgkmcnt(0).
+template <bool AK, bool BKC, int EPI, bool SCHED>
 __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
     __shared__ __attribute__((aligned(1024))) char smem[NSLOT * SLOT_BYTES];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
     const int ntm = cdiv(p.M, BM), ntn = cdiv(p.N, BN);
     const int wg = xcd_remap(blockIdx.x, ntm * ntn);
-    const int tm0 = (wg / ntn) * BM, tn0 = (wg % ntn) * BN;
+    int tm0 = (wg / ntn) * BM, tn0 = (wg % ntn) * BN;
+    if (p.debug_same_tile) { tm0 = 0; tn0 = 0; }  // diagnostic: every block streams one tile (L2)
     const int kbeg = blockIdx.y * p.kchunk;
     const int kend = min(p.K, kbeg + p.kchunk);
     const int nk = (kend - kbeg) / BK;
@@ -357,48 +386,36 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
 #pragma unroll
         for (int b = 0; b < 4; b++) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    auto issue = [&](int kt) {
-        char* slot = smem + (kt % NSLOT) * SLOT_BYTES;
-        const int k0 = kbeg + kt * BK;
-        stage<AK>(A, p.lda, tm0, p.M, k0, slot, wave, lane);
-        stage<BKC>(B, p.ldb, tn0, p.N, k0, slot + IMG_BYTES, wave, lane);
+    auto slot_of = [&](int st) { return smem + (st % NSLOT) * SLOT_BYTES; };
+    auto issue_a = [&](int st) {  // A-image pieces of step st (clamped: re-stage the last step)
+        stage<AK>(A, p.lda, tm0, p.M, kbeg + min(st, nk - 1) * BK, slot_of(st), wave, lane);
     };
-    // step kt+1's pieces landed (this wave: counted vmcnt; every wave: the barrier), slot of
-    // step kt-1 no longer read by anyone -> refill it with step kt+3
-    auto sync_next = [&](int kt) {
-        if (kt + 1 >= nk) return;
-        if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        barrier_lds();
-        if (kt + 3 < nk) issue(kt + 3);
+    auto issue_b = [&](int st) {
+        stage<BKC>(B, p.ldb, tn0, p.N, kbeg + min(st, nk - 1) * BK, slot_of(st) + IMG_BYTES, wave, lane);
     };
-    auto load_b = [&](int kt, bf16x8_t (&fb)[4]) {
-        const char* imgB = smem + (kt % NSLOT) * SLOT_BYTES + IMG_BYTES;
-#pragma unroll
-        for (int b = 0; b < 4; b++) fb[b] = frag<BKC>(imgB, wn * 64 + b * 16, lane);
+    auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
     };
-    auto load_a = [&](int kt, int half, bf16x8_t (&fa)[4]) {
-        const char* imgA = smem + (kt % NSLOT) * SLOT_BYTES;
-#pragma unroll
-        for (int a = 0; a < 4; a++) fa[a] = frag<AK>(imgA, wm * 128 + (half * 4 + a) * 16, lane);
-    };
-    auto mfmas = [&](int half, const bf16x8_t (&fa)[4], const bf16x8_t (&fb)[4]) {
-        __builtin_amdgcn_s_setprio(1);
+    auto mfma_half = [&](int half, const bf16x8_t (&fa)[4], const bf16x8_t (&fb)[4]) {
 #pragma unroll
         for (int a = 0; a < 4; a++)
 #pragma unroll
             for (int b = 0; b < 4; b++)
                 acc[half * 4 + a][b] =
                     __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[b], fa[a], acc[half * 4 + a][b], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
     };
     auto bias_sum = [&](int kt) {
         if constexpr (!AK) {
             if (do_db) {  // fused bias gradient: column sums of this A image (rows of dW)
-                const char* imgA = smem + (kt % NSLOT) * SLOT_BYTES;
+                const char* imgA = slot_of(kt);
                 const int m = tid & 255, kh = (tid >> 8) * 16;
 #pragma unroll
-                for (int k = kh; k < kh + 16; k++) {
+                for (int kk = 0; kk < 16; kk++) {
+                    const int k = kh + kk;
                     const int c = (m >> 3) ^ mn_swz(k);
                     dbacc += bf2f(*reinterpret_cast<const bf16_t*>(imgA + k * 512 + c * 16 + (m & 7) * 2));
                 }
@@ -406,43 +423,41 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
         }
     };
 
-    // Two phases per K-step, fragments always one phase ahead of the MFMAs:
-    //   phase 0: read A rows 64..127 of step kt      | MFMA A rows 0..63   x B  (16)
-    //   phase 1: barrier for step kt+1, refill ring; read B and A rows 0..63 of step kt+1
-    //                                                | MFMA A rows 64..127 x B  (16)
-    bf16x8_t alo[4], ahi[4], b0[4], b1[4];
-#pragma unroll
-    for (int kt = 0; kt < NSLOT - 1; kt++)
-        if (kt < nk) issue(kt);
+    const bool lagging = wave >= 4;
     if (nk > 0) {
-        if (nk >= 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else if (nk == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        barrier_lds();
-        load_b(0, b0);
-        load_a(0, 0, alo);
-    }
-    for (int kt = 0; kt < nk; kt += 2) {
-        load_a(kt, 1, ahi);
-        mfmas(0, alo, b0);
-        sync_next(kt);
-        if (kt + 1 < nk) {
-            load_b(kt + 1, b1);
-            load_a(kt + 1, 0, alo);
+        issue_a(0); issue_b(0); issue_a(1); issue_b(1);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // own pieces of step 0
+        bar();
+        if (lagging) {
+            __builtin_amdgcn_s_setprio(1);  // static priority for the younger half (T5)
+            bar();                          // stagger: one barrier behind waves 0-3
         }
-        mfmas(1, ahi, b0);
+    }
+    bf16x8_t fb[4], alo[4], ahi[4];
+    for (int kt = 0; kt < nk; kt++) {
+        const char* img = slot_of(kt);
+        // ---- phase 0
+#pragma unroll
+        for (int b = 0; b < 4; b++) fb[b] = frag<BKC>(img + IMG_BYTES, wn * 64 + b * 16, lane);
+#pragma unroll
+        for (int a = 0; a < 4; a++) alo[a] = frag<AK>(img, wm * 128 + a * 16, lane);
+        issue_a(kt + 2);
+        bar();
+        mfma_half(0, alo, fb);
+        bar();
+        // ---- phase 1
+#pragma unroll
+        for (int a = 0; a < 4; a++) ahi[a] = frag<AK>(img, wm * 128 + (4 + a) * 16, lane);
         bias_sum(kt);
-        if (kt + 1 >= nk) break;
-        load_a(kt + 1, 1, ahi);
-        mfmas(0, alo, b1);
-        sync_next(kt + 1);
-        if (kt + 2 < nk) {
-            load_b(kt + 2, b0);
-            load_a(kt + 2, 0, alo);
-        }
-        mfmas(1, ahi, b1);
-        bias_sum(kt + 1);
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // own pieces of step kt+1 landed
+        issue_b(kt + 2);
+        bar();
+        mfma_half(1, ahi, fb);
+        bar();
     }
+    if (nk > 0 && !lagging) bar();  // balance the stagger barrier
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // retire the trailing re-staged pieces
+    __builtin_amdgcn_s_setprio(0);
     if constexpr (!AK) {
         if (do_db) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -455,6 +470,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
     }
 
     const int i = lane & 15, g = lane >> 4;
+    f32x4_t csum[4] = {};
 #pragma unroll
     for (int a = 0; a < 8; a++) {
         const int m = tm0 + wm * 128 + a * 16 + i;
@@ -464,6 +480,23 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
             const int n = tn0 + wn * 64 + b * 16 + 4 * g;
             if (n >= p.N) continue;
             epilogue<EPI>(p, m, n, acc[a][b]);
+            if constexpr (EPI == EPI_BF16_DGELU) csum[b] += acc[a][b];
+        }
+    }
+    if constexpr (EPI == EPI_BF16_DGELU) {
+        if (p.colsum_out) {  // fused bias gradient of the next GEMM: column sums of this output
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    float t = csum[b][r];
+                    t += __shfl_xor(t, 1, 64);
+                    t += __shfl_xor(t, 2, 64);
+                    t += __shfl_xor(t, 4, 64);
+                    t += __shfl_xor(t, 8, 64);
+                    const int n = tn0 + wn * 64 + b * 16 + 4 * g + r;
+                    if (i == 0 && n < p.N) atomicAdd(p.colsum_out + n, t);
+                }
         }
     }
 }
@@ -573,11 +606,34 @@ __global__ __launch_bounds__(256) void colsum_kernel(float* __restrict__ dbias,
     atomicAdd(dbias + n, s);
 }
 
+// C[m][n] += sum_z slab[z][m][n]   (M x N fp32, ldc == N for the slabs)
+__global__ __launch_bounds__(256) void slab_reduce_k(float* __restrict__ C, long long ldc,
+                                                     const float* __restrict__ slab, int M, int N,
+                                                     int splits) {
+    const long long n4 = (long long)M * N / 4;
+    const long long plane = (long long)M * N;
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+        const long long e = i * 4;
+        const int m = (int)(e / N), n = (int)(e - (long long)m * N);
+        float4 acc = reinterpret_cast<const float4*>(slab)[i];
+        for (int z = 1; z < splits; z++) {
+            const float4 t = *reinterpret_cast<const float4*>(slab + z * plane + e);
+            acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
+        }
+        float4* c = reinterpret_cast<float4*>(C + (long long)m * ldc + n);
+        float4 o = *c;
+        o.x += acc.x; o.y += acc.y; o.z += acc.z; o.w += acc.w;
+        *c = o;
+    }
+}
+
 static GemmParams make_params(const GemmArgs& a, int kchunk) {
     GemmParams p;
-    p.A = a.A; p.B = a.B; p.C = a.C; p.C2 = a.C2; p.aux = a.aux; p.bias = a.bias; p.dbias = a.dbias;
+    p.A = a.A; p.B = a.B; p.C = a.C; p.C2 = a.C2; p.aux = a.aux; p.bias = a.bias; p.dbias = a.dbias; p.colsum_out = a.colsum_out;
     p.lda = a.lda; p.ldb = a.ldb; p.ldc = a.ldc; p.ldaux = a.ldaux;
     p.M = a.M; p.N = a.N; p.K = a.K; p.kchunk = kchunk;
+    static const int same = getenv("VIT_DEBUG_SAME_TILE") ? 1 : 0;
+    p.debug_same_tile = same;
     return p;
 }
 
@@ -652,9 +708,13 @@ static void launch_bf16(const GemmArgs& a, const GemmParams& p, dim3 grid, hipSt
 
 template <bool AK, bool BKC>
 static void launch_g2(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStream_t s) {
+    static const int sched = getenv("VIT_G2_SCHED") ? atoi(getenv("VIT_G2_SCHED")) : 1;
     switch (a.epi) {
 #define VIT_CASE(E) \
-    case E: g2::gemm_kernel<AK, BKC, E><<<grid, g2::NT, 0, s>>>(p); break;
+    case E:                                                                    \
+        if (sched) g2::gemm_kernel<AK, BKC, E, true><<<grid, g2::NT, 0, s>>>(p);  \
+        else g2::gemm_kernel<AK, BKC, E, false><<<grid, g2::NT, 0, s>>>(p);       \
+        break;
         VIT_CASE(EPI_F32_STORE)
         VIT_CASE(EPI_F32_ACC)
         VIT_CASE(EPI_F32_ATOMIC)
@@ -662,9 +722,15 @@ static void launch_g2(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStre
         VIT_CASE(EPI_BF16_GELU)
         VIT_CASE(EPI_F32_RESID)
         VIT_CASE(EPI_BF16_DGELU)
+        VIT_CASE(EPI_F32_SLAB)
 #undef VIT_CASE
         default: set_error("gemm_bf16: unsupported epilogue %d", a.epi); return;
     }
+}
+
+static int grid_blocks(long long n) {
+    long long b = (n + 255) / 256;
+    return (int)(b < 1 ? 1 : (b > 4096 ? 4096 : b));
 }
 
 static int gemm_variant() {
@@ -684,20 +750,37 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s) {
         return;
     }
     const bool big = a.K % g2::KTILE == 0 && a.M >= 256 && a.N >= 256 && gemm_variant() == 2 &&
-                     (a.a_kcontig && a.b_kcontig || getenv("VIT_G2_ALL"));
+                     !getenv("VIT_G2_KK_ONLY");
     if (big) {
         const int tiles = cdiv(a.M, g2::BM) * cdiv(a.N, g2::BN);
         int split = 1;
         if (a.epi == EPI_F32_ATOMIC) split = a.splitk > 0 ? a.splitk : choose_split_waves(tiles, a.K / g2::KTILE);
         int kchunk = cdiv(cdiv(a.K, split), g2::KTILE) * g2::KTILE;
         split = cdiv(a.K, kchunk);
-        GemmParams p = make_params(a, kchunk);
+        GemmArgs b = a;
+        float* slab = nullptr;
+        if (a.epi == EPI_F32_ATOMIC && split > 1 && a.N % 4 == 0) {
+            // split-K partials to fp32 slabs + one reduce (no float atomics in the GEMM)
+            const size_t need = (size_t)split * a.M * a.N * sizeof(float);
+            slab = a.ws ? (a.ws_bytes >= need ? a.ws : nullptr) : (float*)workspace(need);
+            if (slab) {
+                b.epi = EPI_F32_SLAB;
+                b.C = slab;
+                b.ldc = a.N;
+            }
+        }
+        GemmParams p = make_params(b, kchunk);
         dim3 grid(tiles, split);
-        if (a.a_kcontig && a.b_kcontig) launch_g2<true, true>(a, p, grid, s);
-        else if (a.a_kcontig && !a.b_kcontig) launch_g2<true, false>(a, p, grid, s);
-        else if (!a.a_kcontig && !a.b_kcontig) launch_g2<false, false>(a, p, grid, s);
-        else launch_g2<false, true>(a, p, grid, s);
+        if (a.a_kcontig && a.b_kcontig) launch_g2<true, true>(b, p, grid, s);
+        else if (a.a_kcontig && !a.b_kcontig) launch_g2<true, false>(b, p, grid, s);
+        else if (!a.a_kcontig && !a.b_kcontig) launch_g2<false, false>(b, p, grid, s);
+        else launch_g2<false, true>(b, p, grid, s);
         after_launch("gemm_bf16_256");
+        if (slab) {
+            slab_reduce_k<<<grid_blocks((long long)a.M * a.N / 4), 256, 0, s>>>(
+                (float*)a.C, a.ldc, slab, a.M, a.N, split);
+            after_launch("gemm_slab_reduce");
+        }
         return;
     }
     const int tiles = cdiv(a.M, bf::BM) * cdiv(a.N, bf::BN);
@@ -713,6 +796,8 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s) {
     else if (!a.a_kcontig && !a.b_kcontig) launch_bf16<false, false>(a, p, grid, s);
     else launch_bf16<false, true>(a, p, grid, s);
     after_launch("gemm_bf16");
+    if (a.colsum_out && a.epi == EPI_BF16_DGELU)  // the 128x128 kernel has no fused column sums
+        colsum_bf16(a.colsum_out, (const bf16_t*)a.C, a.M, a.N, a.ldc, s);
 }
 
 void colsum_f32(float* dbias, const float* X, int M, int N, long long ld, hipStream_t s) {

@@ -206,19 +206,20 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_k(float* __restrict__ dinp, bf
                                                     const float* __restrict__ dres_in,
                                                     float* __restrict__ dweight,
                                                     float* __restrict__ dbias,
+                                                    float* __restrict__ dsum,
                                                     const float* __restrict__ dout,
                                                     const float* __restrict__ inp,
                                                     const float* __restrict__ weight,
                                                     const float* __restrict__ mean,
                                                     const float* __restrict__ rstd, long long rows,
                                                     int C) {
-    extern __shared__ float sm[];  // [4 waves][2][C]
+    extern __shared__ float sm[];  // [4 waves][3][C]
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    float4 w4[NV], dw[NV], db[NV];
+    float4 w4[NV], dw[NV], db[NV], ds[NV];
 #pragma unroll
     for (int j = 0; j < NV; j++) {
         w4[j] = reinterpret_cast<const float4*>(weight)[lane + 64 * j];
-        dw[j] = db[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        dw[j] = db[j] = ds[j] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     const long long nwaves = (long long)gridDim.x * 4;
     for (long long row = blockIdx.x * 4LL + wave; row < rows; row += nwaves) {
@@ -253,6 +254,7 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_k(float* __restrict__ dinp, bf
                 const float4 ri = reinterpret_cast<const float4*>(dres_in + row * C)[k];
                 const float4 t = make_float4(ri.x + dv.x, ri.y + dv.y, ri.z + dv.z, ri.w + dv.w);
                 *o = t;
+                ds[j].x += t.x; ds[j].y += t.y; ds[j].z += t.z; ds[j].w += t.w;
                 if (dinp_bf)
                     reinterpret_cast<uint2*>(dinp_bf + row * C)[k] =
                         make_uint2(pack_bf16x2(t.x, t.y), pack_bf16x2(t.z, t.w));
@@ -263,16 +265,18 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_k(float* __restrict__ dinp, bf
             }
         }
     }
-    float* mw = sm + wave * 2 * C;
+    float* mw = sm + wave * 3 * C;
 #pragma unroll
     for (int j = 0; j < NV; j++) {
         reinterpret_cast<float4*>(mw)[lane + 64 * j] = dw[j];
         reinterpret_cast<float4*>(mw + C)[lane + 64 * j] = db[j];
+        reinterpret_cast<float4*>(mw + 2 * C)[lane + 64 * j] = ds[j];
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < 2 * C; i += 256) {
-        const float t = sm[i] + sm[2 * C + i] + sm[4 * C + i] + sm[6 * C + i];
-        atomicAdd(i < C ? dweight + i : dbias + (i - C), t);
+    const int nsum = dsum ? 3 * C : 2 * C;
+    for (int i = threadIdx.x; i < nsum; i += 256) {
+        const float t = sm[i] + sm[3 * C + i] + sm[6 * C + i] + sm[9 * C + i];
+        atomicAdd(i < C ? dweight + i : (i < 2 * C ? dbias + (i - C) : dsum + (i - 2 * C)), t);
     }
 }
 
@@ -418,9 +422,9 @@ static int ln_bwd_grid(long long rows) {
     return (int)(g < 1 ? 1 : (g > 2048 ? 2048 : g));
 }
 static void ln_backward_any(float* dinp, bf16_t* dinp_bf, const float* dres_in, float* dw,
-                            float* db, const float* dout, const float* inp, const float* w,
-                            const float* mean, const float* rstd, long long rows, int C,
-                            hipStream_t s) {
+                            float* db, float* dsum, const float* dout, const float* inp,
+                            const float* w, const float* mean, const float* rstd, long long rows,
+                            int C, hipStream_t s) {
     if (rows <= 0) return;
     const bool vec = C % 256 == 0 && C <= 2048 &&
                      (((uintptr_t)dinp | (uintptr_t)dout | (uintptr_t)inp | (uintptr_t)w |
@@ -429,12 +433,14 @@ static void ln_backward_any(float* dinp, bf16_t* dinp_bf, const float* dres_in, 
         ln_bwd_k<float><<<ln_bwd_grid(rows), 256, 2 * C * sizeof(float), s>>>(
             dinp, dinp_bf, dres_in, dw, db, dout, inp, w, mean, rstd, rows, C);
         after_launch("layernorm_backward");
+        if (dsum) colsum_f32(dsum, dinp, (int)rows, C, C, s);
         return;
     }
     long long g = (rows + 15) / 16;  // ~4 rows per wave
     const int grid = (int)(g < 1 ? 1 : (g > 1024 ? 1024 : g));
-    const size_t lds = 8 * (size_t)C * sizeof(float);
-#define VIT_LNB(NV) ln_bwd_vec_k<NV><<<grid, 256, lds, s>>>(dinp, dinp_bf, dres_in, dw, db, dout, inp, w, mean, rstd, rows, C)
+    const size_t lds = 12 * (size_t)C * sizeof(float);
+    if (dsum && !dres_in) { set_error("layernorm_backward: output column sum needs dres_in"); return; }
+#define VIT_LNB(NV) ln_bwd_vec_k<NV><<<grid, 256, lds, s>>>(dinp, dinp_bf, dres_in, dw, db, dsum, dout, inp, w, mean, rstd, rows, C)
     switch (C / 256) {
         case 1: VIT_LNB(1); break;
         case 2: VIT_LNB(2); break;
@@ -451,12 +457,14 @@ static void ln_backward_any(float* dinp, bf16_t* dinp_bf, const float* dres_in, 
 void ln_backward_f32(float* dinp, float* dw, float* db, const float* dout, const float* inp,
                      const float* w, const float* mean, const float* rstd, long long rows, int C,
                      hipStream_t s) {
-    ln_backward_any(dinp, nullptr, nullptr, dw, db, dout, inp, w, mean, rstd, rows, C, s);
+    ln_backward_any(dinp, nullptr, nullptr, dw, db, nullptr, dout, inp, w, mean, rstd, rows, C, s);
 }
 void ln_backward_fused(float* dres_out, bf16_t* dres_out_bf, const float* dres_in, float* dw,
-                       float* db, const float* dout, const float* inp, const float* w,
-                       const float* mean, const float* rstd, long long rows, int C, hipStream_t s) {
-    ln_backward_any(dres_out, dres_out_bf, dres_in, dw, db, dout, inp, w, mean, rstd, rows, C, s);
+                       float* db, float* dres_colsum, const float* dout, const float* inp,
+                       const float* w, const float* mean, const float* rstd, long long rows, int C,
+                       hipStream_t s) {
+    ln_backward_any(dres_out, dres_out_bf, dres_in, dw, db, dres_colsum, dout, inp, w, mean, rstd,
+                    rows, C, s);
 }
 void convert_f2bf(bf16_t* out, const float* inp, long long n, hipStream_t s) {
     if (n <= 0) return;

@@ -13,10 +13,12 @@ void ln_forward_bf16(bf16_t* out, float* mean, float* rstd, const float* inp, co
 void ln_backward_f32(float* dinp, float* dw, float* db, const float* dout, const float* inp,
                      const float* w, const float* mean, const float* rstd, long long rows, int C,
                      hipStream_t s);
-// dres_out = dres_in + LN_dinp(dout);  dres_out_bf = bf16(dres_out) (nullable)
+// dres_out = dres_in + LN_dinp(dout);  dres_out_bf = bf16(dres_out) (nullable);
+// dres_colsum += column sums of dres_out (nullable: the next bias gradient, fused)
 void ln_backward_fused(float* dres_out, bf16_t* dres_out_bf, const float* dres_in, float* dw,
-                       float* db, const float* dout, const float* inp, const float* w,
-                       const float* mean, const float* rstd, long long rows, int C, hipStream_t s);
+                       float* db, float* dres_colsum, const float* dout, const float* inp,
+                       const float* w, const float* mean, const float* rstd, long long rows, int C,
+                       hipStream_t s);
 void convert_f2bf(bf16_t* out, const float* inp, long long n, hipStream_t s);
 void sgd(float* p, const float* g, long long n, float lr, hipStream_t s);
 void softmax_rows(float* probs, const float* logits, long long rows, int V, hipStream_t s);
@@ -41,6 +43,8 @@ void attn_backward_f32(float* dinp, float* dpreatt, float* datt, const float* do
 bool attn_fused_supported(int T, int C, int NH);
 void attn_forward_fused(bf16_t* out, float* lse, const bf16_t* qkv, int B, int T, int C, int NH,
                         hipStream_t s);
+// dqkv_colsum (nullable, [3C]) += column sums of dqkv (the qkv bias gradient, fused)
 void attn_backward_fused(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t* out,
-                         const float* lse, int B, int T, int C, int NH, hipStream_t s);
+                         const float* lse, int B, int T, int C, int NH, hipStream_t s,
+                         float* dqkv_colsum = nullptr, float* part_ws = nullptr);
 }  // namespace vit

@@ -94,6 +94,9 @@ struct Trainer {
 
     float* params = nullptr;
     float* grads = nullptr;
+    float* gemm_ws = nullptr;     // split-K slabs of the wgrad GEMMs (stream-ordered on s)
+    float* attn_part = nullptr;   // per-(b,h) qkv-bias partial sums of the attention backward
+    size_t gemm_ws_bytes = 0;
     bf16_t* pbf = nullptr;
     float* pixels = nullptr;
     int* labels = nullptr;
@@ -337,6 +340,10 @@ struct Trainer {
             datty = alloc<bf16_t>(BT * C);
             dqkv = alloc<bf16_t>(BT * 3 * C);
             dpatch_bf = alloc<bf16_t>((long long)B * NP * C);
+            // slabs: <= 32 splits of the largest weight gradient (4C x C)
+            gemm_ws_bytes = (size_t)32 * 4 * C * (size_t)std::max(C, KP) * sizeof(float);
+            gemm_ws = alloc<float>((long long)(gemm_ws_bytes / sizeof(float)));
+            attn_part = alloc<float>((long long)B * NH * 3 * 64);
         } else {
             patches_f = alloc<float>((long long)B * NP * KP);
             dpatch_f = alloc<float>((long long)B * NP * C);
@@ -494,6 +501,7 @@ struct Trainer {
         w.A = dout; w.lda = OC; w.a_kcontig = false;
         w.B = inp; w.ldb = Cin; w.b_kcontig = false;
         w.C = dW; w.ldc = Cin; w.M = OC; w.N = Cin; w.K = (int)BT; w.epi = EPI_F32_ATOMIC;
+        w.ws = gemm_ws; w.ws_bytes = gemm_ws_bytes;
         gemm(cls, w, true);
     }
 
@@ -503,6 +511,12 @@ struct Trainer {
         head_backward(dcur);
         chunk_done(0);
         convert_f2bf(dres_bf, dcur, BT * C, s);
+        // bias gradients are fused into the kernels that produce each gradient tensor:
+        //   fcproj_b += colsum(dres3): LN1-backward of layer l+1 (head rows for the last layer)
+        //   fc_b     += colsum(dfch):  fcproj dgrad epilogue
+        //   attproj_b+= colsum(dres2): LN2-backward
+        //   qkv_b    += colsum(dqkv):  attention backward
+        colsum_f32(G(P_FCPROJB, L - 1), dcls_x, B, C, C, s);
         for (int l = L - 1; l >= 0; l--) {
             LayerActs& a = la[l];
             const float* x = l == 0 ? encoded : la[l - 1].res3;
@@ -511,18 +525,19 @@ struct Trainer {
             d1.A = dres_bf; d1.lda = C; d1.B = W(P_FCPROJW, l); d1.ldb = 4 * C; d1.b_kcontig = false;
             d1.C = dfch; d1.ldc = 4 * C; d1.aux = a.fch; d1.ldaux = 4 * C;
             d1.M = (int)BT; d1.N = 4 * C; d1.K = C; d1.epi = EPI_BF16_DGELU;
+            d1.colsum_out = G(P_FCB, l);
             gemm(TC_FCPROJ_DGRAD, d1, true);
-            wgrad(TC_FCPROJ_WGRAD, dres_bf, C, a.fchg, 4 * C, G(P_FCPROJW, l), G(P_FCPROJB, l));
+            wgrad(TC_FCPROJ_WGRAD, dres_bf, C, a.fchg, 4 * C, G(P_FCPROJW, l), nullptr);
             // fc: dln2 = dfch . fcw
             GemmArgs d2;
             d2.A = dfch; d2.lda = 4 * C; d2.B = W(P_FCW, l); d2.ldb = C; d2.b_kcontig = false;
             d2.C = dln; d2.ldc = C; d2.M = (int)BT; d2.N = C; d2.K = 4 * C; d2.epi = EPI_F32_STORE;
             gemm(TC_FC_DGRAD, d2, true);
-            wgrad(TC_FC_WGRAD, dfch, 4 * C, a.ln2, C, G(P_FCW, l), G(P_FCB, l));
-            // ln2 backward + residual: dres2 = dres3 + LN2'(dln2)
+            wgrad(TC_FC_WGRAD, dfch, 4 * C, a.ln2, C, G(P_FCW, l), nullptr);
+            // ln2 backward + residual: dres2 = dres3 + LN2'(dln2); attproj_b += colsum(dres2)
             tbeg(TC_LN_BWD, 0);
-            ln_backward_fused(dnxt, dres_bf, dcur, G(P_LN2W, l), G(P_LN2B, l), dln, a.res2,
-                              P(P_LN2W, l), a.ln2_mean, a.ln2_rstd, BT, C, s);
+            ln_backward_fused(dnxt, dres_bf, dcur, G(P_LN2W, l), G(P_LN2B, l), G(P_ATTPROJB, l), dln,
+                              a.res2, P(P_LN2W, l), a.ln2_mean, a.ln2_rstd, BT, C, s);
             tend();
             std::swap(dcur, dnxt);
             // attproj
@@ -530,19 +545,22 @@ struct Trainer {
             d3.A = dres_bf; d3.lda = C; d3.B = W(P_ATTPROJW, l); d3.ldb = C; d3.b_kcontig = false;
             d3.C = datty; d3.ldc = C; d3.M = (int)BT; d3.N = C; d3.K = C; d3.epi = EPI_BF16_STORE;
             gemm(TC_PROJ_DGRAD, d3, true);
-            wgrad(TC_PROJ_WGRAD, dres_bf, C, a.atty, C, G(P_ATTPROJW, l), G(P_ATTPROJB, l));
-            // attention
+            wgrad(TC_PROJ_WGRAD, dres_bf, C, a.atty, C, G(P_ATTPROJW, l), nullptr);
+            // attention (+ qkv_b)
             tbeg(TC_ATTN_BWD, 8.0 * B * (double)T * T * C);
-            attn_backward_fused(dqkv, datty, a.qkv, a.atty, a.lse, B, T, C, NH, s);
+            attn_backward_fused(dqkv, datty, a.qkv, a.atty, a.lse, B, T, C, NH, s, G(P_QKVB, l),
+                                attn_part);
             tend();
             // qkv
             GemmArgs d4;
             d4.A = dqkv; d4.lda = 3 * C; d4.B = W(P_QKVW, l); d4.ldb = C; d4.b_kcontig = false;
             d4.C = dln; d4.ldc = C; d4.M = (int)BT; d4.N = C; d4.K = 3 * C; d4.epi = EPI_F32_STORE;
             gemm(TC_QKV_DGRAD, d4, true);
-            wgrad(TC_QKV_WGRAD, dqkv, 3 * C, a.ln1, C, G(P_QKVW, l), G(P_QKVB, l));
+            wgrad(TC_QKV_WGRAD, dqkv, 3 * C, a.ln1, C, G(P_QKVW, l), nullptr);
+            // ln1 backward: dres = dres2 + LN1'(dln1); fcproj_b of layer l-1 += colsum(dres)
             tbeg(TC_LN_BWD, 0);
-            ln_backward_fused(dnxt, dres_bf, dcur, G(P_LN1W, l), G(P_LN1B, l), dln, x, P(P_LN1W, l),
+            ln_backward_fused(dnxt, dres_bf, dcur, G(P_LN1W, l), G(P_LN1B, l),
+                              l > 0 ? G(P_FCPROJB, l - 1) : nullptr, dln, x, P(P_LN1W, l),
                               a.ln1_mean, a.ln1_rstd, BT, C, s);
             tend();
             std::swap(dcur, dnxt);
@@ -556,6 +574,7 @@ struct Trainer {
             w.A = dpatch_bf; w.lda = C; w.a_kcontig = false;
             w.B = patches_bf; w.ldb = KP; w.b_kcontig = false;
             w.C = G(P_PATCH_W); w.ldc = KP; w.M = C; w.N = KP; w.K = B * NP; w.epi = EPI_F32_ATOMIC;
+            w.ws = gemm_ws; w.ws_bytes = gemm_ws_bytes;
             gemm_bf16(w, s);
         }
         patch_small_grads(G(P_CLS), G(P_WPE), G(P_PATCH_B), dcur, B, T, C, s);
