@@ -35,6 +35,25 @@ PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip t
 PEAK_HBM_GBS = 8000.0
 
 
+def pmc_traffic(kernel_class):
+    """HBM bytes per launch of `kernel_class` from the newest committed PMC summary
+    (profiles/<tag>_traffic.json, written by tools/summarize_profile.py from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench; FETCH_SIZE x 2 on gfx950).
+    PMC counters cannot be read from inside a timed run, so this is the latest profiled
+    measurement of the same kernel, named by its source file in `traffic_source`."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        c = d.get("classes", {}).get(kernel_class)
+        if c:
+            return c["bytes_per_dispatch"], os.path.relpath(f, ROOT)
+    return None, None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -198,8 +217,11 @@ def main():
             d = gemms[dom]
             avg_ms = d["ms"] / d["calls"]
             ach = d["flops"] / d["calls"] / (avg_ms * 1e-3) / 1e12
+            traffic, tsrc = pmc_traffic(dom)
             roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS,
-                    "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                    "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
+                    "traffic": round(traffic) if traffic else None, "traffic_unit": "bytes/launch",
+                    "traffic_source": tsrc,
                     "avg_launch_ms": round(avg_ms, 4), "flops_per_launch": d["flops"] / d["calls"]}
         ksum = {k: {"ms_per_step": round(v["ms"] / args.steps, 3), "calls_per_step": v["calls"] // args.steps,
                     "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1) if v["flops"] and v["ms"] else None}

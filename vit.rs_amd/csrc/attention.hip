@@ -510,15 +510,26 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_k(bf16_t* __restrict__ dqk
     }
 }
 
-// out[s*C + h*64 + d] += sum_b part[(b*NH + h)][s*64 + d]
-__global__ void attn_colsum_reduce_k(float* __restrict__ out, const float* __restrict__ part, int B,
-                                     int NH, int C) {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // over 3*C
-    if (idx >= 3 * C) return;
-    const int sct = idx / C, c = idx - sct * C, h = c / HS, d = c - h * HS;
+// out[s*C + h*64 + d] += sum_b part[(b*NH + h)][s*64 + d]; one 1024-thread block per (s, h):
+// 16 batch lanes x 64 columns, fixed-order tree over the lanes (deterministic).
+__global__ __launch_bounds__(1024) void attn_colsum_reduce_k(float* __restrict__ out,
+                                                             const float* __restrict__ part, int B,
+                                                             int NH, int C) {
+    __shared__ float red[16][HS];
+    const int sh = blockIdx.x;  // 0 .. 3*NH-1
+    const int sct = sh / NH, h = sh - sct * NH;
+    const int d = threadIdx.x & (HS - 1), lane_b = threadIdx.x >> 6;
     float t = 0.f;
-    for (int b = 0; b < B; b++) t += part[((long long)b * NH + h) * 3 * HS + sct * HS + d];
-    out[idx] += t;
+#pragma unroll 4
+    for (int b = lane_b; b < B; b += 16) t += part[((long long)b * NH + h) * 3 * HS + sct * HS + d];
+    red[lane_b][d] = t;
+    __syncthreads();
+    if (lane_b == 0) {
+        float a = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; i++) a += red[i][d];
+        out[sct * C + h * HS + d] += a;
+    }
 }
 }  // namespace fa
 
@@ -582,7 +593,7 @@ void attn_backward_fused(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, co
                        dqkv_colsum ? part_ws : nullptr)
     after_launch("attention_backward_fused");
     if (dqkv_colsum) {
-        fa::attn_colsum_reduce_k<<<cdiv(3 * C, 256), 256, 0, s>>>(dqkv_colsum, part_ws, B, NH, C);
+        fa::attn_colsum_reduce_k<<<3 * NH, 1024, 0, s>>>(dqkv_colsum, part_ws, B, NH, C);
         after_launch("attention_colsum_reduce");
     }
 }

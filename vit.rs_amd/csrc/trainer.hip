@@ -669,7 +669,7 @@ struct Trainer {
 
     // ------------------------------------------------------------------ DP
     void chunk_done(int c) {
-        if (!comm || world <= 1 || !overlap) return;
+        if (!comm || !overlap) return;
         VIT_HIP(hipEventRecord(chunk_ev[c], s));
         VIT_HIP(hipStreamWaitEvent(s_comm, chunk_ev[c], 0));
         const long long o = chunk_off[c], n = chunk_off[c + 1] - chunk_off[c];
@@ -677,7 +677,7 @@ struct Trainer {
         if (r != ncclSuccess) set_error("ncclAllReduce(chunk %d): %s", c, ncclGetErrorString(r));
     }
     void finish_allreduce() {
-        if (!comm || world <= 1) return;
+        if (!comm) return;  // (world 1 with a communicator still runs RCCL: the tested path)
         if (!overlap) {
             ncclResult_t r = ncclAllReduce(grads, grads, (size_t)arena_elems, ncclFloat32, ncclSum, comm, s);
             if (r != ncclSuccess) set_error("ncclAllReduce: %s", ncclGetErrorString(r));
@@ -797,7 +797,7 @@ int vit_trainer_forward(vit_trainer_t* h, int b_global) {
 int vit_trainer_zero_grad(vit_trainer_t* h) {
     auto& t = h->t;
     // the previous step's all-reduce must be done with the arena before it is cleared
-    if (t.comm && t.world > 1) {
+    if (t.comm) {
         VIT_HIP(hipEventRecord(t.comm_done, t.s_comm));
         VIT_HIP(hipStreamWaitEvent(t.s, t.comm_done, 0));
     }
@@ -858,7 +858,10 @@ int vit_trainer_dp_init(vit_trainer_t* h, int rank, int world, const char* uid, 
     t.rank = rank;
     t.world = world;
     t.overlap = overlap;
-    if (world <= 1) return 0;
+    if (world < 1 || rank < 0 || rank >= world) {
+        set_error("vit_trainer_dp_init: bad rank %d / world %d", rank, world);
+        return 1;
+    }
     ncclUniqueId id;
     memcpy(&id, uid, sizeof(id));
     VIT_HIP(hipSetDevice(t.device));
