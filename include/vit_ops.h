@@ -126,6 +126,17 @@ void layernorm_forward_bf16(uint16_t* out, float* mean, float* rstd, const float
 void gemm_bf16_ex(void* C, long long ldc, const uint16_t* A, long long lda, int a_kcontig,
                   const uint16_t* B, long long ldb, int b_kcontig, const float* bias,
                   float* dbias, int M, int N, int K, int epi, int splitk);
+/* the fused epilogues of the trainer's GEMMs: epi 4 C = pre = acc + bias, C2 = gelu(pre)
+ * (both bf16); 5 C_f32 = acc + bias + aux_f32; 6 C_bf16 = acc * gelu'(aux_bf16) and, when
+ * colsum_out is not NULL, colsum_out[n] += sum_m C[m][n]; 0 / 3 as gemm_bf16_ex. */
+void gemm_bf16_fused(void* C, void* C2, long long ldc, const void* aux, long long ldaux,
+                     const uint16_t* A, long long lda, int a_kcontig, const uint16_t* B,
+                     long long ldb, int b_kcontig, const float* bias, float* colsum_out, int M,
+                     int N, int K, int epi);
+/* tools: GEMM engine selection (1 = 128x128, 2 = 256x256 one workgroup per CU, the default,
+ * 4 = 256x128 two per CU) and diagnostics (flag 2: skip epilogues, main-loop timing only) */
+void gemm_bf16_set_variant(int variant);
+void gemm_bf16_set_debug(int flags);
 void convert_f32_to_bf16(uint16_t* out, const float* inp, long long n);
 void convert_bf16_to_f32(float* out, const uint16_t* inp, long long n);
 

@@ -105,19 +105,26 @@ def test_bf16_trainer_vs_oracle(gpu, oracle32, name, B):
 
 
 def test_training_reduces_loss(gpu):
+    """40 SGD steps on one batch: both precisions fit it (loss / 10) and the bf16 trajectory tracks
+    the fp32 one over the first steps.  lr 0.1: at 0.5 the fp32 run itself diverges for a while
+    (2.4 -> 14 -> 25 before recovering), which made the end point chaotic."""
     v = gpu
     cfg = v.data.CONFIGS["test_h64"]
     params = v.data.init_params(cfg, "parity", seed=1)
     px, lab = v.data.synthetic_batch(cfg, 8, seed=2)
+    traj = {}
     for prec in (v.VIT_FP32, v.VIT_BF16):
         m = v.ViT.build(cfg, 8, prec, params=params)
         m.set_batch(px, lab)
         losses = []
         for _ in range(40):
-            m.train_step(0.5)
+            m.train_step(0.1)
             losses.append(float(v.lib().vit_trainer_mean_loss(m.h)))
-        assert losses[-1] < 0.6 * losses[0], (prec, losses[0], losses[-1])
+        assert losses[-1] < 0.1 * losses[0], (prec, [round(x, 3) for x in losses])
+        traj[prec] = np.array(losses)
         m.close()
+    early = np.abs(traj[v.VIT_BF16][:8] / traj[v.VIT_FP32][:8] - 1).max()
+    assert early < 5e-2, (early, traj)
 
 
 def test_vit_b16_full_size_step(gpu):

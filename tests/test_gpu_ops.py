@@ -282,10 +282,21 @@ def test_error_channel(gpu):
 
 
 # ------------------------------------------------------------------ generic bf16 GEMM engine
-@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (304, 520, 128), (776, 1000, 192), (512, 264, 640)])
+@pytest.fixture(params=[2, 3, 4])
+def engine(request, gpu):
+    """Run a test under each GEMM engine (2 = 256x256, 3 = its stream-K persistent form, 4 = 256x128
+    two per CU), then restore the default."""
+    gpu.lib().gemm_bf16_set_variant(request.param)
+    yield request.param
+    gpu.lib().gemm_bf16_set_variant(2)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (304, 520, 128), (776, 1000, 192), (512, 264, 640),
+                                   (1000, 136, 96)])
 @pytest.mark.parametrize("ak,bk", [(1, 1), (1, 0), (0, 0), (0, 1)])
-def test_gemm_bf16_layouts(gpu, M, N, K, ak, bk):
-    """Every operand layout through both GEMM kernels (256x256 LDS-DMA and 128x128), ragged M/N."""
+def test_gemm_bf16_layouts(gpu, engine, M, N, K, ak, bk):
+    """Every operand layout through the GEMM engines (LDS-DMA 256x128 / 256x256, and the 128x128
+    kernel for shapes they do not take), ragged M/N."""
     v = gpu
     rng = np.random.default_rng(M * 7 + N * 3 + K + 10 * ak + bk)
     a = rng.normal(size=(M, K)).astype(np.float32)
@@ -308,3 +319,55 @@ def test_gemm_bf16_layouts(gpu, M, N, K, ak, bk):
         assert rel_err(got, want) < (1e-2 if epi == 3 else 2e-3), epi
         if dbias is not None:
             assert rel_err(dbias.numpy(), ar.sum(1)) < 2e-3
+
+
+def _gelu64(x):
+    s = np.sqrt(2.0 / np.pi)
+    return 0.5 * x * (1.0 + np.tanh(s * (x + 0.044715 * x ** 3)))
+
+
+def _gelu_grad64(x):  # D4-corrected derivative (sech^2 of the tanh argument)
+    s = np.sqrt(2.0 / np.pi)
+    a = s * (x + 0.044715 * x ** 3)
+    th = np.tanh(a)
+    return 0.5 * (1 + th) + 0.5 * x * (1 - th * th) * s * (1 + 3 * 0.044715 * x * x)
+
+
+@pytest.mark.parametrize("M,N,K", [(1576, 768, 192), (520, 384, 256), (6304, 3072, 192), (8192, 2304, 96)])
+def test_gemm_bf16_fused_epilogues(gpu, engine, M, N, K):
+    """The trainer's fused epilogues against float64 numpy: bias+GELU pair (fc forward),
+    bias+fp32 residual (proj / fcproj forward), GELU' x aux with the fused column sum
+    (fcproj dgrad -> fc bias gradient)."""
+    v = gpu
+    rng = np.random.default_rng(M + N + K)
+    a = rng.uniform(-1, 1, size=(M, K)).astype(np.float32)
+    w = (rng.uniform(-1, 1, size=(N, K)) * 0.1).astype(np.float32)
+    ab, wb = v.bf16_bits(a), v.bf16_bits(w)
+    ar = v.bf16_to_f32(ab).reshape(M, K).astype(np.float64)
+    wr = v.bf16_to_f32(wb).reshape(N, K).astype(np.float64)
+    bias = rng.normal(size=N).astype(np.float32)
+    A, W = D(v, ab, np.uint16), D(v, wb, np.uint16)
+    pre = ar @ wr.T + bias
+    # 4: C = pre (bf16), C2 = gelu(pre) (bf16)
+    c1, c2 = Z(v, M * N, np.uint16), Z(v, M * N, np.uint16)
+    v.call("gemm_bf16_fused", c1, c2, N, None, 0, A, K, 1, W, K, 1, D(v, bias), None, M, N, K, 4)
+    assert rel_err(v.bf16_to_f32(c1.numpy()).reshape(M, N), pre) < 1e-2
+    assert rel_err(v.bf16_to_f32(c2.numpy()).reshape(M, N), _gelu64(pre)) < 1e-2
+    # 5: C_f32 = acc + bias + aux_f32
+    res = rng.normal(size=(M, N)).astype(np.float32)
+    c3 = Z(v, M * N)
+    v.call("gemm_bf16_fused", c3, None, N, D(v, res), N, A, K, 1, W, K, 1, D(v, bias), None, M, N, K, 5)
+    assert rel_err(c3.numpy().reshape(M, N), pre + res) < 2e-3
+    # 6: C_bf16 = (acc) * gelu'(aux_bf16); colsum += column sums of C (dgrad layout: W is [K][N])
+    wkn = (rng.uniform(-1, 1, size=(K, N)) * 0.1).astype(np.float32)
+    wkb = v.bf16_bits(wkn)
+    wkr = v.bf16_to_f32(wkb).reshape(K, N).astype(np.float64)
+    x = rng.normal(size=(M, N)).astype(np.float32)
+    xb = v.bf16_bits(x)
+    xr = v.bf16_to_f32(xb).reshape(M, N).astype(np.float64)
+    c4, cs = Z(v, M * N, np.uint16), D(v, np.ones(N, np.float32))
+    v.call("gemm_bf16_fused", c4, None, N, D(v, xb, np.uint16), N, A, K, 1, D(v, wkb, np.uint16), N, 0,
+           None, cs, M, N, K, 6)
+    want = (ar @ wkr) * _gelu_grad64(xr)
+    assert rel_err(v.bf16_to_f32(c4.numpy()).reshape(M, N), want) < 1e-2
+    assert rel_err(cs.numpy(), 1.0 + want.sum(0)) < 1e-2

@@ -1,7 +1,12 @@
-"""Microbenchmark of the bf16 GEMM engine at the ViT-B/16 B=256 training shapes (HIP events).
+"""Microbenchmark of the bf16 GEMM engines at the trainer's ViT-B/16 B=256 GEMMs (HIP events).
 
-    python tools/bench_gemm.py [--iters 20] [--batch 256]
-Prints one line per GEMM (layout, M, N, K, ms, TFLOP/s).  VIT_GEMM=1 selects the 128x128 kernel.
+    python tools/bench_gemm.py [--iters 10] [--variants 2,4] [--no-epi]
+
+Every GEMM of one transformer layer (forward, dgrad, wgrad) with the epilogue the trainer uses
+(bias, GELU pair, fp32 residual, GELU' with the fused fc-bias column sum, split-K slabs).  Engines
+are A/B'd in ONE process, interleaved round by round (cdna_hip_programming.md §5.4 rule 24); the
+median over rounds is printed.  --no-epi adds main-loop-only rows (gemm_bf16_set_debug(2)).
+Operands are uniform [-1, 1) bf16 (random data: zero-filled operands read ~20 % fast).
 """
 import argparse
 import os
@@ -15,54 +20,101 @@ from vitpkg import vit  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--C", type=int, default=768)
-    ap.add_argument("--only", default=None, help="comma-separated shape names")
+    ap.add_argument("--variants", default="2,4")
+    ap.add_argument("--no-epi", action="store_true")
+    ap.add_argument("--only", default=None, help="comma-separated GEMM names")
     args = ap.parse_args()
     L = vit.lib()
     assert L.vit_init(0) == 0
     C, BT = args.C, args.batch * 197
     rng = np.random.default_rng(0)
-    maxe = BT * 4 * C
-    buf_a = vit.DeviceArray.from_numpy(vit.bf16_bits(rng.uniform(-1, 1, size=maxe).astype(np.float32)), np.uint16)
-    buf_b = vit.DeviceArray.from_numpy(vit.bf16_bits(rng.uniform(-1, 1, size=16 * C * C).astype(np.float32)), np.uint16)
-    buf_b2 = vit.DeviceArray.from_numpy(vit.bf16_bits(rng.uniform(-1, 1, size=maxe).astype(np.float32)), np.uint16)
-    out = vit.DeviceArray.zeros(maxe * 2, np.float32)
-    bias = vit.DeviceArray.zeros(4 * C, np.float32)
+    big = BT * 4 * C
+
+    def dev_bf16(n):
+        return vit.DeviceArray.from_numpy(vit.bf16_bits(rng.uniform(-1, 1, size=n).astype(np.float32)), np.uint16)
+
+    act = dev_bf16(big)       # A operands (activations / output gradients)
+    act2 = dev_bf16(big)      # B operand of wgrad
+    wts = dev_bf16(4 * C * C)  # weights
+    aux16 = dev_bf16(big)     # GELU' input
+    aux32 = vit.DeviceArray.from_numpy(rng.uniform(-1, 1, size=BT * C).astype(np.float32))
+    out = vit.DeviceArray.zeros(big, np.float32)
+    out2 = vit.DeviceArray.zeros(big, np.uint16)
+    bias = vit.DeviceArray.from_numpy(rng.uniform(-1, 1, size=4 * C).astype(np.float32))
+    csum = vit.DeviceArray.zeros(4 * C, np.float32)
     e0, e1 = L.vit_event_create(), L.vit_event_create()
-    # (name, M, N, K, ak, bk, epi)
-    shapes = []
-    for nm, oc, ic in (("qkv", 3 * C, C), ("proj", C, C), ("fc", 4 * C, C), ("fcproj", C, 4 * C)):
-        shapes.append((f"fwd_{nm}", BT, oc, ic, 1, 1, 3))
-        shapes.append((f"dgrad_{nm}", BT, ic, oc, 1, 0, 0))
-        shapes.append((f"wgrad_{nm}", oc, ic, BT, 0, 0, 2))
-    tot_ms, tot_fl = 0.0, 0.0
+
+    # name, M, N, K, a_kcontig, lda, b_kcontig, ldb, epi
+    g = [
+        ("fwd_qkv", BT, 3 * C, C, 1, C, 1, C, 3),
+        ("fwd_proj", BT, C, C, 1, C, 1, C, 5),
+        ("fwd_fc", BT, 4 * C, C, 1, C, 1, C, 4),
+        ("fwd_fcproj", BT, C, 4 * C, 1, 4 * C, 1, 4 * C, 5),
+        ("dgrad_fcproj", BT, 4 * C, C, 1, C, 0, 4 * C, 6),
+        ("dgrad_fc", BT, C, 4 * C, 1, 4 * C, 0, C, 0),
+        ("dgrad_proj", BT, C, C, 1, C, 0, C, 3),
+        ("dgrad_qkv", BT, C, 3 * C, 1, 3 * C, 0, C, 0),
+        ("wgrad_fcproj", C, 4 * C, BT, 0, C, 0, 4 * C, 2),
+        ("wgrad_fc", 4 * C, C, BT, 0, 4 * C, 0, C, 2),
+        ("wgrad_proj", C, C, BT, 0, C, 0, C, 2),
+        ("wgrad_qkv", 3 * C, C, BT, 0, 3 * C, 0, C, 2),
+    ]
     if args.only:
         keep = set(args.only.split(","))
-        shapes = [sh for sh in shapes if sh[0] in keep]
-    for name, M, N, K, ak, bk, epi in shapes:
-        lda = K if ak else M
-        ldb = K if bk else N
-        B_ = buf_b if (ak and name.startswith(("fwd", "dgrad"))) else buf_b2
-        def run():
-            L.gemm_bf16_ex(out.ptr, N, buf_a.ptr, lda, ak, B_.ptr, ldb, bk,
-                           bias.ptr if epi != 2 else None, None, M, N, K, epi, 0)
-        for _ in range(3):
-            run()
-        L.vit_sync()
-        vit.check(name)
-        L.vit_event_record(e0)
-        for _ in range(args.iters):
-            run()
-        L.vit_event_record(e1)
-        ms = L.vit_event_elapsed_ms(e0, e1) / args.iters
-        vit.check(name)
+        g = [x for x in g if x[0] in keep]
+    variants = [int(v) for v in args.variants.split(",")]
+    modes = [0, 2] if args.no_epi else [0]
+
+    def run(name, M, N, K, ak, lda, bk, ldb, epi):
+        if epi == 2:
+            L.gemm_bf16_ex(out.ptr, N, act.ptr, lda, ak, act2.ptr, ldb, bk, None, None, M, N, K, 2, 0)
+        else:
+            aux = aux16.ptr if epi == 6 else (aux32.ptr if epi == 5 else None)
+            L.gemm_bf16_fused(out.ptr if epi in (0, 5) else out2.ptr, out.ptr if epi == 4 else None, N,
+                              aux, N, act.ptr, lda, ak, wts.ptr, ldb, bk,
+                              bias.ptr if epi != 6 else None, csum.ptr if epi == 6 else None, M, N, K, epi)
+
+    res = {}
+    for rd in range(args.rounds):
+        for sh in g:
+            for var in variants:
+                for mode in modes:
+                    L.gemm_bf16_set_variant(var)
+                    L.gemm_bf16_set_debug(mode)
+                    for _ in range(2):
+                        run(*sh)
+                    L.vit_sync()
+                    vit.check(sh[0])
+                    L.vit_event_record(e0)
+                    for _ in range(args.iters):
+                        run(*sh)
+                    L.vit_event_record(e1)
+                    L.vit_sync()
+                    ms = L.vit_event_elapsed_ms(e0, e1) / args.iters
+                    vit.check(sh[0])
+                    res.setdefault((sh[0], var, mode), []).append(ms)
+    L.gemm_bf16_set_debug(0)
+    tot = {}
+    print(f"{'gemm':14s} {'M':>6s} {'N':>5s} {'K':>6s} epi " +
+          " ".join(f"{'v%d%s' % (v, '/noepi' if m else ''):>16s}" for v in variants for m in modes))
+    for sh in g:
+        name, M, N, K = sh[:4]
         fl = 2.0 * M * N * K
-        tot_ms += ms
-        tot_fl += fl
-        print(f"{name:14s} M={M:6d} N={N:5d} K={K:6d}  {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TFLOP/s", flush=True)
-    print(f"{'all':14s} {tot_ms:8.3f} ms per layer-set  {tot_fl / tot_ms / 1e9:8.1f} TFLOP/s")
+        cells = []
+        for v in variants:
+            for m in modes:
+                ms = float(np.median(res[(name, v, m)]))
+                tot[(v, m)] = tot.get((v, m), 0.0) + ms
+                cells.append(f"{ms * 1e3:7.1f}us {fl / ms / 1e9:6.0f}TF")
+        print(f"{name:14s} {M:6d} {N:5d} {K:6d} {sh[8]:3d} " + " ".join(f"{c:>16s}" for c in cells), flush=True)
+    fl_all = sum(2.0 * x[1] * x[2] * x[3] for x in g)
+    print("total per layer: " + "  ".join(
+        f"v{v}{'/noepi' if m else ''} {tot[(v, m)]:.3f} ms ({fl_all / tot[(v, m)] / 1e9:.0f} TF/s)"
+        for v in variants for m in modes))
 
 
 if __name__ == "__main__":

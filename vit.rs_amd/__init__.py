@@ -17,7 +17,7 @@ import sys
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libvit_hip.so")
+LIB_PATH = os.environ.get("VIT_LIB") or os.path.join(HERE, "libvit_hip.so")  # VIT_LIB: A/B builds
 
 from . import data  # noqa: E402  (configs, canonical layout, seeded synthetic inputs)
 
@@ -79,6 +79,8 @@ _SIGS = {
     "attention_backward_fused_bf16": (None, [P, P, P, P, P, I, I, I, I]),
     "layernorm_forward_bf16": (None, [P, P, P, P, P, P, I, I, I]),
     "gemm_bf16_ex": (None, [P, LL, P, LL, I, P, LL, I, P, P, I, I, I, I, I]),
+    "gemm_bf16_fused": (None, [P, P, LL, P, LL, P, LL, I, P, LL, I, P, P, I, I, I, I]),
+    "gemm_bf16_set_variant": (None, [I]), "gemm_bf16_set_debug": (None, [I]),
     "convert_f32_to_bf16": (None, [P, P, LL]),
     "convert_bf16_to_f32": (None, [P, P, LL]),
     # trainer

@@ -22,6 +22,7 @@ bool has_error();
 hipStream_t stream();
 bool sync_each_op();
 void* workspace(size_t bytes);  // per-thread device scratch, grown on demand
+void* sk_workspace(size_t bytes);  // per-thread stream-K GEMM scratch, zero-filled on growth
 void after_launch(const char* what);
 }  // namespace vit
 
@@ -71,6 +72,24 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
     float th = tanhf(a);
     float sech2 = 1.0f - th * th;  // == 1/cosh^2(a)
     return 0.5f * (1.0f + th) + x * 0.5f * sech2 * s * (1.0f + 3.0f * 0.044715f * x * x);
+}
+
+// The same two functions in the logistic form used by the bf16 GEMM epilogues, where they run
+// on every element of a 256x256 output tile per CU and tanhf (a long libm sequence) made the
+// fc / fcproj-dgrad epilogues VALU-bound:  0.5(1 + tanh a) = sigmoid(2a), 1 - tanh^2 a =
+// 4 sigmoid(2a)(1 - sigmoid(2a)).  One v_exp + one v_rcp per element; |error| <~ 1e-7
+// absolute against the tanh form, far below the bf16 rounding of the stored value.
+__device__ __forceinline__ float gelu_fast_f(float x) {
+    const float s2 = 2.0f * 0.7978845608028654f;
+    const float a2 = s2 * (x + 0.044715f * x * x * x);  // 2a
+    return x * __frcp_rn(1.0f + __expf(-a2));
+}
+__device__ __forceinline__ float gelu_grad_fast_f(float x) {
+    const float s = 0.7978845608028654f;
+    const float x2 = x * x;
+    const float a2 = 2.0f * s * (x + 0.044715f * x2 * x);
+    const float sg = __frcp_rn(1.0f + __expf(-a2));  // 0.5(1 + tanh a)
+    return sg + 2.0f * x * sg * (1.0f - sg) * s * (1.0f + 3.0f * 0.044715f * x2);
 }
 
 // optimizer_step (train_vit.rs:740): p -= lr*g with two roundings like the Rust reference

@@ -14,6 +14,8 @@ struct Ctx {
     char msg[512] = {0};
     void* ws = nullptr;
     size_t ws_bytes = 0;
+    void* sk = nullptr;  // stream-K scratch (flags + partial tiles), zero-filled
+    size_t sk_bytes = 0;
 };
 thread_local Ctx g_ctx;
 int g_sync_each = -1;
@@ -53,6 +55,24 @@ void* workspace(size_t bytes) {
         g_ctx.ws_bytes = want;
     }
     return g_ctx.ws;
+}
+void* sk_workspace(size_t bytes) {
+    if (bytes > g_ctx.sk_bytes) {
+        if (g_ctx.sk) {
+            VIT_HIP(hipDeviceSynchronize());
+            VIT_HIP(hipFree(g_ctx.sk));
+        }
+        g_ctx.sk = nullptr;
+        g_ctx.sk_bytes = 0;
+        if (hipMalloc(&g_ctx.sk, bytes) != hipSuccess) {
+            set_error("sk_workspace: hipMalloc(%zu) failed", bytes);
+            return nullptr;
+        }
+        VIT_HIP(hipMemset(g_ctx.sk, 0, bytes));  // the hand-off flags start (and end) at 0
+        VIT_HIP(hipDeviceSynchronize());
+        g_ctx.sk_bytes = bytes;
+    }
+    return g_ctx.sk;
 }
 void after_launch(const char* what) {
     hipError_t e = hipGetLastError();

@@ -46,7 +46,12 @@ struct GemmArgs {
     // (ordered on the context stream); the trainer passes its own buffer for its stream.
     float* ws = nullptr;
     size_t ws_bytes = 0;
+    // stream-K scratch (hand-off flags + partial tiles, gemm_sk_bytes()), zero-filled before first
+    // use and left zeroed by every launch; nullptr = the calling thread's.  Launches sharing one
+    // scratch must be ordered (same stream).
+    char* sk_ws = nullptr;
 };
+size_t gemm_sk_bytes();
 
 // fp32 operands, exact-fp32 MFMA (v_mfma_f32_16x16x4_f32); any shape/stride. Parity path.
 void gemm_f32(const GemmArgs& a, hipStream_t s);
@@ -54,6 +59,10 @@ void gemm_f32(const GemmArgs& a, hipStream_t s);
 // operands, lda/ldb%8==0, the contiguous dim of an M/N-contig operand %8==0, N%4==0.
 void gemm_bf16(const GemmArgs& a, hipStream_t s);
 bool gemm_bf16_supported(const GemmArgs& a);
+// engine selection for A/B measurements in one process: 1 = 128x128, 2 = 256x256 (1 WG/CU, default),
+// 4 = 256x128 (2 WG/CU); anything else = 2 (the default); debug flag 2 = skip epilogues (main loop only)
+void gemm_set_variant(int v);
+void gemm_set_debug(int flags);
 
 // column sums: dbias[n] += sum_m X[m*ld + n]   (X fp32 or bf16)
 void colsum_f32(float* dbias, const float* X, int M, int N, long long ld, hipStream_t s);

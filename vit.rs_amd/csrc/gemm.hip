@@ -31,7 +31,36 @@ struct GemmParams {
     int M, N, K;
     int kchunk;  // K range per split (multiple of the K tile)
     int debug_same_tile;
+    int no_epi;  // diagnostic (gemm_bf16_set_debug): skip the epilogue, keep the accumulators live
+    int tiles;   // output tiles of the launch (the grid is tiles x K-splits)
 };
+
+// (tile, K-split) of this workgroup.  Workgroups are dealt round-robin over the 8 XCDs in
+// linear-id order (x fastest), so the XCD-aware remap runs over the whole (split, tile) grid: the
+// ~1/8 of the grid on one XCD is a contiguous range of the same K-split's tiles, which share
+// their A and B K-slices in that XCD's L2 (split-K wgrad launches have tiles x splits blocks).
+__device__ __forceinline__ void split_remap(int tiles, int& tile, int& split) {
+    const int nwg = gridDim.x * gridDim.y;
+    const int l = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, nwg);
+    split = l / tiles;
+    tile = l - split * tiles;
+}
+__device__ __forceinline__ int split_index(int tiles) {
+    int t, s;
+    split_remap(tiles, t, s);
+    return s;
+}
+
+// diagnostic: time the main loop alone (the accumulators stay live so nothing is eliminated)
+template <int NA, int NB>
+__device__ __forceinline__ bool skip_epilogue(const GemmParams& p, f32x4_t (&acc)[NA][NB]) {
+    if (!p.no_epi) return false;
+#pragma unroll
+    for (int a = 0; a < NA; a++)
+#pragma unroll
+        for (int b = 0; b < NB; b++) asm volatile("" ::"v"(acc[a][b]));
+    return true;
+}
 
 // epilogue for one lane's C[m][n..n+3] (n % 4 == 0, m < M, n < N)
 template <int EPI>
@@ -63,25 +92,159 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, int m, int n, f32x
         *reinterpret_cast<uint2*>((bf16_t*)p.C + off) =
             make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
         *reinterpret_cast<uint2*>((bf16_t*)p.C2 + off) =
-            make_uint2(pack_bf16x2(gelu_f(v[0]), gelu_f(v[1])),
-                       pack_bf16x2(gelu_f(v[2]), gelu_f(v[3])));
+            make_uint2(pack_bf16x2(gelu_fast_f(v[0]), gelu_fast_f(v[1])),
+                       pack_bf16x2(gelu_fast_f(v[2]), gelu_fast_f(v[3])));
     } else if constexpr (EPI == EPI_F32_RESID) {
         const float4 r = *reinterpret_cast<const float4*>((const float*)p.aux +
                                                           (long long)m * p.ldaux + n);
         *reinterpret_cast<float4*>((float*)p.C + off) =
             make_float4(v[0] + r.x, v[1] + r.y, v[2] + r.z, v[3] + r.w);
     } else if constexpr (EPI == EPI_F32_SLAB) {
-        float* slab = (float*)p.C + (long long)blockIdx.y * p.M * p.ldc;
+        float* slab = (float*)p.C + (long long)split_index(p.tiles) * p.M * p.ldc;
         *reinterpret_cast<float4*>(slab + off) = make_float4(v[0], v[1], v[2], v[3]);
     } else if constexpr (EPI == EPI_BF16_DGELU) {
         const uint2 h = *reinterpret_cast<const uint2*>((const bf16_t*)p.aux +
                                                         (long long)m * p.ldaux + n);
         const float x0 = __uint_as_float(h.x << 16), x1 = __uint_as_float(h.x & 0xffff0000u);
         const float x2 = __uint_as_float(h.y << 16), x3 = __uint_as_float(h.y & 0xffff0000u);
-        v[0] *= gelu_grad_f(x0); v[1] *= gelu_grad_f(x1);
-        v[2] *= gelu_grad_f(x2); v[3] *= gelu_grad_f(x3);
+        v[0] *= gelu_grad_fast_f(x0); v[1] *= gelu_grad_fast_f(x1);
+        v[2] *= gelu_grad_fast_f(x2); v[3] *= gelu_grad_fast_f(x3);
         *reinterpret_cast<uint2*>((bf16_t*)p.C + off) =
             make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+    }
+}
+
+// ------------------------------------------------------------- row-contiguous (staged) epilogue
+// Columns n..n+7 of row m (n % 8 == 0), v = raw accumulators: one 16-B (bf16) or 2 x 16-B (fp32)
+// access per lane and operand, so a wave instruction covers whole 128-B lines.  cs accumulates
+// the column sums of the DGELU output (fused bias gradient).
+template <int EPI>
+__device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, float (&v)[8],
+                                          float (&cs)[8]) {
+    if constexpr (EPI != EPI_F32_ATOMIC && EPI != EPI_BF16_DGELU && EPI != EPI_F32_SLAB) {
+        if (p.bias) {
+            const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
+            const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
+            v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+            v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+        }
+    }
+    const long long off = (long long)m * p.ldc + n;
+    auto st_f32 = [&](float* q) {
+        reinterpret_cast<float4*>(q)[0] = make_float4(v[0], v[1], v[2], v[3]);
+        reinterpret_cast<float4*>(q)[1] = make_float4(v[4], v[5], v[6], v[7]);
+    };
+    auto pack8 = [&](const float (&w)[8]) {
+        return make_uint4(pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3]), pack_bf16x2(w[4], w[5]),
+                          pack_bf16x2(w[6], w[7]));
+    };
+    if constexpr (EPI == EPI_F32_STORE) {
+        st_f32((float*)p.C + off);
+    } else if constexpr (EPI == EPI_F32_ACC) {
+        float* q = (float*)p.C + off;
+        const float4 o0 = reinterpret_cast<const float4*>(q)[0];
+        const float4 o1 = reinterpret_cast<const float4*>(q)[1];
+        v[0] += o0.x; v[1] += o0.y; v[2] += o0.z; v[3] += o0.w;
+        v[4] += o1.x; v[5] += o1.y; v[6] += o1.z; v[7] += o1.w;
+        st_f32(q);
+    } else if constexpr (EPI == EPI_F32_ATOMIC) {
+        float* q = (float*)p.C + off;
+#pragma unroll
+        for (int j = 0; j < 8; j++) atomicAdd(q + j, v[j]);
+    } else if constexpr (EPI == EPI_F32_SLAB) {
+        st_f32((float*)p.C + (long long)split_index(p.tiles) * p.M * p.ldc + off);
+    } else if constexpr (EPI == EPI_BF16_STORE) {
+        *reinterpret_cast<uint4*>((bf16_t*)p.C + off) = pack8(v);
+    } else if constexpr (EPI == EPI_BF16_GELU) {
+        float gv[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) gv[j] = gelu_fast_f(v[j]);
+        *reinterpret_cast<uint4*>((bf16_t*)p.C + off) = pack8(v);
+        *reinterpret_cast<uint4*>((bf16_t*)p.C2 + off) = pack8(gv);
+    } else if constexpr (EPI == EPI_F32_RESID) {
+        const float* r = (const float*)p.aux + (long long)m * p.ldaux + n;
+        const float4 r0 = reinterpret_cast<const float4*>(r)[0];
+        const float4 r1 = reinterpret_cast<const float4*>(r)[1];
+        v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
+        v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
+        st_f32((float*)p.C + off);
+    } else if constexpr (EPI == EPI_BF16_DGELU) {
+        const uint4 h = *reinterpret_cast<const uint4*>((const bf16_t*)p.aux + (long long)m * p.ldaux + n);
+        const uint32_t hw[4] = {h.x, h.y, h.z, h.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            v[2 * j] *= gelu_grad_fast_f(__uint_as_float(hw[j] << 16));
+            v[2 * j + 1] *= gelu_grad_fast_f(__uint_as_float(hw[j] & 0xffff0000u));
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) cs[j] += v[j];
+        *reinterpret_cast<uint4*>((bf16_t*)p.C + off) = pack8(v);
+    }
+}
+
+// Epilogue of one wave's 128x64 accumulator tile (8x4 16x16 tiles; lane (i,g) of tile (a,b) holds
+// row 16a+i, columns 16b+4g..+3) through a wave-private LDS area of 64 x 68 fp32 (17 KiB, two
+// passes of 64 rows): each lane then owns 8 consecutive columns of a row, so every global load
+// and store of the epilogue is a 16-B access and a wave instruction covers 8 rows x 128 B (bf16)
+// or 8 rows x 256 B (fp32) instead of 16 rows x 32 B.  Callers guarantee the area is free
+// (every wave past the main loop and its LDS-DMA retired).
+constexpr int STG_LD = 68;                       // padded row (floats): conflict-free b128 access
+constexpr int STG_WAVE_BYTES = 64 * STG_LD * 4;  // 17,408 B per wave
+template <int EPI>
+__device__ __forceinline__ void staged_epilogue(const GemmParams& p, f32x4_t (&acc)[8][4],
+                                                char* stage, int lane, int m0, int n0) {
+    float* st = reinterpret_cast<float*>(stage);
+    const int i = lane & 15, g = lane >> 4;
+    const int rr = lane >> 3, cc = (lane & 7) * 8;
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int pass = 0; pass < 2; pass++) {
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+                *reinterpret_cast<f32x4_t*>(st + (a * 16 + i) * STG_LD + b * 16 + 4 * g) = acc[pass * 4 + a][b];
+#pragma unroll
+        for (int it = 0; it < 8; it++) {
+            const int r = it * 8 + rr;
+            float v[8];
+            const f32x4_t lo = *reinterpret_cast<const f32x4_t*>(st + r * STG_LD + cc);
+            const f32x4_t hi = *reinterpret_cast<const f32x4_t*>(st + r * STG_LD + cc + 4);
+            v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+            v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+            const int m = m0 + pass * 64 + r, n = n0 + cc;
+            if (m >= p.M) continue;
+            if (n + 8 <= p.N) {
+                epilogue8<EPI>(p, m, n, v, cs);
+            } else if (n + 4 <= p.N) {  // ragged N (N % 8 == 4): the 4-wide form
+                f32x4_t t = lo;
+                epilogue<EPI>(p, m, n, t);
+                if constexpr (EPI == EPI_BF16_DGELU) {
+                    const uint2 h = *reinterpret_cast<const uint2*>((const bf16_t*)p.aux + (long long)m * p.ldaux + n);
+                    cs[0] += lo[0] * gelu_grad_fast_f(__uint_as_float(h.x << 16));
+                    cs[1] += lo[1] * gelu_grad_fast_f(__uint_as_float(h.x & 0xffff0000u));
+                    cs[2] += lo[2] * gelu_grad_fast_f(__uint_as_float(h.y << 16));
+                    cs[3] += lo[3] * gelu_grad_fast_f(__uint_as_float(h.y & 0xffff0000u));
+                }
+            }
+        }
+    }
+    if constexpr (EPI == EPI_BF16_DGELU) {
+        if (p.colsum_out) {  // fused bias gradient of the next GEMM: column sums of this output
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                float t = cs[j];
+                t += __shfl_xor(t, 8, 64);
+                t += __shfl_xor(t, 16, 64);
+                t += __shfl_xor(t, 32, 64);
+                cs[j] = t;
+            }
+            if (rr == 0) {
+#pragma unroll
+                for (int j = 0; j < 8; j++)
+                    if (n0 + cc + j < p.N) atomicAdd(p.colsum_out + n0 + cc + j, cs[j]);
+            }
+        }
     }
 }
 
@@ -362,17 +525,19 @@ __device__ __forceinline__ void barrier_lds() {
 // NSLOT slots, DMA two steps ahead; a wave retires its own pieces of step s+1 (vmcnt) in phase 1
 // of step s, two barriers (three with the stagger) before anyone reads them; a slot is refilled
 // >= 6 barriers after its last read; every barrier is preceded by lgkmcnt(0).
+constexpr int SMEM_BYTES = NSLOT * SLOT_BYTES > 8 * STG_WAVE_BYTES ? NSLOT * SLOT_BYTES : 8 * STG_WAVE_BYTES;
 template <bool AK, bool BKC, int EPI, bool SCHED>
 __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
-    __shared__ __attribute__((aligned(1024))) char smem[NSLOT * SLOT_BYTES];
+    __shared__ __attribute__((aligned(1024))) char smem[SMEM_BYTES];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
     const int ntm = cdiv(p.M, BM), ntn = cdiv(p.N, BN);
-    const int wg = xcd_remap(blockIdx.x, ntm * ntn);
+    int wg, split;
+    split_remap(ntm * ntn, wg, split);
     int tm0 = (wg / ntn) * BM, tn0 = (wg % ntn) * BN;
     if (p.debug_same_tile) { tm0 = 0; tn0 = 0; }  // diagnostic: every block streams one tile (L2)
-    const int kbeg = blockIdx.y * p.kchunk;
+    const int kbeg = split * p.kchunk;
     const int kend = min(p.K, kbeg + p.kchunk);
     const int nk = (kend - kbeg) / BK;
     const bf16_t* A = (const bf16_t*)p.A;
@@ -469,38 +634,405 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
         }
     }
 
+    if (skip_epilogue(p, acc)) return;
+    // every wave's LDS-DMA retired and its reads done before the ring becomes staging space
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    staged_epilogue<EPI>(p, acc, smem + wave * STG_WAVE_BYTES, lane, tm0 + wm * 128, tn0 + wn * 64);
+}
+}  // namespace g2
+
+// ============================================================================ stream-K persistent
+// g3: the g2 tile / pipeline (256x256, 8 waves, LDS-DMA ring, staggered halves) run as ONE
+// persistent workgroup per CU over a contiguous range of the launch's (tile, K-step) space
+// ("stream-K").  Why: with one tile per workgroup every CU reached its epilogue at the same
+// moment, so the output stores (128-512 KiB per tile) went out as chip-wide HBM bursts with the
+// matrix pipes idle, and N = 768 launches (591 tiles) ran 2.31 tiles per CU in 3 rounds.  Here
+// each CU gets W/P K-steps; tile boundaries fall at a different point on every CU, so epilogues
+// are spread over the launch, and the ring keeps streaming across tile boundaries (the DMA for
+// the next tile's first steps is already in flight while a tile's epilogue runs).
+// A tile cut by a range boundary is computed in two parts: the CU whose range STARTS inside the
+// tile (it reaches that part first) writes its fp32 partial accumulators with write-through
+// (sc1) stores, each wave then adds 1 to the boundary's flag; the CU whose range ENDS inside the
+// tile (it reaches the tile's first K-steps last) polls the flag with sc1 loads, reads the
+// partial with sc1 loads (MI355X_MICROARCH.md, hand-off table row 3: no release/acquire fence),
+// adds it and runs the epilogue.  Every consumer wave adds 1 as well; the one that brings the
+// count to 16 resets it to 0 for the next launch.  W/P >= S (tiles >= CUs) so a tile is cut at
+// most once.  Epilogues go through a dedicated 32 KiB LDS staging area (4 KiB per wave: 16 rows
+// x 64 fp32, XOR-swizzled), so they never touch the ring.
+namespace g3 {
+using g2::BM;
+using g2::BN;
+using g2::BK;
+using g2::NT;
+using g2::NSLOT;
+using g2::IMG_BYTES;
+using g2::SLOT_BYTES;
+constexpr int RING_BYTES = NSLOT * SLOT_BYTES;        // 128 KiB
+constexpr int STG16_WAVE = 16 * 64 * 4;               // 4 KiB per wave
+constexpr int SMEM_BYTES = RING_BYTES + 8 * STG16_WAVE;  // 160 KiB
+constexpr int PART_BYTES = 8 * 32 * 64 * 16;          // fp32 partial tile, fragment-native: 256 KiB
+constexpr int FLAG_BYTES = 4096;                      // flags[1024] in front of the partials
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// 16-row staged epilogue: pass a writes acc[a][0..3] (rows 16a..16a+15 of the wave tile) into the
+// wave's area (element (r, c) at r*256 + ((c/4 ^ r) * 16) + (c%4)*4: conflict-free for both the
+// fragment writes and the row reads); lane then owns row (lane>>3) + 8*it, columns 8*(lane&7)..+7.
+template <int EPI>
+__device__ __forceinline__ void staged_epilogue16(const GemmParams& p, f32x4_t (&acc)[8][4],
+                                                  char* stg, int lane, int m0, int n0) {
     const int i = lane & 15, g = lane >> 4;
-    f32x4_t csum[4] = {};
+    const int rr = lane >> 3, c8 = lane & 7;
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int a = 0; a < 8; a++) {
-        const int m = tm0 + wm * 128 + a * 16 + i;
-        if (m >= p.M) continue;
+        __builtin_amdgcn_sched_barrier(0);  // one pass at a time: no loads hoisted across passes
 #pragma unroll
-        for (int b = 0; b < 4; b++) {
-            const int n = tn0 + wn * 64 + b * 16 + 4 * g;
-            if (n >= p.N) continue;
-            epilogue<EPI>(p, m, n, acc[a][b]);
-            if constexpr (EPI == EPI_BF16_DGELU) csum[b] += acc[a][b];
+        for (int b = 0; b < 4; b++)
+            *reinterpret_cast<f32x4_t*>(stg + i * 256 + (((b * 4 + g) ^ i) << 4)) = acc[a][b];
+#pragma unroll
+        for (int it = 0; it < 2; it++) {
+            const int r = it * 8 + rr;
+            const f32x4_t lo = *reinterpret_cast<const f32x4_t*>(stg + r * 256 + (((2 * c8) ^ r) << 4));
+            const f32x4_t hi = *reinterpret_cast<const f32x4_t*>(stg + r * 256 + (((2 * c8 + 1) ^ r) << 4));
+            float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            const int m = m0 + a * 16 + r, n = n0 + c8 * 8;
+            if (m >= p.M) continue;
+            if (n + 8 <= p.N) {
+                epilogue8<EPI>(p, m, n, v, cs);
+            } else if (n + 4 <= p.N) {
+                f32x4_t t = lo;
+                epilogue<EPI>(p, m, n, t);
+                if constexpr (EPI == EPI_BF16_DGELU) {
+                    const uint2 h = *reinterpret_cast<const uint2*>((const bf16_t*)p.aux + (long long)m * p.ldaux + n);
+                    cs[0] += lo[0] * gelu_grad_fast_f(__uint_as_float(h.x << 16));
+                    cs[1] += lo[1] * gelu_grad_fast_f(__uint_as_float(h.x & 0xffff0000u));
+                    cs[2] += lo[2] * gelu_grad_fast_f(__uint_as_float(h.y << 16));
+                    cs[3] += lo[3] * gelu_grad_fast_f(__uint_as_float(h.y & 0xffff0000u));
+                }
+            }
         }
     }
     if constexpr (EPI == EPI_BF16_DGELU) {
-        if (p.colsum_out) {  // fused bias gradient of the next GEMM: column sums of this output
+        if (p.colsum_out) {
 #pragma unroll
-            for (int b = 0; b < 4; b++)
+            for (int j = 0; j < 8; j++) {
+                float t = cs[j];
+                t += __shfl_xor(t, 8, 64);
+                t += __shfl_xor(t, 16, 64);
+                t += __shfl_xor(t, 32, 64);
+                cs[j] = t;
+            }
+            if (rr == 0) {
 #pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    float t = csum[b][r];
-                    t += __shfl_xor(t, 1, 64);
-                    t += __shfl_xor(t, 2, 64);
-                    t += __shfl_xor(t, 4, 64);
-                    t += __shfl_xor(t, 8, 64);
-                    const int n = tn0 + wn * 64 + b * 16 + 4 * g + r;
-                    if (i == 0 && n < p.N) atomicAdd(p.colsum_out + n, t);
-                }
+                for (int j = 0; j < 8; j++)
+                    if (n0 + c8 * 8 + j < p.N) atomicAdd(p.colsum_out + n0 + c8 * 8 + j, cs[j]);
+            }
         }
     }
 }
-}  // namespace g2
+
+template <bool AK, bool BKC, int EPI>
+__global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p, char* __restrict__ sk_ws, int S) {
+    __shared__ __attribute__((aligned(1024))) char smem[SMEM_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int ntn = cdiv(p.N, BN);
+    const int P = gridDim.x;
+    const int w = xcd_remap(blockIdx.x, P);  // XCD-contiguous ranges: neighbouring tiles share L2
+    const int Wtot = p.tiles * S;  // host guarantees < 2^31
+    const int g_begin = (int)((long long)Wtot * w / P), g_end = (int)((long long)Wtot * (w + 1) / P);
+    const bf16_t* A = (const bf16_t*)p.A;
+    const bf16_t* B = (const bf16_t*)p.B;
+    int* flags = reinterpret_cast<int*>(sk_ws);
+    char* parts = sk_ws + FLAG_BYTES;
+    char* stg = smem + RING_BYTES + wave * STG16_WAVE;
+
+    f32x4_t acc[8][4];
+
+    // global step gs -> ring slot, tile origin and k offset (clamped to the range's last step:
+    // re-staging it keeps the per-step DMA count, and so every vmcnt literal, uniform)
+    auto slot_of = [&](int gs) { return smem + ((gs - g_begin) & (NSLOT - 1)) * SLOT_BYTES; };
+    auto coords = [&](int gs, int& m0, int& n0, int& k0) {
+        const int c = gs < g_end ? gs : g_end - 1;
+        const int t = c / S, ks = c - t * S;
+        m0 = (t / ntn) * BM;
+        n0 = (t % ntn) * BN;
+        k0 = ks * BK;
+    };
+    auto issue_a = [&](int gs) {
+        int m0, n0, k0;
+        coords(gs, m0, n0, k0);
+        g2::stage<AK>(A, p.lda, m0, p.M, k0, slot_of(gs), wave, lane);
+    };
+    auto issue_b = [&](int gs) {
+        int m0, n0, k0;
+        coords(gs, m0, n0, k0);
+        g2::stage<BKC>(B, p.ldb, n0, p.N, k0, slot_of(gs) + IMG_BYTES, wave, lane);
+    };
+    auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto mfma_half = [&](int half, const bf16x8_t (&fa)[4], const bf16x8_t (&fb)[4]) {
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+                acc[half * 4 + a][b] =
+                    __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[b], fa[a], acc[half * 4 + a][b], 0, 0, 0);
+    };
+
+    const bool lagging = wave >= 4;
+    const bool any = g_end > g_begin;
+    if (any) {
+        issue_a(g_begin); issue_b(g_begin); issue_a(g_begin + 1); issue_b(g_begin + 1);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        bar();
+        if (lagging) {
+            __builtin_amdgcn_s_setprio(1);
+            bar();
+        }
+    }
+    int gs = g_begin;
+    while (gs < g_end) {
+        // ---- one tile segment [gs, seg_end) of tile t
+        const int t = gs / S;
+        const int tbeg = t * S, tend = tbeg + S;
+        const int seg_end = min(g_end, tend);
+        const bool starts_in = tbeg < g_begin;  // range starts inside t: this part is a partial
+        const bool ends_in = seg_end < tend;     // range ends inside t: the partial comes in here
+        if (ends_in) {
+            // t's later K-steps were the FIRST work of the next range: its partial is (almost
+            // surely) published; it becomes the starting value of the accumulators
+            int spins = 0;
+            while (__hip_atomic_load(flags + w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 8 &&
+                   spins < (1 << 24)) {
+                __builtin_amdgcn_s_sleep(4);
+                spins++;
+            }
+            __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+                parts + (long long)(w + 1) * PART_BYTES, (short)0, PART_BYTES, 0x00020000);
+#pragma unroll
+            for (int a = 0; a < 8; a++)
+#pragma unroll
+                for (int b = 0; b < 4; b++)
+                    acc[a][b] = __builtin_bit_cast(
+                        f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                     r, ((wave * 32 + a * 4 + b) * 64 + lane) * 16, 0, 16 /* sc1 */));
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) {
+                const int old = __hip_atomic_fetch_add(flags + w + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (old == 15) __hip_atomic_store(flags + w + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        } else {
+#pragma unroll
+            for (int a = 0; a < 8; a++)
+#pragma unroll
+                for (int b = 0; b < 4; b++) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        }
+        for (; gs < seg_end; gs++) {
+            const char* img = slot_of(gs);
+            bf16x8_t fb[4], alo[4], ahi[4];
+            // ---- phase 0
+#pragma unroll
+            for (int b = 0; b < 4; b++) fb[b] = g2::frag<BKC>(img + IMG_BYTES, wn * 64 + b * 16, lane);
+#pragma unroll
+            for (int a = 0; a < 4; a++) alo[a] = g2::frag<AK>(img, wm * 128 + a * 16, lane);
+            issue_a(gs + 2);
+            bar();
+            mfma_half(0, alo, fb);
+            bar();
+            // ---- phase 1
+#pragma unroll
+            for (int a = 0; a < 4; a++) ahi[a] = g2::frag<AK>(img, wm * 128 + (4 + a) * 16, lane);
+            asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // own pieces of step gs+1 landed
+            issue_b(gs + 2);
+            bar();
+            mfma_half(1, ahi, fb);
+            bar();
+        }
+        if (starts_in) {
+            // fragment-native fp32 partial, write-through (sc1); then count this wave in
+            __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+                parts + (long long)w * PART_BYTES, (short)0, PART_BYTES, 0x00020000);
+#pragma unroll
+            for (int a = 0; a < 8; a++)
+#pragma unroll
+                for (int b = 0; b < 4; b++)
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        __builtin_bit_cast(u32x4, acc[a][b]), r,
+                        ((wave * 32 + a * 4 + b) * 64 + lane) * 16, 0, 16 /* sc1 */);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) __hip_atomic_fetch_add(flags + w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (!skip_epilogue(p, acc)) {
+            const int m0 = (t / ntn) * BM + wm * 128, n0 = (t % ntn) * BN + wn * 64;
+            staged_epilogue16<EPI>(p, acc, stg, lane, m0, n0);
+        }
+    }
+    if (any && !lagging) bar();  // balance the stagger barrier
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(0);
+}
+}  // namespace g3
+
+// ============================================================================ bf16 GEMM, 256x128
+// Two workgroups per CU.  A 256x128x32 block tile on 256 threads = 4 waves (2 M x 2 N), one
+// wave per SIMD, 128x64 per wave (8x4 v_mfma_f32_16x16x32_bf16 tiles, as g2).  The LDS ring is
+// 3 slots x 24 KiB = 72 KiB, so two workgroups share a CU (144 KiB) and the hardware pairs
+// their waves on every SIMD: while one workgroup stores its epilogue (bias / GELU / residual,
+// HBM-bound for K = 768) or issues its fragment reads, the other keeps the matrix pipe busy.
+// With one 256x256 workgroup per CU those phases ran serialised with the MFMAs, and all CUs hit
+// their epilogues at the same moment.  Per K-step: counted vmcnt retires this wave's own pieces
+// of step s (step s+1 stays in flight across the barrier), one raw s_barrier, LDS-DMA of step
+// s+2 into the slot read at step s-1, 12 fragment reads, 32 MFMAs.
+namespace g4 {
+constexpr int BM = 256, BN = 128, BK = 32, NT = 256;
+constexpr int NSLOT = 3;
+constexpr int A_BYTES = BM * BK * 2;           // 16 KiB
+constexpr int B_BYTES = BN * BK * 2;           // 8 KiB
+constexpr int SLOT_BYTES = A_BYTES + B_BYTES;  // 24 KiB
+constexpr int KTILE = BK;                      // K granularity required of callers
+constexpr int PIECES = BM / 64 + BN / 64;      // LDS-DMA instructions per wave per K-step (6)
+static_assert(PIECES == 6, "vmcnt literal below");
+static_assert(NSLOT * SLOT_BYTES >= 4 * STG_WAVE_BYTES, "staged epilogue area");
+
+// K-contig image [R rows][32 k] (64 B rows): 16-B chunk' = chunk ^ ((row >> 1) & 3)
+__device__ __forceinline__ int kc_swz(int row) { return (row >> 1) & 3; }
+// M/N-contig image [32 k][R] (2R-byte rows): chunk' = chunk ^ f(k), f spreading the 8 k rows a
+// 32-lane half of ds_read_b64_tr_b16 touches over distinct 32-B bank groups
+template <int R>
+__device__ __forceinline__ int mn_swz(int k) {
+    if constexpr (R == 256) return ((k & 3) << 2) | (((k >> 3) & 1) << 1);
+    else return ((k & 3) << 1) | (((k >> 3) & 1) << 3);
+}
+
+// this wave's R/64 one-KiB pieces of an operand image (piece blk = 4j + wave)
+template <bool KC, int R>
+__device__ __forceinline__ void stage(const bf16_t* __restrict__ base, long long ld, int row0,
+                                      int rows_lim, int k0, char* img, int wave, int lane) {
+#pragma unroll
+    for (int j = 0; j < R / 64; j++) {
+        const int blk = j * 4 + wave;
+        const bf16_t* src;
+        if constexpr (KC) {
+            const int row = blk * 16 + (lane >> 2);
+            const int c = (lane & 3) ^ kc_swz(row);
+            const int gr = min(row0 + row, rows_lim - 1);
+            src = base + (long long)gr * ld + k0 + c * 8;
+        } else {
+            constexpr int CPR = R / 8;             // 16-B chunks per k row
+            constexpr int KPB = 64 / CPR;          // k rows per piece
+            const int k = blk * KPB + lane / CPR;
+            const int c = (lane % CPR) ^ mn_swz<R>(k);
+            const int gc = min(row0 + c * 8, rows_lim - 8);
+            src = base + (long long)(k0 + k) * ld + gc;
+        }
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(img + blk * 1024),
+                                         16, 0, 0);
+    }
+}
+
+// 8 bf16 of rows/cols [r0, r0+16) for the slot's 32-deep k: lane (i,g) gets k = 8g + j
+template <bool KC, int R>
+__device__ __forceinline__ bf16x8_t frag(const char* img, int r0, int lane) {
+    const int i = lane & 15, g = lane >> 4;
+    if constexpr (KC) {
+        const int r = r0 + i;
+        return *reinterpret_cast<const bf16x8_t*>(img + r * 64 + ((g ^ kc_swz(r)) << 4));
+    } else {
+        const int q = i >> 2, p = i & 3;
+        const int ch = (r0 >> 3) + (p >> 1);
+        const int k0 = 8 * g + q, k1 = k0 + 4;
+        const char* a0 = img + k0 * (2 * R) + ((ch ^ mn_swz<R>(k0)) << 4) + (p & 1) * 8;
+        const char* a1 = img + k1 * (2 * R) + ((ch ^ mn_swz<R>(k1)) << 4) + (p & 1) * 8;
+        const bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4_t, a0));
+        const bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4_t, a1));
+        return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+}
+
+// tile order inside the XCD-contiguous range: groups of GM M-tiles walked column by column, so
+// the workgroups resident on one XCD share a few A panels and a few B panels in its L2
+__device__ __forceinline__ void group_order(int t, int ntm, int ntn, int& tm, int& tn) {
+    constexpr int GM = 8;
+    const int per = GM * ntn;
+    const int grp = t / per;
+    const int first = grp * GM;
+    const int gsz = min(GM, ntm - first);
+    const int r = t - grp * per;
+    tm = first + r % gsz;
+    tn = r / gsz;
+}
+
+template <bool AK, bool BKC, int EPI>
+__global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
+    __shared__ __attribute__((aligned(1024))) char smem[NSLOT * SLOT_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int ntm = cdiv(p.M, BM), ntn = cdiv(p.N, BN);
+    int tm, tn, wg, split;
+    split_remap(ntm * ntn, wg, split);
+    group_order(wg, ntm, ntn, tm, tn);
+    const int tm0 = tm * BM, tn0 = tn * BN;
+    const int kbeg = split * p.kchunk;
+    const int kend = min(p.K, kbeg + p.kchunk);
+    const int nk = (kend - kbeg) / BK;
+    const bf16_t* A = (const bf16_t*)p.A;
+    const bf16_t* B = (const bf16_t*)p.B;
+
+    f32x4_t acc[8][4];
+#pragma unroll
+    for (int a = 0; a < 8; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    auto issue = [&](int st) {
+        char* sl = smem + (st % NSLOT) * SLOT_BYTES;
+        const int k0 = kbeg + st * BK;
+        stage<AK, BM>(A, p.lda, tm0, p.M, k0, sl, wave, lane);
+        stage<BKC, BN>(B, p.ldb, tn0, p.N, k0, sl + A_BYTES, wave, lane);
+    };
+    if (nk > 0) issue(0);
+    if (nk > 1) issue(1);
+    for (int kt = 0; kt < nk; kt++) {
+        // this wave's pieces of step kt have landed (step kt+1's stay in flight); its reads of
+        // step kt-1 are done; after the barrier both hold for every wave
+        __builtin_amdgcn_sched_barrier(0);
+        if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        if (kt + 2 < nk) issue(kt + 2);  // into the slot of step kt-1
+        const char* img = smem + (kt % NSLOT) * SLOT_BYTES;
+        bf16x8_t fa[8], fb[4];
+#pragma unroll
+        for (int b = 0; b < 4; b++) fb[b] = frag<BKC, BN>(img + A_BYTES, wn * 64 + b * 16, lane);
+#pragma unroll
+        for (int a = 0; a < 8; a++) fa[a] = frag<AK, BM>(img, wm * 128 + a * 16, lane);
+#pragma unroll
+        for (int a = 0; a < 8; a++)
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[b], fa[a], acc[a][b], 0, 0, 0);
+    }
+
+    if (skip_epilogue(p, acc)) return;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    staged_epilogue<EPI>(p, acc, smem + wave * STG_WAVE_BYTES, lane, tm0 + wm * 128, tn0 + wn * 64);
+}
+}  // namespace g4
 
 // ============================================================================ fp32 MFMA GEMM
 namespace f32 {
@@ -627,6 +1159,22 @@ __global__ __launch_bounds__(256) void slab_reduce_k(float* __restrict__ C, long
     }
 }
 
+// engine selection (gemm_bf16_set_variant; default from VIT_GEMM, else 2):
+//   1 = 128x128 register-staged, 2 = 256x256 one workgroup per CU, 3 = 2 as stream-K persistent
+//   (launches with >= 1 tile per CU; the rest, e.g. split-K wgrad, take 2), 4 = 256x128 two per CU
+static int g_variant = -1;
+static int g_debug_flags = 0;
+static int gemm_variant() {
+    if (g_variant < 0) {
+        const char* e = getenv("VIT_GEMM");
+        g_variant = e ? atoi(e) : 2;
+        if (g_variant != 1 && g_variant != 3 && g_variant != 4) g_variant = 2;
+    }
+    return g_variant;
+}
+void gemm_set_variant(int v) { g_variant = (v == 1 || v == 3 || v == 4) ? v : 2; }
+void gemm_set_debug(int flags) { g_debug_flags = flags; }
+
 static GemmParams make_params(const GemmArgs& a, int kchunk) {
     GemmParams p;
     p.A = a.A; p.B = a.B; p.C = a.C; p.C2 = a.C2; p.aux = a.aux; p.bias = a.bias; p.dbias = a.dbias; p.colsum_out = a.colsum_out;
@@ -634,6 +1182,8 @@ static GemmParams make_params(const GemmArgs& a, int kchunk) {
     p.M = a.M; p.N = a.N; p.K = a.K; p.kchunk = kchunk;
     static const int same = getenv("VIT_DEBUG_SAME_TILE") ? 1 : 0;
     p.debug_same_tile = same;
+    p.no_epi = (g_debug_flags & 2) ? 1 : 0;
+    p.tiles = 1;
     return p;
 }
 
@@ -733,13 +1283,123 @@ static int grid_blocks(long long n) {
     return (int)(b < 1 ? 1 : (b > 4096 ? 4096 : b));
 }
 
-static int gemm_variant() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("VIT_GEMM");
-        v = (e && e[0] == '1') ? 1 : 2;  // VIT_GEMM=1 forces the 128x128 register-staged kernel
+template <bool AK, bool BKC>
+static void launch_g4(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStream_t s) {
+    switch (a.epi) {
+#define VIT_CASE(E) \
+    case E: g4::gemm_kernel<AK, BKC, E><<<grid, g4::NT, 0, s>>>(p); break;
+        VIT_CASE(EPI_F32_STORE)
+        VIT_CASE(EPI_F32_ACC)
+        VIT_CASE(EPI_BF16_STORE)
+        VIT_CASE(EPI_BF16_GELU)
+        VIT_CASE(EPI_F32_RESID)
+        VIT_CASE(EPI_BF16_DGELU)
+        VIT_CASE(EPI_F32_SLAB)
+#undef VIT_CASE
+        default: set_error("gemm_bf16: unsupported epilogue %d", a.epi); return;
     }
-    return v;
+}
+
+// split-K for two-workgroups-per-CU kernels: the smallest split whose last round fills >= 90% of
+// the 512 workgroup slots, keeping >= 32 K-steps per split
+static int choose_split_g4(int tiles, int nk) {
+    int best = 1;
+    double best_eff = 0.0;
+    for (int s = 1; s <= 64 && nk / s >= 32; s++) {
+        const int blocks = tiles * s;
+        const int rounds = (blocks + 511) / 512;
+        const double eff = (double)blocks / (rounds * 512.0) * (blocks >= 256 ? 1.0 : blocks / 256.0);
+        if (eff > best_eff + 1e-9) { best_eff = eff; best = s; }
+        if (eff >= 0.9) break;
+    }
+    return best;
+}
+
+static void gemm_bf16_g4(const GemmArgs& a, hipStream_t s) {
+    const int tiles = cdiv(a.M, g4::BM) * cdiv(a.N, g4::BN);
+    int split = 1;
+    if (a.epi == EPI_F32_ATOMIC) split = a.splitk > 0 ? a.splitk : choose_split_g4(tiles, a.K / g4::KTILE);
+    int kchunk = cdiv(cdiv(a.K, split), g4::KTILE) * g4::KTILE;
+    split = cdiv(a.K, kchunk);
+    GemmArgs b = a;
+    float* slab = nullptr;
+    if (a.epi == EPI_F32_ATOMIC) {
+        // split-K partials go to fp32 slabs + one reduce (no float atomics in the GEMM); a single
+        // split accumulates in place
+        if (split > 1) {
+            const size_t need = (size_t)split * a.M * a.N * sizeof(float);
+            slab = a.ws ? (a.ws_bytes >= need ? a.ws : nullptr) : (float*)workspace(need);
+            if (!slab) { set_error("gemm_bf16: split-K workspace of %zu bytes unavailable", need); return; }
+            b.epi = EPI_F32_SLAB;
+            b.C = slab;
+            b.ldc = a.N;
+        } else {
+            b.epi = EPI_F32_ACC;
+        }
+    }
+    GemmParams p = make_params(b, kchunk);
+    p.tiles = tiles;
+    dim3 grid(tiles, split);
+    if (a.a_kcontig && a.b_kcontig) launch_g4<true, true>(b, p, grid, s);
+    else if (a.a_kcontig && !a.b_kcontig) launch_g4<true, false>(b, p, grid, s);
+    else if (!a.a_kcontig && !a.b_kcontig) launch_g4<false, false>(b, p, grid, s);
+    else launch_g4<false, true>(b, p, grid, s);
+    after_launch("gemm_bf16_256x128");
+    if (slab) {
+        slab_reduce_k<<<grid_blocks((long long)a.M * a.N / 4), 256, 0, s>>>(
+            (float*)a.C, a.ldc, slab, a.M, a.N, split);
+        after_launch("gemm_slab_reduce");
+    }
+    // bias gradient of a wgrad (M-contig A = dout^T): column sums of dout over the K rows
+    if (a.dbias && !a.a_kcontig) colsum_bf16(a.dbias, (const bf16_t*)a.A, a.K, a.M, a.lda, s);
+}
+
+static int num_cus() {
+    static int n = -1;
+    if (n < 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        if (n > 1000) n = 1000;  // flags[] capacity
+    }
+    return n;
+}
+size_t gemm_sk_bytes() { return g3::FLAG_BYTES + (size_t)num_cus() * g3::PART_BYTES; }
+
+template <bool AK, bool BKC>
+static void launch_g3(int epi, const GemmParams& p, int P, char* ws, int S, hipStream_t s) {
+    switch (epi) {
+#define VIT_CASE(E) \
+    case E: g3::gemm_kernel<AK, BKC, E><<<P, g3::NT, 0, s>>>(p, ws, S); break;
+        VIT_CASE(EPI_F32_STORE)
+        VIT_CASE(EPI_F32_ACC)
+        VIT_CASE(EPI_BF16_STORE)
+        VIT_CASE(EPI_BF16_GELU)
+        VIT_CASE(EPI_F32_RESID)
+        VIT_CASE(EPI_BF16_DGELU)
+#undef VIT_CASE
+        default: set_error("gemm_bf16: unsupported epilogue %d", epi); return;
+    }
+}
+
+// stream-K persistent launch (g3) when the launch has at least one tile per CU; false = not taken
+static bool gemm_bf16_g3(const GemmArgs& a, hipStream_t s) {
+    const int P = num_cus();
+    const long long tiles = (long long)cdiv(a.M, g3::BM) * cdiv(a.N, g3::BN);
+    const int S = a.K / g3::BK;
+    if (a.epi == EPI_F32_ATOMIC || a.epi == EPI_F32_SLAB) return false;
+    if (tiles < P || a.K % g3::BK || S < 2 || tiles * S >= (1LL << 31)) return false;
+    char* ws = a.sk_ws ? a.sk_ws : (char*)sk_workspace(gemm_sk_bytes());
+    if (!ws) return true;  // error already set
+    GemmParams p = make_params(a, a.K);
+    p.tiles = (int)tiles;
+    if (a.a_kcontig && a.b_kcontig) launch_g3<true, true>(a.epi, p, P, ws, S, s);
+    else if (a.a_kcontig && !a.b_kcontig) launch_g3<true, false>(a.epi, p, P, ws, S, s);
+    else if (!a.a_kcontig && !a.b_kcontig) launch_g3<false, false>(a.epi, p, P, ws, S, s);
+    else launch_g3<false, true>(a.epi, p, P, ws, S, s);
+    after_launch("gemm_bf16_streamk");
+    return true;
 }
 
 void gemm_bf16(const GemmArgs& a, hipStream_t s) {
@@ -749,7 +1409,13 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s) {
                   a.M, a.N, a.K, a.lda, a.ldb);
         return;
     }
-    const bool big = a.K % g2::KTILE == 0 && a.M >= 256 && a.N >= 256 && gemm_variant() == 2 &&
+    if (gemm_variant() == 3 && a.M >= 256 && a.N >= 256 && gemm_bf16_g3(a, s)) return;
+    if (gemm_variant() == 4 && a.K % g4::KTILE == 0 && a.M >= 256 && a.N >= 128 &&
+        (a.epi != EPI_F32_ATOMIC || a.N % 4 == 0)) {
+        gemm_bf16_g4(a, s);
+        return;
+    }
+    const bool big = a.K % g2::KTILE == 0 && a.M >= 256 && a.N >= 256 && gemm_variant() != 1 &&
                      !getenv("VIT_G2_KK_ONLY");
     if (big) {
         const int tiles = cdiv(a.M, g2::BM) * cdiv(a.N, g2::BN);
@@ -770,6 +1436,7 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s) {
             }
         }
         GemmParams p = make_params(b, kchunk);
+        p.tiles = tiles;
         dim3 grid(tiles, split);
         if (a.a_kcontig && a.b_kcontig) launch_g2<true, true>(b, p, grid, s);
         else if (a.a_kcontig && !a.b_kcontig) launch_g2<true, false>(b, p, grid, s);

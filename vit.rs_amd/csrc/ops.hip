@@ -693,6 +693,23 @@ void gemm_bf16_ex(void* C, long long ldc, const uint16_t* A, long long lda, int 
     a.M = M; a.N = N; a.K = K; a.epi = epi; a.splitk = splitk;
     gemm_bf16(a, stream());
 }
+void gemm_bf16_fused(void* C, void* C2, long long ldc, const void* aux, long long ldaux,
+                     const uint16_t* A, long long lda, int a_kcontig, const uint16_t* B,
+                     long long ldb, int b_kcontig, const float* bias, float* colsum_out, int M,
+                     int N, int K, int epi) {
+    VIT_REQUIRE(epi == EPI_BF16_GELU || epi == EPI_F32_RESID || epi == EPI_BF16_DGELU ||
+                    epi == EPI_F32_STORE || epi == EPI_BF16_STORE,
+                "gemm_bf16_fused: epi %d", epi);
+    GemmArgs a;
+    a.A = A; a.lda = lda; a.a_kcontig = a_kcontig != 0;
+    a.B = B; a.ldb = ldb; a.b_kcontig = b_kcontig != 0;
+    a.C = C; a.C2 = C2; a.ldc = ldc; a.aux = aux; a.ldaux = ldaux; a.bias = bias;
+    a.colsum_out = colsum_out;
+    a.M = M; a.N = N; a.K = K; a.epi = epi;
+    gemm_bf16(a, stream());
+}
+void gemm_bf16_set_variant(int variant) { gemm_set_variant(variant); }
+void gemm_bf16_set_debug(int flags) { gemm_set_debug(flags); }
 void convert_f32_to_bf16(uint16_t* out, const float* inp, long long n) {
     convert_f2bf(out, inp, n, stream());
 }
