@@ -1,0 +1,49 @@
+"""Microbenchmark of the fused bf16 attention kernels at ViT-B/16 B=256 (HIP events).
+    python tools/bench_attn.py [--iters 10] [--batch 256]"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from vitpkg import vit  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--T", type=int, default=197)
+    ap.add_argument("--NH", type=int, default=12)
+    args = ap.parse_args()
+    L = vit.lib()
+    assert L.vit_init(0) == 0
+    B, T, NH = args.batch, args.T, args.NH
+    C = 64 * NH
+    rng = np.random.default_rng(0)
+    qkv = vit.DeviceArray.from_numpy(vit.bf16_bits(rng.normal(size=B * T * 3 * C).astype(np.float32)), np.uint16)
+    dout = vit.DeviceArray.from_numpy(vit.bf16_bits(rng.normal(size=B * T * C).astype(np.float32)), np.uint16)
+    out = vit.DeviceArray.zeros(B * T * C, np.uint16)
+    lse = vit.DeviceArray.zeros(B * NH * T, np.float32)
+    dqkv = vit.DeviceArray.zeros(B * T * 3 * C, np.uint16)
+    e0, e1 = L.vit_event_create(), L.vit_event_create()
+    fl_f = 4.0 * B * T * T * C
+    for name, fn, fl in (
+            ("fwd", lambda: L.attention_forward_fused_bf16(out.ptr, lse.ptr, qkv.ptr, B, T, C, NH), fl_f),
+            ("bwd", lambda: L.attention_backward_fused_bf16(dqkv.ptr, dout.ptr, qkv.ptr, out.ptr, lse.ptr, B, T, C, NH), 2 * fl_f)):
+        for _ in range(2):
+            fn()
+        L.vit_sync()
+        vit.check(name)
+        L.vit_event_record(e0)
+        for _ in range(args.iters):
+            fn()
+        L.vit_event_record(e1)
+        ms = L.vit_event_elapsed_ms(e0, e1) / args.iters
+        vit.check(name)
+        print(f"attention {name}: {ms * 1e3:8.1f} us  {fl / ms / 1e9:7.1f} TFLOP/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,6 +1,6 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 120 python -u tools/loss_traj.py 0.5 > gpurun_out/traj.log 2>&1 &&
-VIT_LIB=$PWD/tools/_old/libvit_hip.so timeout -k 10 120 python -u tools/loss_traj.py 0.5 >> gpurun_out/traj.log 2>&1 &&
-timeout -k 10 120 python -u tools/loss_traj.py 0.2 >> gpurun_out/traj.log 2>&1
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_model.py -x -q --timeout 120 --timeout-method thread -k "attention or bf16_trainer or reduces" > gpurun_out/t2.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof5 -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof5.log 2>&1

@@ -221,18 +221,36 @@ __device__ __forceinline__ bf16x8_t pack_acc(f32x4_t a, f32x4_t b) {
     r[4] = (__bf16)b[0]; r[5] = (__bf16)b[1]; r[6] = (__bf16)b[2]; r[7] = (__bf16)b[3];
     return r;
 }
+// v_exp_f32 (2^x, ~1 ulp; results below 2^-126 flush to 0, irrelevant for probabilities that
+// are rounded to bf16); exp2f adds a denormal range-reduction sequence around it
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 __device__ __forceinline__ f32x4_t mfma(bf16x8_t a, bf16x8_t b, f32x4_t c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
-__device__ __forceinline__ void load_rows(bf16_t* img, int stride, const bf16_t* src, long long ld,
-                                          int T, int Tp) {
-    // rows of 64 bf16 = 8 x 16 B; rows >= T zero-filled
-    for (int idx = threadIdx.x; idx < Tp * 8; idx += blockDim.x) {
-        const int t = idx >> 3, c = idx & 7;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (t < T) v = *reinterpret_cast<const uint4*>(src + (long long)t * ld + c * 8);
-        *reinterpret_cast<uint4*>(img + t * stride + c * 8) = v;
-    }
+// rows of 64 bf16 (8 x 16 B each, rows >= T zero-filled) of NOP operands into their LDS images.
+// Every global load of the thread is issued before its first LDS store, so the whole staging is
+// one memory round trip (a load -> store loop serialised one round trip per 16-B chunk row).
+template <int TP, int NTHR, int NOP>
+__device__ __forceinline__ void load_images(bf16_t* const (&img)[NOP], const int (&stride)[NOP],
+                                            const bf16_t* const (&src)[NOP],
+                                            const long long (&ld)[NOP], int T) {
+    constexpr int PER = (TP * 8 + NTHR - 1) / NTHR;
+    uint4 v[NOP][PER];
+#pragma unroll
+    for (int o = 0; o < NOP; o++)
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            const int idx = j * NTHR + (int)threadIdx.x, t = idx >> 3, c = idx & 7;
+            v[o][j] = make_uint4(0, 0, 0, 0);
+            if (idx < TP * 8 && t < T) v[o][j] = *reinterpret_cast<const uint4*>(src[o] + (long long)t * ld[o] + c * 8);
+        }
+#pragma unroll
+    for (int o = 0; o < NOP; o++)
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            const int idx = j * NTHR + (int)threadIdx.x, t = idx >> 3, c = idx & 7;
+            if (idx < TP * 8) *reinterpret_cast<uint4*>(img[o] + t * stride[o] + c * 8) = v[o][j];
+        }
 }
 __device__ __forceinline__ void store4(bf16_t* dst, f32x4_t v, float mul) {
     *reinterpret_cast<uint2*>(dst) =
@@ -244,21 +262,17 @@ __global__ __launch_bounds__(256) void attn_fwd_fused_k(bf16_t* __restrict__ out
                                                         float* __restrict__ lse,
                                                         const bf16_t* __restrict__ qkv, int T,
                                                         int C, int NH) {
-    __shared__ __attribute__((aligned(16))) bf16_t Ks[TMAX * SK];
-    __shared__ __attribute__((aligned(16))) bf16_t Vs[TMAX * SV];
     constexpr int TP = NKT * 16;
+    __shared__ __attribute__((aligned(16))) bf16_t Ks[TP * SK];
+    __shared__ __attribute__((aligned(16))) bf16_t Vs[TP * SV];
     const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
     const long long C3 = 3LL * C;
     const bf16_t* base = qkv + (long long)b * T * C3 + h * HS;
-    load_rows(Ks, SK, base + C, C3, T, TP);
-    load_rows(Vs, SV, base + 2 * C, C3, T, TP);
-    __syncthreads();
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, g = lane >> 4;
-    const float c = LOG2E / sqrtf((float)HS);
-    const int nqt = (T + 15) / 16;
-    for (int qt = w; qt < nqt; qt += 4) {
+    // Q fragments of a 16-query tile straight from HBM (rows >= T -> 0); the next tile's are
+    // requested while the current one computes, the first ones before the K/V staging
+    auto load_q = [&](int qt, bf16x8_t (&qf)[2]) {
         const int q = qt * 16 + i;
-        bf16x8_t qf[2];
 #pragma unroll
         for (int s = 0; s < 2; s++) {
             bf16x4_t lo = {}, hi = {};
@@ -269,6 +283,23 @@ __global__ __launch_bounds__(256) void attn_fwd_fused_k(bf16_t* __restrict__ out
             }
             qf[s] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
         }
+    };
+    const int nqt = (T + 15) / 16;
+    bf16x8_t qn[2];
+    load_q(w, qn);
+    {
+        bf16_t* const img[2] = {Ks, Vs};
+        const int st[2] = {SK, SV};
+        const bf16_t* const src[2] = {base + C, base + 2 * C};
+        const long long ld[2] = {C3, C3};
+        load_images<TP, 256, 2>(img, st, src, ld, T);
+    }
+    __syncthreads();
+    const float c = LOG2E / sqrtf((float)HS);
+    for (int qt = w; qt < nqt; qt += 4) {
+        const int q = qt * 16 + i;
+        const bf16x8_t qf[2] = {qn[0], qn[1]};
+        if (qt + 4 < nqt) load_q(qt + 4, qn);
         f32x4_t sacc[NKT];
 #pragma unroll
         for (int kt = 0; kt < NKT; kt++) {
@@ -295,7 +326,7 @@ __global__ __launch_bounds__(256) void attn_fwd_fused_k(bf16_t* __restrict__ out
         for (int kt = 0; kt < NKT; kt++)
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                const float p = exp2f(sacc[kt][r] - mx);
+                const float p = fexp2(sacc[kt][r] - mx);
                 sacc[kt][r] = p;
                 l += p;
             }
@@ -341,10 +372,13 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_k(bf16_t* __restrict__ dqk
     const bf16_t* dbase = dout + (long long)b * T * C + h * HS;
     for (int t = threadIdx.x; t < NWB * 3 * HS; t += blockDim.x) csum_s[t] = 0.f;
     const bf16_t* obase = out + (long long)b * T * C + h * HS;
-    load_rows(Qs, SK, base, C3, T, TP);
-    load_rows(Ks, SK, base + C, C3, T, TP);
-    load_rows(Vs, SK, base + 2 * C, C3, T, TP);
-    load_rows(Ds, SK, dbase, C, T, TP);
+    {
+        bf16_t* const img[4] = {Qs, Ks, Vs, Ds};
+        const int st[4] = {SK, SK, SK, SK};
+        const bf16_t* const src[4] = {base, base + C, base + 2 * C, dbase};
+        const long long ld[4] = {C3, C3, C3, C};
+        load_images<TP, 512, 4>(img, st, src, ld, T);
+    }
     for (int t = threadIdx.x; t < TP; t += blockDim.x) {
         float dl = 0.f, ls = INFINITY;
         if (t < T) {
@@ -510,6 +544,371 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_k(bf16_t* __restrict__ dqk
     }
 }
 
+// ----------------------------------------------------------------------------------------------
+// Backward as two roles of one launch with 32-row register tiles (attn_bwd_pair_k: bwd_kv_body
+// and bwd_q_body), a 256-thread workgroup per (b,h) and role, two workgroups per CU (LDS ~66 KB).  The single-kernel
+// form above holds Q, K, V and dO in 147 KB of LDS (one workgroup per CU) and reads four LDS
+// fragments per two MFMAs; here each fragment read from LDS feeds two 16-row MFMA tiles:
+//   kv: wave owns 32 keys (K, V fragments in registers, dK^T / dV^T accumulators); per 32-query
+//       chunk: S, dP (8 + 8 MFMA, Q / dO rows from LDS), P = exp2(S c - lse), dS = P (dP - delta),
+//       dV^T += dO^T P, dK^T += Q^T dS (8 + 8 MFMA, transposed reads).  delta = rowsum(dO * O)
+//       (the O(T^2) form of train_vit.rs:583-589) is computed by each role for the rows it needs.
+//   q:  wave owns 32 queries (Q, dO fragments in registers, dQ^T accumulators); per 32-key chunk:
+//       S^T, dP^T (8 + 8, K / V rows from LDS), dQ^T += K^T dS^T (8).
+// Rows >= T are zero-filled, so padded keys contribute nothing to dQ; padded queries have
+// lse = +inf (P = 0).  P of padded keys is zeroed for the fused bias column sums.
+template <int NKT>
+constexpr int bwd_lds_bytes() { return 2 * NKT * 16 * SK * 2 + 2 * NKT * 16 * 4 + 4 * 2 * HS * 4; }
+
+template <int NKT>
+__device__ __forceinline__ void bwd_kv_body(char* lds, int bh, bf16_t* __restrict__ dqkv,
+                                            const bf16_t* __restrict__ dout,
+                                            const bf16_t* __restrict__ qkv,
+                                            const bf16_t* __restrict__ out,
+                                            const float* __restrict__ lse, int T, int C, int NH,
+                                            float* __restrict__ dsum) {
+    constexpr int TP = NKT * 16;  // padded length, multiple of 32
+    bf16_t* Qs = reinterpret_cast<bf16_t*>(lds);
+    bf16_t* Ds = Qs + TP * SK;
+    float* lse_s = reinterpret_cast<float*>(Ds + TP * SK);
+    float* del_s = lse_s + TP;
+    float (*csum_s)[2 * HS] = reinterpret_cast<float (*)[2 * HS]>(del_s + TP);
+    const int b = bh / NH, h = bh % NH;
+    const long long C3 = 3LL * C;
+    const bf16_t* base = qkv + (long long)b * T * C3 + h * HS;
+    const bf16_t* dbase = dout + (long long)b * T * C + h * HS;
+    const bf16_t* obase = out + (long long)b * T * C + h * HS;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, i = lane & 15, g = lane >> 4;
+    // K, V fragments of a 2 x 16-key tile straight from HBM (rows >= T -> 0); the wave's first
+    // tile is requested before the Q/dO staging so its latency hides behind it
+    auto load_kv = [&](int kt, bf16x8_t (&kf)[2][2], bf16x8_t (&vf)[2][2]) {
+#pragma unroll
+        for (int kk = 0; kk < 2; kk++) {
+            const int key = kt * 32 + kk * 16 + i;
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                bf16x4_t klo = {}, khi = {}, vlo = {}, vhi = {};
+                if (key < T) {
+                    const bf16_t* pk = base + (long long)key * C3 + C + 32 * s + 4 * g;
+                    klo = *reinterpret_cast<const bf16x4_t*>(pk);
+                    khi = *reinterpret_cast<const bf16x4_t*>(pk + 16);
+                    vlo = *reinterpret_cast<const bf16x4_t*>(pk + C);
+                    vhi = *reinterpret_cast<const bf16x4_t*>(pk + C + 16);
+                }
+                kf[kk][s] = __builtin_shufflevector(klo, khi, 0, 1, 2, 3, 4, 5, 6, 7);
+                vf[kk][s] = __builtin_shufflevector(vlo, vhi, 0, 1, 2, 3, 4, 5, 6, 7);
+            }
+        }
+    };
+    bf16x8_t kf[2][2], vf[2][2];
+    if (w < TP / 32) load_kv(w, kf, vf);
+    {
+        bf16_t* const img[2] = {Qs, Ds};
+        const int st[2] = {SK, SK};
+        const bf16_t* const src[2] = {base, dbase};
+        const long long ld[2] = {C3, C};
+        load_images<TP, 256, 2>(img, st, src, ld, T);
+    }
+    __syncthreads();
+    // delta = rowsum(dO * O) per query (O from HBM, dO from the image), lse staged
+    for (int t = tid; t < TP; t += 256) {
+        float dl = 0.f, ls = INFINITY;
+        if (t < T) {
+            ls = lse[(long long)bh * T + t];
+            uint4 ov[8];
+#pragma unroll
+            for (int c = 0; c < 8; c++) ov[c] = *reinterpret_cast<const uint4*>(obase + (long long)t * C + c * 8);
+#pragma unroll
+            for (int c = 0; c < 8; c++) {
+                const uint4 dv = *reinterpret_cast<const uint4*>(Ds + t * SK + c * 8);
+                const uint32_t* o32 = reinterpret_cast<const uint32_t*>(&ov[c]);
+                const uint32_t* d32 = reinterpret_cast<const uint32_t*>(&dv);
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    dl += __uint_as_float(o32[e] << 16) * __uint_as_float(d32[e] << 16);
+                    dl += __uint_as_float(o32[e] & 0xffff0000u) * __uint_as_float(d32[e] & 0xffff0000u);
+                }
+            }
+        }
+        lse_s[t] = ls;
+        del_s[t] = dl;
+    }
+    __syncthreads();
+    const float scale = 1.0f / sqrtf((float)HS);
+    const float c = LOG2E * scale;
+    f32x4_t ck[4] = {}, cv[4] = {};  // this lane's share of the dK / dV column sums
+    for (int kt = w; kt < TP / 32; kt += 4) {
+        const int key0 = kt * 32;
+        if (kt != w) load_kv(kt, kf, vf);
+        const bool kok[2] = {key0 + i < T, key0 + 16 + i < T};
+        f32x4_t dv[2][4], dk[2][4];
+#pragma unroll
+        for (int kk = 0; kk < 2; kk++)
+#pragma unroll
+            for (int dt = 0; dt < 4; dt++) dv[kk][dt] = dk[kk][dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+        for (int qs = 0; qs < TP / 32; qs++) {
+            f32x4_t P[2][2], dS[2][2];  // [kk][u]: lane (i,g) -> [q = 32qs+16u+4g+r][key = 16kk+i]
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const int qt0 = qs * 32 + u * 16;
+                const bf16x8_t q0 = frag_row(Qs, SK, qt0, 0, lane), q1 = frag_row(Qs, SK, qt0, 1, lane);
+                const bf16x8_t d0 = frag_row(Ds, SK, qt0, 0, lane), d1 = frag_row(Ds, SK, qt0, 1, lane);
+                float lq[4], dq[4];
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    lq[r] = lse_s[qt0 + 4 * g + r];
+                    dq[r] = del_s[qt0 + 4 * g + r];
+                }
+#pragma unroll
+                for (int kk = 0; kk < 2; kk++) {
+                    f32x4_t s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+                    s = mfma(q0, kf[kk][0], s);
+                    s = mfma(q1, kf[kk][1], s);
+                    dp = mfma(d0, vf[kk][0], dp);
+                    dp = mfma(d1, vf[kk][1], dp);
+                    // padded keys (K, V rows zero) get P != 0 here; they only reach dK / dV rows
+                    // that are neither stored nor summed
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const float pv = fexp2(s[r] * c - lq[r]);
+                        P[kk][u][r] = pv;
+                        dS[kk][u][r] = pv * (dp[r] - dq[r]);
+                    }
+                }
+            }
+            bf16x8_t pb[2], db[2];
+#pragma unroll
+            for (int kk = 0; kk < 2; kk++) {
+                pb[kk] = pack_acc(P[kk][0], P[kk][1]);
+                db[kk] = pack_acc(dS[kk][0], dS[kk][1]);
+            }
+#pragma unroll
+            for (int dt = 0; dt < 4; dt++) {
+                const bf16x8_t td = frag_tr(Ds, SK, 32 * qs, 16 * dt, lane);
+                const bf16x8_t tq = frag_tr(Qs, SK, 32 * qs, 16 * dt, lane);
+#pragma unroll
+                for (int kk = 0; kk < 2; kk++) {
+                    dv[kk][dt] = mfma(td, pb[kk], dv[kk][dt]);
+                    dk[kk][dt] = mfma(tq, db[kk], dk[kk][dt]);
+                }
+            }
+        }
+        // lane (i,g) of tile (kk,dt): key = key0 + 16kk + i, d = 16dt + 4g + r
+#pragma unroll
+        for (int kk = 0; kk < 2; kk++) {
+            if (!kok[kk]) continue;
+            bf16_t* dst = dqkv + ((long long)b * T + key0 + kk * 16 + i) * C3 + h * HS + 4 * g;
+#pragma unroll
+            for (int dt = 0; dt < 4; dt++) {
+                store4(dst + C + 16 * dt, dk[kk][dt], scale);
+                store4(dst + 2 * C + 16 * dt, dv[kk][dt], 1.0f);
+            }
+        }
+        if (dsum) {
+#pragma unroll
+            for (int kk = 0; kk < 2; kk++) {
+                if (!kok[kk]) continue;
+#pragma unroll
+                for (int dt = 0; dt < 4; dt++) {
+                    ck[dt] += dk[kk][dt] * scale;
+                    cv[dt] += dv[kk][dt];
+                }
+            }
+        }
+    }
+    if (dsum) {  // per-(b,h) column sums of dK, dV -> dsum[bh][64..191]
+#pragma unroll
+        for (int dt = 0; dt < 4; dt++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                float tk = ck[dt][r], tv = cv[dt][r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    tk += __shfl_xor(tk, o, 64);
+                    tv += __shfl_xor(tv, o, 64);
+                }
+                if (i == 0) {
+                    csum_s[w][16 * dt + 4 * g + r] = tk;
+                    csum_s[w][HS + 16 * dt + 4 * g + r] = tv;
+                }
+            }
+        __syncthreads();
+        if (tid < 2 * HS)
+            dsum[(long long)bh * 3 * HS + HS + tid] = csum_s[0][tid] + csum_s[1][tid] + csum_s[2][tid] + csum_s[3][tid];
+    }
+}
+
+template <int NKT>
+__device__ __forceinline__ void bwd_q_body(char* lds, int bh, bf16_t* __restrict__ dqkv,
+                                           const bf16_t* __restrict__ dout,
+                                           const bf16_t* __restrict__ qkv,
+                                           const bf16_t* __restrict__ out,
+                                           const float* __restrict__ lse, int T, int C, int NH,
+                                           float* __restrict__ dsum) {
+    constexpr int TP = NKT * 16;
+    bf16_t* Ks = reinterpret_cast<bf16_t*>(lds);
+    bf16_t* Vs = Ks + TP * SK;
+    float (*csum_s)[HS] = reinterpret_cast<float (*)[HS]>(Vs + TP * SK);
+    const int b = bh / NH, h = bh % NH;
+    const bf16_t* obase = out + (long long)b * T * C + h * HS;
+    const long long C3 = 3LL * C;
+    const bf16_t* base = qkv + (long long)b * T * C3 + h * HS;
+    const bf16_t* dbase = dout + (long long)b * T * C + h * HS;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, i = lane & 15, g = lane >> 4;
+    // own 32-query tile: Q / dO fragments, lse, delta straight from HBM; the next tile's are
+    // requested while the current one computes, the first ones before the K/V staging
+    auto load_tile = [&](int qt, bf16x8_t (&qf)[2][2], bf16x8_t (&df)[2][2], float (&lq)[2], float (&dl)[2]) {
+        const int q0 = qt * 32;
+        float part[2] = {0.f, 0.f};
+#pragma unroll
+        for (int qq = 0; qq < 2; qq++) {
+            const int q = q0 + qq * 16 + i;
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                bf16x4_t a0 = {}, a1 = {}, b0 = {}, b1 = {}, o0 = {}, o1 = {};
+                if (q < T) {
+                    const bf16_t* pq = base + (long long)q * C3 + 32 * s + 4 * g;
+                    const bf16_t* pd = dbase + (long long)q * C + 32 * s + 4 * g;
+                    const bf16_t* po = obase + (long long)q * C + 32 * s + 4 * g;
+                    a0 = *reinterpret_cast<const bf16x4_t*>(pq);
+                    a1 = *reinterpret_cast<const bf16x4_t*>(pq + 16);
+                    b0 = *reinterpret_cast<const bf16x4_t*>(pd);
+                    b1 = *reinterpret_cast<const bf16x4_t*>(pd + 16);
+                    o0 = *reinterpret_cast<const bf16x4_t*>(po);
+                    o1 = *reinterpret_cast<const bf16x4_t*>(po + 16);
+                }
+                qf[qq][s] = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+                df[qq][s] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+                // delta = rowsum(dO * O): this lane's 16 of the query's 64 columns
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    part[qq] += (float)b0[e] * (float)o0[e];
+                    part[qq] += (float)b1[e] * (float)o1[e];
+                }
+            }
+            lq[qq] = q < T ? lse[(long long)bh * T + q] : INFINITY;
+        }
+#pragma unroll
+        for (int qq = 0; qq < 2; qq++) {  // the 4 lanes of a query are lane, lane ^ 16, ^ 32
+            float t = part[qq];
+            t += __shfl_xor(t, 16, 64);
+            t += __shfl_xor(t, 32, 64);
+            dl[qq] = t;
+        }
+    };
+    bf16x8_t qn[2][2], dn[2][2];
+    float lqn[2], dln[2];
+    if (w < TP / 32) load_tile(w, qn, dn, lqn, dln);
+    {
+        bf16_t* const img[2] = {Ks, Vs};
+        const int st[2] = {SK, SK};
+        const bf16_t* const src[2] = {base + C, base + 2 * C};
+        const long long ld[2] = {C3, C3};
+        load_images<TP, 256, 2>(img, st, src, ld, T);
+    }
+    __syncthreads();
+    const float scale = 1.0f / sqrtf((float)HS);
+    const float c = LOG2E * scale;
+    f32x4_t cq[4] = {};
+    for (int qt = w; qt < TP / 32; qt += 4) {
+        const int q0 = qt * 32;
+        bf16x8_t qf[2][2], df[2][2];
+        float lq[2], dl[2];
+#pragma unroll
+        for (int qq = 0; qq < 2; qq++) {
+            lq[qq] = lqn[qq];
+            dl[qq] = dln[qq];
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                qf[qq][s] = qn[qq][s];
+                df[qq][s] = dn[qq][s];
+            }
+        }
+        if (qt + 4 < TP / 32) load_tile(qt + 4, qn, dn, lqn, dln);
+        f32x4_t dq[2][4];
+#pragma unroll
+        for (int qq = 0; qq < 2; qq++)
+#pragma unroll
+            for (int dt = 0; dt < 4; dt++) dq[qq][dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+        for (int ks = 0; ks < TP / 32; ks++) {
+            f32x4_t dS[2][2];  // [qq][u]: lane (i,g) -> [key = 32ks+16u+4g+r][q = 16qq+i]
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const int kt0 = ks * 32 + u * 16;
+                const bf16x8_t k0 = frag_row(Ks, SK, kt0, 0, lane), k1 = frag_row(Ks, SK, kt0, 1, lane);
+                const bf16x8_t v0 = frag_row(Vs, SK, kt0, 0, lane), v1 = frag_row(Vs, SK, kt0, 1, lane);
+#pragma unroll
+                for (int qq = 0; qq < 2; qq++) {
+                    f32x4_t s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+                    s = mfma(k0, qf[qq][0], s);
+                    s = mfma(k1, qf[qq][1], s);
+                    dp = mfma(v0, df[qq][0], dp);
+                    dp = mfma(v1, df[qq][1], dp);
+#pragma unroll
+                    for (int r = 0; r < 4; r++) dS[qq][u][r] = fexp2(s[r] * c - lq[qq]) * (dp[r] - dl[qq]);
+                }
+            }
+            bf16x8_t db[2];
+#pragma unroll
+            for (int qq = 0; qq < 2; qq++) db[qq] = pack_acc(dS[qq][0], dS[qq][1]);
+#pragma unroll
+            for (int dt = 0; dt < 4; dt++) {
+                const bf16x8_t tk = frag_tr(Ks, SK, 32 * ks, 16 * dt, lane);
+#pragma unroll
+                for (int qq = 0; qq < 2; qq++) dq[qq][dt] = mfma(tk, db[qq], dq[qq][dt]);
+            }
+        }
+#pragma unroll
+        for (int qq = 0; qq < 2; qq++) {
+            const int q = q0 + qq * 16 + i;
+            if (q >= T) continue;
+            bf16_t* dst = dqkv + ((long long)b * T + q) * C3 + h * HS + 4 * g;
+#pragma unroll
+            for (int dt = 0; dt < 4; dt++) store4(dst + 16 * dt, dq[qq][dt], scale);
+        }
+        if (dsum) {  // padded queries: dS = exp2(-inf) * ... = 0
+#pragma unroll
+            for (int qq = 0; qq < 2; qq++)
+#pragma unroll
+                for (int dt = 0; dt < 4; dt++) cq[dt] += dq[qq][dt] * scale;
+        }
+    }
+    if (dsum) {
+#pragma unroll
+        for (int dt = 0; dt < 4; dt++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                float tq = cq[dt][r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) tq += __shfl_xor(tq, o, 64);
+                if (i == 0) csum_s[w][16 * dt + 4 * g + r] = tq;
+            }
+        __syncthreads();
+        if (tid < HS) dsum[(long long)bh * 3 * HS + tid] = csum_s[0][tid] + csum_s[1][tid] + csum_s[2][tid] + csum_s[3][tid];
+    }
+}
+
+// kv and q roles of one (b,h) in ONE launch: the two workgroups of a pair are dealt to the same
+// XCD back to back (block ids 16k + x and 16k + 8 + x), so the second reads of Q, K, V, dO, O
+// are served from that XCD's L2 instead of HBM.  Both roles compute delta themselves.
+template <int NKT>
+__global__ __launch_bounds__(256, 2) void attn_bwd_pair_k(bf16_t* __restrict__ dqkv,
+                                                          const bf16_t* __restrict__ dout,
+                                                          const bf16_t* __restrict__ qkv,
+                                                          const bf16_t* __restrict__ out,
+                                                          const float* __restrict__ lse, int T,
+                                                          int C, int NH, int BH,
+                                                          float* __restrict__ dsum) {
+    __shared__ __attribute__((aligned(16))) char lds[bwd_lds_bytes<NKT>()];
+    const int x = blockIdx.x & 7, grp = blockIdx.x >> 3;
+    const int role = grp & 1, bh = (grp >> 1) * 8 + x;
+    if (bh >= BH) return;
+    if (role == 0) bwd_kv_body<NKT>(lds, bh, dqkv, dout, qkv, out, lse, T, C, NH, dsum);
+    else bwd_q_body<NKT>(lds, bh, dqkv, dout, qkv, out, lse, T, C, NH, dsum);
+}
+
 // out[s*C + h*64 + d] += sum_b part[(b*NH + h)][s*64 + d]; one 1024-thread block per (s, h):
 // 16 batch lanes x 64 columns, fixed-order tree over the lanes (deterministic).
 __global__ __launch_bounds__(1024) void attn_colsum_reduce_k(float* __restrict__ out,
@@ -577,23 +976,28 @@ void attn_forward_fused(bf16_t* out, float* lse, const bf16_t* qkv, int B, int T
 
 void attn_backward_fused(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t* out,
                          const float* lse, int B, int T, int C, int NH, hipStream_t s,
-                         float* dqkv_colsum, float* part_ws) {
+                         float* dqkv_colsum, float* ws) {
     if (!attn_fused_supported(T, C, NH)) {
         set_error("attention_backward_fused: needs head size 64 and T<=256 (T=%d C=%d NH=%d)", T, C, NH);
         return;
     }
     const int nkt = cdiv(T, 32) * 2;
     dim3 grid(B * NH);
-#define VIT_BWD_THREADS 512
-    if (dqkv_colsum && !part_ws) {
-        set_error("attention_backward_fused: column sums need a [B*NH*192] workspace");
-        return;
+    static const int one_kernel = getenv("VIT_ATTN_BWD") ? atoi(getenv("VIT_ATTN_BWD")) : 0;
+    // ws: [B*NH*192] per-(b,h) bias partial sums
+    const size_t need = (size_t)B * NH * 3 * fa::HS * sizeof(float);
+    if (!ws) ws = (float*)workspace(need);
+    if (!ws) return;
+    float* part = dqkv_colsum ? ws : nullptr;
+    if (one_kernel == 1) {
+        VIT_NKT_DISPATCH_T(fa::attn_bwd_fused_k, 512, dqkv, dout, qkv, out, lse, T, C, NH, part)
+    } else {
+        grid = dim3(2 * cdiv(B * NH, 8) * 8);
+        VIT_NKT_DISPATCH_T(fa::attn_bwd_pair_k, 256, dqkv, dout, qkv, out, lse, T, C, NH, B * NH, part)
     }
-    VIT_NKT_DISPATCH_T(fa::attn_bwd_fused_k, VIT_BWD_THREADS, dqkv, dout, qkv, out, lse, T, C, NH,
-                       dqkv_colsum ? part_ws : nullptr)
     after_launch("attention_backward_fused");
     if (dqkv_colsum) {
-        fa::attn_colsum_reduce_k<<<3 * NH, 1024, 0, s>>>(dqkv_colsum, part_ws, B, NH, C);
+        fa::attn_colsum_reduce_k<<<3 * NH, 1024, 0, s>>>(dqkv_colsum, part, B, NH, C);
         after_launch("attention_colsum_reduce");
     }
 }

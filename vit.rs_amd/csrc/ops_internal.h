@@ -46,5 +46,6 @@ void attn_forward_fused(bf16_t* out, float* lse, const bf16_t* qkv, int B, int T
 // dqkv_colsum (nullable, [3C]) += column sums of dqkv (the qkv bias gradient, fused)
 void attn_backward_fused(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t* out,
                          const float* lse, int B, int T, int C, int NH, hipStream_t s,
-                         float* dqkv_colsum = nullptr, float* part_ws = nullptr);
+                         float* dqkv_colsum = nullptr, float* ws = nullptr);
+// ws (nullable = thread workspace): B*NH*192 floats — per-(b,h) bias partial sums
 }  // namespace vit

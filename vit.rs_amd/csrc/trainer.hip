@@ -343,7 +343,7 @@ struct Trainer {
             // slabs: <= 32 splits of the largest weight gradient (4C x C)
             gemm_ws_bytes = (size_t)32 * 4 * C * (size_t)std::max(C, KP) * sizeof(float);
             gemm_ws = alloc<float>((long long)(gemm_ws_bytes / sizeof(float)));
-            attn_part = alloc<float>((long long)B * NH * 3 * 64);
+            attn_part = alloc<float>((long long)B * NH * (3 * 64 + T));  // bias partials | delta
         } else {
             patches_f = alloc<float>((long long)B * NP * KP);
             dpatch_f = alloc<float>((long long)B * NP * C);
