@@ -13,7 +13,8 @@ BEFORE the library so the process has a single HIP runtime.
 
 Prints ONE JSON line (rank 0).  `value` = images/s of the whole job = N*B*K / max-over-ranks
 wall time of the K timed steps.  `roofline` describes the dominant GEMM class, timed with HIP
-events on the trainer's stream over the same timed steps.  `cpu_baseline` = the CPU oracle
+events on the stream each kernel runs on, over a second pass of the same K steps (the events
+are kept out of the timed region of `value`).  `cpu_baseline` = the CPU oracle
 (the reference loops restated in C, single thread) timed on this host on a bounded sample.
 """
 import argparse
@@ -185,26 +186,37 @@ def main():
         m.train_step(args.lr, b_global)
     m.sync()
     loss_w = m.forward() if args.warmup else float("nan")   # sanity: finite loss after warmup
-    m.timing_reset()
-    m.set_timing(not args.no_timing)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    m.sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        m.train_step(args.lr, b_global)
-    m.sync()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    m.set_timing(False)
-    kern = m.timing() if not args.no_timing else {}
+
+    def timed(steps):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        m.sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            m.train_step(args.lr, b_global)
+        m.sync()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([dt], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        return dt
+
+    # the timed region: K plain steps (no per-kernel events: ~70 event pairs per step cost ~3 %)
+    dt = timed(args.steps)
+    # then the same K steps again with HIP events around every kernel class on the stream it is
+    # launched on, for the per-kernel breakdown and the roofline of the dominant kernel
+    kern = {}
+    if not args.no_timing:
+        m.timing_reset()
+        m.set_timing(True)
+        timed(args.steps)
+        m.set_timing(False)
+        kern = m.timing()
     ips = world * B * args.steps / dt
     _, gflop_img = cfg.train_gflop_per_image()
 
@@ -238,6 +250,8 @@ def main():
             "train_gflop_per_image": round(gflop_img, 3),
             "loss_after_warmup": round(loss_w, 4),
             "roofline": roof, "kernels": ksum,
+            "kernels_note": "per-kernel ms from HIP events over a second pass of the same steps; "
+                            "wgrad GEMMs run on a second stream beside the main stream",
         }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg)

@@ -1,6 +1,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_model.py -x -q --timeout 120 --timeout-method thread -k "attention or bf16_trainer or reduces" > gpurun_out/t2.log 2>&1 &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof5 -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof5.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_model.py -x -q --timeout 120 --timeout-method thread > gpurun_out/t2.log 2>&1 &&
+timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/bench_2s.log 2>&1 &&
+VIT_BWD_STREAMS=1 timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/bench_1s.log 2>&1 &&
+timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-timing > gpurun_out/bench_2s_nt.log 2>&1

@@ -1,8 +1,5 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-export TMPDIR=/tmp
-timeout -k 10 60 rocprofv3 -L > gpurun_out/counters.txt 2>&1
-timeout -k 10 120 python3 tools/bench_attn.py > gpurun_out/battn.log 2>&1 &&
-timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT --kernel-trace -d gpurun_out/pmc1 -o run -- python3 tools/bench_attn.py --iters 2 > gpurun_out/pmc1.log 2>&1 &&
-timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_MISC --kernel-trace -d gpurun_out/pmc2 -o run -- python3 tools/bench_attn.py --iters 2 > gpurun_out/pmc2.log 2>&1
+timeout -k 10 200 python3 tools/bench_gemm.py --no-epi --variants 2 --rounds 2 > gpurun_out/bg_norm.log 2>&1 &&
+VIT_DEBUG_SAME_TILE=1 timeout -k 10 200 python3 tools/bench_gemm.py --no-epi --variants 2 --rounds 2 > gpurun_out/bg_same.log 2>&1

@@ -89,6 +89,13 @@ struct Trainer {
     int n_chunks = 0;
 
     hipStream_t s = nullptr, s_comm = nullptr;
+    // backward weight-gradient stream: the wgrad GEMMs of a layer run beside the dgrad / LN /
+    // attention kernels of the main stream (they only read activations and write grads)
+    hipStream_t s2 = nullptr;
+    bool two_streams = true;
+    enum BwdEv { EV_RESA, EV_RESB, EV_DFCH, EV_DQKV, EV_W1, EV_W2, EV_W3, EV_W4, EV_JOIN, EV_COUNT };
+    hipEvent_t bev[EV_COUNT]{};
+    std::vector<hipEvent_t> chunk_ev2;
     std::vector<hipEvent_t> chunk_ev;
     hipEvent_t comm_done = nullptr;
 
@@ -121,7 +128,7 @@ struct Trainer {
     // grads scratch
     float *dlosses = nullptr, *dlogits = nullptr, *dlnf = nullptr, *dcls_x = nullptr;
     float *dres_a = nullptr, *dres_b = nullptr, *dln = nullptr;
-    bf16_t *dres_bf = nullptr, *dfch = nullptr, *datty = nullptr, *dqkv = nullptr, *dpatch_bf = nullptr;
+    bf16_t *dres_bf = nullptr, *dres_bf2 = nullptr, *dfch = nullptr, *datty = nullptr, *dqkv = nullptr, *dpatch_bf = nullptr;
     float* dpatch_f = nullptr;
     // fp32-mode per-layer grad scratch (one layer, zeroed per layer)
     float *g_block = nullptr;
@@ -135,7 +142,7 @@ struct Trainer {
 
     // ---- timing
     bool timing = false;
-    struct Rec { int cls; hipEvent_t a, b; };
+    struct Rec { int cls; hipEvent_t a, b; hipStream_t st; };
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
     std::vector<Rec> recs;
@@ -230,8 +237,9 @@ struct Trainer {
     }
 
     // ---- timing helpers
-    void tbeg(int cls, double flops) {
+    void tbeg(int cls, double flops, hipStream_t st = nullptr) {
         if (!timing) return;
+        if (!st) st = s;
         if (ev_used + 2 > ev_pool.size()) {
             for (int k = 0; k < 64; k++) {
                 hipEvent_t e;
@@ -239,19 +247,20 @@ struct Trainer {
                 ev_pool.push_back(e);
             }
         }
-        Rec r{cls, ev_pool[ev_used], ev_pool[ev_used + 1]};
+        Rec r{cls, ev_pool[ev_used], ev_pool[ev_used + 1], st};
         ev_used += 2;
-        VIT_HIP(hipEventRecord(r.a, s));
+        VIT_HIP(hipEventRecord(r.a, st));
         recs.push_back(r);
         t_flops[cls] += flops;
     }
     void tend() {
         if (!timing) return;
-        VIT_HIP(hipEventRecord(recs.back().b, s));
+        VIT_HIP(hipEventRecord(recs.back().b, recs.back().st));
     }
     void collect() {
         if (recs.empty()) return;
         VIT_HIP(hipStreamSynchronize(s));
+        VIT_HIP(hipStreamSynchronize(s2));
         for (auto& r : recs) {
             float ms = 0.f;
             if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
@@ -287,8 +296,16 @@ struct Trainer {
         if (hipSetDevice(dev) != hipSuccess) { set_error("trainer: hipSetDevice(%d)", dev); return false; }
         VIT_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
         VIT_HIP(hipStreamCreateWithFlags(&s_comm, hipStreamNonBlocking));
+        VIT_HIP(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+        {
+            const char* e = getenv("VIT_BWD_STREAMS");
+            two_streams = !(e && atoi(e) == 1);
+        }
+        for (auto& e : bev) VIT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         chunk_ev.resize(L + 2);
         for (auto& e : chunk_ev) VIT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        chunk_ev2.resize(L + 2);
+        for (auto& e : chunk_ev2) VIT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         VIT_HIP(hipEventCreateWithFlags(&comm_done, hipEventDisableTiming));
         build_layout();
         params = alloc<float>(arena_elems);
@@ -336,6 +353,7 @@ struct Trainer {
             }
             dln = alloc<float>(BT * C);
             dres_bf = alloc<bf16_t>(BT * C);
+            dres_bf2 = alloc<bf16_t>(BT * C);
             dfch = alloc<bf16_t>(BT * 4 * C);
             datty = alloc<bf16_t>(BT * C);
             dqkv = alloc<bf16_t>(BT * 3 * C);
@@ -389,13 +407,17 @@ struct Trainer {
     void destroy() {
         if (s) (void)hipStreamSynchronize(s);
         if (s_comm) (void)hipStreamSynchronize(s_comm);
+        if (s2) (void)hipStreamSynchronize(s2);
         if (comm) ncclCommDestroy(comm);
         for (auto& a : allocs) (void)hipFree(a.p);
         for (auto e : chunk_ev) (void)hipEventDestroy(e);
+        for (auto e : chunk_ev2) (void)hipEventDestroy(e);
+        for (auto e : bev) if (e) (void)hipEventDestroy(e);
         for (auto e : ev_pool) (void)hipEventDestroy(e);
         if (comm_done) (void)hipEventDestroy(comm_done);
         if (s) (void)hipStreamDestroy(s);
         if (s_comm) (void)hipStreamDestroy(s_comm);
+        if (s2) (void)hipStreamDestroy(s2);
     }
 
     void refresh_bf16() {
@@ -494,23 +516,39 @@ struct Trainer {
         head_forward();
     }
 
+    // dW[OC,Cin] += dout^T . inp (reduction over B*T rows, split-K slabs) on the weight-gradient
+    // stream once `ready` (recorded on the main stream when dout is final) has passed; `done`
+    // marks the end of its reads of dout / inp
     void wgrad(int cls, const bf16_t* dout, int OC, const bf16_t* inp, int Cin, float* dW,
-               float* db) {
-        GemmArgs w;  // dW[OC,Cin] += dout^T . inp, db += colsum(dout)  (reduction over B*T rows)
-        w.dbias = db;
+               hipEvent_t ready, hipEvent_t done) {
+        GemmArgs w;
         w.A = dout; w.lda = OC; w.a_kcontig = false;
         w.B = inp; w.ldb = Cin; w.b_kcontig = false;
         w.C = dW; w.ldc = Cin; w.M = OC; w.N = Cin; w.K = (int)BT; w.epi = EPI_F32_ATOMIC;
         w.ws = gemm_ws; w.ws_bytes = gemm_ws_bytes;
-        gemm(cls, w, true);
+        hipStream_t st = two_streams ? s2 : s;
+        if (two_streams) {
+            VIT_HIP(hipEventRecord(ready, s));
+            VIT_HIP(hipStreamWaitEvent(s2, ready, 0));
+        }
+        tbeg(cls, 2.0 * w.M * (double)w.N * w.K, st);
+        gemm_bf16(w, st);
+        tend();
+        if (two_streams) VIT_HIP(hipEventRecord(done, s2));
+    }
+    // the main stream may overwrite a buffer once the wgrad that reads it (`done`) has finished
+    void after_wgrad(hipEvent_t done) {
+        if (two_streams) VIT_HIP(hipStreamWaitEvent(s, done, 0));
     }
 
     void backward_bf16() {
         float* dcur = dres_a;
         float* dnxt = dres_b;
+        bf16_t* rbA = dres_bf;   // bf16 copy of dres3 (read by fcproj dgrad / wgrad)
+        bf16_t* rbB = dres_bf2;  // bf16 copy of dres2 (read by attproj dgrad / wgrad)
         head_backward(dcur);
         chunk_done(0);
-        convert_f2bf(dres_bf, dcur, BT * C, s);
+        convert_f2bf(rbA, dcur, BT * C, s);
         // bias gradients are fused into the kernels that produce each gradient tensor:
         //   fcproj_b += colsum(dres3): LN1-backward of layer l+1 (head rows for the last layer)
         //   fc_b     += colsum(dfch):  fcproj dgrad epilogue
@@ -520,51 +558,59 @@ struct Trainer {
         for (int l = L - 1; l >= 0; l--) {
             LayerActs& a = la[l];
             const float* x = l == 0 ? encoded : la[l - 1].res3;
-            // fcproj: dfch = (dres3 . fcprojw) * gelu'(fch)
+            // fcproj: dfch = (dres3 . fcprojw) * gelu'(fch);  fcprojw += dres3^T . fchg
+            wgrad(TC_FCPROJ_WGRAD, rbA, C, a.fchg, 4 * C, G(P_FCPROJW, l), bev[EV_RESA], bev[EV_W1]);
+            after_wgrad(bev[EV_W2]);  // the previous layer's fc wgrad has read dfch
             GemmArgs d1;
-            d1.A = dres_bf; d1.lda = C; d1.B = W(P_FCPROJW, l); d1.ldb = 4 * C; d1.b_kcontig = false;
+            d1.A = rbA; d1.lda = C; d1.B = W(P_FCPROJW, l); d1.ldb = 4 * C; d1.b_kcontig = false;
             d1.C = dfch; d1.ldc = 4 * C; d1.aux = a.fch; d1.ldaux = 4 * C;
             d1.M = (int)BT; d1.N = 4 * C; d1.K = C; d1.epi = EPI_BF16_DGELU;
             d1.colsum_out = G(P_FCB, l);
             gemm(TC_FCPROJ_DGRAD, d1, true);
-            wgrad(TC_FCPROJ_WGRAD, dres_bf, C, a.fchg, 4 * C, G(P_FCPROJW, l), nullptr);
-            // fc: dln2 = dfch . fcw
+            // fc: dln2 = dfch . fcw;  fcw += dfch^T . ln2
+            wgrad(TC_FC_WGRAD, dfch, 4 * C, a.ln2, C, G(P_FCW, l), bev[EV_DFCH], bev[EV_W2]);
             GemmArgs d2;
             d2.A = dfch; d2.lda = 4 * C; d2.B = W(P_FCW, l); d2.ldb = C; d2.b_kcontig = false;
             d2.C = dln; d2.ldc = C; d2.M = (int)BT; d2.N = C; d2.K = 4 * C; d2.epi = EPI_F32_STORE;
             gemm(TC_FC_DGRAD, d2, true);
-            wgrad(TC_FC_WGRAD, dfch, 4 * C, a.ln2, C, G(P_FCW, l), nullptr);
             // ln2 backward + residual: dres2 = dres3 + LN2'(dln2); attproj_b += colsum(dres2)
+            after_wgrad(bev[EV_W3]);  // the previous layer's attproj wgrad has read rbB
             tbeg(TC_LN_BWD, 0);
-            ln_backward_fused(dnxt, dres_bf, dcur, G(P_LN2W, l), G(P_LN2B, l), G(P_ATTPROJB, l), dln,
+            ln_backward_fused(dnxt, rbB, dcur, G(P_LN2W, l), G(P_LN2B, l), G(P_ATTPROJB, l), dln,
                               a.res2, P(P_LN2W, l), a.ln2_mean, a.ln2_rstd, BT, C, s);
             tend();
             std::swap(dcur, dnxt);
             // attproj
+            wgrad(TC_PROJ_WGRAD, rbB, C, a.atty, C, G(P_ATTPROJW, l), bev[EV_RESB], bev[EV_W3]);
             GemmArgs d3;
-            d3.A = dres_bf; d3.lda = C; d3.B = W(P_ATTPROJW, l); d3.ldb = C; d3.b_kcontig = false;
+            d3.A = rbB; d3.lda = C; d3.B = W(P_ATTPROJW, l); d3.ldb = C; d3.b_kcontig = false;
             d3.C = datty; d3.ldc = C; d3.M = (int)BT; d3.N = C; d3.K = C; d3.epi = EPI_BF16_STORE;
             gemm(TC_PROJ_DGRAD, d3, true);
-            wgrad(TC_PROJ_WGRAD, dres_bf, C, a.atty, C, G(P_ATTPROJW, l), nullptr);
             // attention (+ qkv_b)
+            after_wgrad(bev[EV_W4]);  // the previous layer's qkv wgrad has read dqkv
             tbeg(TC_ATTN_BWD, 8.0 * B * (double)T * T * C);
             attn_backward_fused(dqkv, datty, a.qkv, a.atty, a.lse, B, T, C, NH, s, G(P_QKVB, l),
                                 attn_part);
             tend();
             // qkv
+            wgrad(TC_QKV_WGRAD, dqkv, 3 * C, a.ln1, C, G(P_QKVW, l), bev[EV_DQKV], bev[EV_W4]);
             GemmArgs d4;
             d4.A = dqkv; d4.lda = 3 * C; d4.B = W(P_QKVW, l); d4.ldb = C; d4.b_kcontig = false;
             d4.C = dln; d4.ldc = C; d4.M = (int)BT; d4.N = C; d4.K = 3 * C; d4.epi = EPI_F32_STORE;
             gemm(TC_QKV_DGRAD, d4, true);
-            wgrad(TC_QKV_WGRAD, dqkv, 3 * C, a.ln1, C, G(P_QKVW, l), nullptr);
             // ln1 backward: dres = dres2 + LN1'(dln1); fcproj_b of layer l-1 += colsum(dres)
+            after_wgrad(bev[EV_W1]);  // this layer's fcproj wgrad has read rbA
             tbeg(TC_LN_BWD, 0);
-            ln_backward_fused(dnxt, dres_bf, dcur, G(P_LN1W, l), G(P_LN1B, l),
+            ln_backward_fused(dnxt, rbA, dcur, G(P_LN1W, l), G(P_LN1B, l),
                               l > 0 ? G(P_FCPROJB, l - 1) : nullptr, dln, x, P(P_LN1W, l),
                               a.ln1_mean, a.ln1_rstd, BT, C, s);
             tend();
             std::swap(dcur, dnxt);
             chunk_done(L - l);
+        }
+        if (two_streams) {  // every wgrad done before the slab workspace / grads are reused
+            VIT_HIP(hipEventRecord(bev[EV_JOIN], s2));
+            VIT_HIP(hipStreamWaitEvent(s, bev[EV_JOIN], 0));
         }
         // patch embedding backward (encoder_backward, train_vit.rs:371 -> ViT)
         tbeg(TC_PATCH_BWD, 2.0 * B * NP * (double)KP * C);
@@ -672,6 +718,10 @@ struct Trainer {
         if (!comm || !overlap) return;
         VIT_HIP(hipEventRecord(chunk_ev[c], s));
         VIT_HIP(hipStreamWaitEvent(s_comm, chunk_ev[c], 0));
+        if (two_streams && prec == VIT_BF16) {  // the chunk's weight gradients come from s2
+            VIT_HIP(hipEventRecord(chunk_ev2[c], s2));
+            VIT_HIP(hipStreamWaitEvent(s_comm, chunk_ev2[c], 0));
+        }
         const long long o = chunk_off[c], n = chunk_off[c + 1] - chunk_off[c];
         ncclResult_t r = ncclAllReduce(grads + o, grads + o, (size_t)n, ncclFloat32, ncclSum, comm, s_comm);
         if (r != ncclSuccess) set_error("ncclAllReduce(chunk %d): %s", c, ncclGetErrorString(r));
