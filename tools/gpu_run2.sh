@@ -2,6 +2,5 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests/test_gpu_model.py -x -q --timeout 120 --timeout-method thread > gpurun_out/t2.log 2>&1 &&
-timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/bench_2s.log 2>&1 &&
-VIT_BWD_STREAMS=1 timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/bench_1s.log 2>&1 &&
-timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-timing > gpurun_out/bench_2s_nt.log 2>&1
+timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/bench_mb2.log 2>&1 &&
+VIT_MICROBATCH=1 timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/bench_mb1.log 2>&1

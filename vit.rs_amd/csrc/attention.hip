@@ -927,7 +927,7 @@ __global__ __launch_bounds__(1024) void attn_colsum_reduce_k(float* __restrict__
         float a = 0.f;
 #pragma unroll
         for (int i = 0; i < 16; i++) a += red[i][d];
-        out[sct * C + h * HS + d] += a;
+        atomicAdd(out + sct * C + h * HS + d, a);  // micro-batches reduce into one bias concurrently
     }
 }
 }  // namespace fa

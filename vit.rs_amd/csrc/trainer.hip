@@ -95,6 +95,15 @@ struct Trainer {
     bool two_streams = true;
     enum BwdEv { EV_RESA, EV_RESB, EV_DFCH, EV_DQKV, EV_W1, EV_W2, EV_W3, EV_W4, EV_JOIN, EV_COUNT };
     hipEvent_t bev[EV_COUNT]{};
+    // micro-batches: the batch is processed as NMB row ranges on NMB streams (ms[0] = s), so the
+    // kernels of one half (GEMM epilogue bursts, LayerNorm, attention) overlap the other's GEMM
+    // main loops; wgrads (on s2) still reduce over the whole batch
+    static constexpr int MAXMB = 2;
+    int nmb = 1;
+    hipStream_t ms[MAXMB]{};
+    hipEvent_t mev[MAXMB][EV_COUNT]{};
+    hipEvent_t fork_ev = nullptr, join_ev[MAXMB]{};
+    std::vector<hipEvent_t> chunk_evm;
     std::vector<hipEvent_t> chunk_ev2;
     std::vector<hipEvent_t> chunk_ev;
     hipEvent_t comm_done = nullptr;
@@ -261,6 +270,7 @@ struct Trainer {
         if (recs.empty()) return;
         VIT_HIP(hipStreamSynchronize(s));
         VIT_HIP(hipStreamSynchronize(s2));
+        for (int k = 1; k < MAXMB; k++) VIT_HIP(hipStreamSynchronize(ms[k]));
         for (auto& r : recs) {
             float ms = 0.f;
             if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
@@ -272,10 +282,23 @@ struct Trainer {
         ev_used = 0;
     }
 
-    void gemm(int cls, GemmArgs a, bool bf) {
-        tbeg(cls, 2.0 * a.M * (double)a.N * a.K);
-        if (bf) gemm_bf16(a, s); else gemm_f32(a, s);
+    void gemm(int cls, GemmArgs a, bool bf, hipStream_t st = nullptr) {
+        if (!st) st = s;
+        tbeg(cls, 2.0 * a.M * (double)a.N * a.K, st);
+        if (bf) gemm_bf16(a, st); else gemm_f32(a, st);
         tend();
+    }
+    // fork the micro-batch streams off s / join them back into s
+    void mb_fork() {
+        if (nmb < 2) return;
+        VIT_HIP(hipEventRecord(fork_ev, s));
+        for (int k = 1; k < nmb; k++) VIT_HIP(hipStreamWaitEvent(ms[k], fork_ev, 0));
+    }
+    void mb_join() {
+        for (int k = 1; k < nmb; k++) {
+            VIT_HIP(hipEventRecord(join_ev[k], ms[k]));
+            VIT_HIP(hipStreamWaitEvent(s, join_ev[k], 0));
+        }
     }
 
     // ------------------------------------------------------------------------------
@@ -302,6 +325,19 @@ struct Trainer {
             two_streams = !(e && atoi(e) == 1);
         }
         for (auto& e : bev) VIT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        ms[0] = s;
+        for (int k = 1; k < MAXMB; k++) VIT_HIP(hipStreamCreateWithFlags(&ms[k], hipStreamNonBlocking));
+        for (auto& row : mev)
+            for (auto& e : row) VIT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        VIT_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
+        for (auto& e : join_ev) VIT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        {
+            const char* e = getenv("VIT_MICROBATCH");
+            const int want = e ? atoi(e) : 2;
+            nmb = (want >= 2 && B % 2 == 0 && two_streams) ? 2 : 1;
+        }
+        chunk_evm.resize((size_t)(L + 2) * MAXMB);
+        for (auto& e : chunk_evm) VIT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         chunk_ev.resize(L + 2);
         for (auto& e : chunk_ev) VIT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         chunk_ev2.resize(L + 2);
@@ -408,11 +444,18 @@ struct Trainer {
         if (s) (void)hipStreamSynchronize(s);
         if (s_comm) (void)hipStreamSynchronize(s_comm);
         if (s2) (void)hipStreamSynchronize(s2);
+        for (int k = 1; k < MAXMB; k++) if (ms[k]) (void)hipStreamSynchronize(ms[k]);
         if (comm) ncclCommDestroy(comm);
         for (auto& a : allocs) (void)hipFree(a.p);
         for (auto e : chunk_ev) (void)hipEventDestroy(e);
         for (auto e : chunk_ev2) (void)hipEventDestroy(e);
         for (auto e : bev) if (e) (void)hipEventDestroy(e);
+        for (auto& row : mev)
+            for (auto e : row) if (e) (void)hipEventDestroy(e);
+        if (fork_ev) (void)hipEventDestroy(fork_ev);
+        for (auto e : join_ev) if (e) (void)hipEventDestroy(e);
+        for (auto e : chunk_evm) if (e) (void)hipEventDestroy(e);
+        for (int k = 1; k < MAXMB; k++) if (ms[k]) (void)hipStreamDestroy(ms[k]);
         for (auto e : ev_pool) (void)hipEventDestroy(e);
         if (comm_done) (void)hipEventDestroy(comm_done);
         if (s) (void)hipStreamDestroy(s);
@@ -468,59 +511,71 @@ struct Trainer {
 
     // ------------------------------------------------------------------ bf16 fast path
     void forward_bf16() {
-        const double BTd = (double)BT;
-        // patch embedding (encoder_forward, train_vit.rs:196 -> ViT)
-        tbeg(TC_PATCH, 2.0 * B * NP * (double)KP * C);
-        im2col_bf16(patches_bf, pixels, B, cfg.img, cfg.patch, s);
-        {
+        const int Bm = B / nmb;
+        const long long R = (long long)Bm * T;  // rows per micro-batch
+        mb_fork();
+        for (int mb = 0; mb < nmb; mb++) {
+            // patch embedding (encoder_forward, train_vit.rs:196 -> ViT)
+            hipStream_t st = ms[mb];
+            const long long img0 = (long long)mb * Bm;
+            tbeg(TC_PATCH, 2.0 * Bm * NP * (double)KP * C, st);
+            im2col_bf16(patches_bf + img0 * NP * KP, pixels + img0 * 3 * cfg.img * cfg.img, Bm, cfg.img,
+                        cfg.patch, st);
             GemmArgs a;
-            a.A = patches_bf; a.lda = KP; a.B = W(P_PATCH_W); a.ldb = KP;
-            a.C = emb_tmp; a.ldc = C; a.bias = P(P_PATCH_B);
-            a.M = B * NP; a.N = C; a.K = KP; a.epi = EPI_F32_STORE;
-            gemm_bf16(a, s);
+            a.A = patches_bf + img0 * NP * KP; a.lda = KP; a.B = W(P_PATCH_W); a.ldb = KP;
+            a.C = emb_tmp + img0 * NP * C; a.ldc = C; a.bias = P(P_PATCH_B);
+            a.M = Bm * NP; a.N = C; a.K = KP; a.epi = EPI_F32_STORE;
+            gemm_bf16(a, st);
+            patch_assemble(encoded + img0 * T * C, emb_tmp + img0 * NP * C, P(P_CLS), P(P_WPE), Bm, NP, C, st);
+            tend();
         }
-        patch_assemble(encoded, emb_tmp, P(P_CLS), P(P_WPE), B, NP, C, s);
-        tend();
         for (int l = 0; l < L; l++) {
             LayerActs& a = la[l];
-            const float* x = l == 0 ? encoded : la[l - 1].res3;
-            tbeg(TC_LN_FWD, 0);
-            ln_forward_bf16(a.ln1, a.ln1_mean, a.ln1_rstd, x, P(P_LN1W, l), P(P_LN1B, l), BT, C, s);
-            tend();
-            GemmArgs q;
-            q.A = a.ln1; q.lda = C; q.B = W(P_QKVW, l); q.ldb = C; q.C = a.qkv; q.ldc = 3 * C;
-            q.bias = P(P_QKVB, l); q.M = (int)BT; q.N = 3 * C; q.K = C; q.epi = EPI_BF16_STORE;
-            gemm(TC_QKV_FWD, q, true);
-            tbeg(TC_ATTN_FWD, 4.0 * B * (double)T * T * C);
-            attn_forward_fused(a.atty, a.lse, a.qkv, B, T, C, NH, s);
-            tend();
-            GemmArgs pr;
-            pr.A = a.atty; pr.lda = C; pr.B = W(P_ATTPROJW, l); pr.ldb = C; pr.C = a.res2; pr.ldc = C;
-            pr.bias = P(P_ATTPROJB, l); pr.aux = x; pr.ldaux = C;
-            pr.M = (int)BT; pr.N = C; pr.K = C; pr.epi = EPI_F32_RESID;
-            gemm(TC_PROJ_FWD, pr, true);
-            tbeg(TC_LN_FWD, 0);
-            ln_forward_bf16(a.ln2, a.ln2_mean, a.ln2_rstd, a.res2, P(P_LN2W, l), P(P_LN2B, l), BT, C, s);
-            tend();
-            GemmArgs f;
-            f.A = a.ln2; f.lda = C; f.B = W(P_FCW, l); f.ldb = C; f.C = a.fch; f.C2 = a.fchg;
-            f.ldc = 4 * C; f.bias = P(P_FCB, l); f.M = (int)BT; f.N = 4 * C; f.K = C; f.epi = EPI_BF16_GELU;
-            gemm(TC_FC_FWD, f, true);
-            GemmArgs fp;
-            fp.A = a.fchg; fp.lda = 4 * C; fp.B = W(P_FCPROJW, l); fp.ldb = 4 * C; fp.C = a.res3;
-            fp.ldc = C; fp.bias = P(P_FCPROJB, l); fp.aux = a.res2; fp.ldaux = C;
-            fp.M = (int)BT; fp.N = C; fp.K = 4 * C; fp.epi = EPI_F32_RESID;
-            gemm(TC_FCPROJ_FWD, fp, true);
+            const float* xl = l == 0 ? encoded : la[l - 1].res3;
+            for (int mb = 0; mb < nmb; mb++) {
+                hipStream_t st = ms[mb];
+                const long long r0 = (long long)mb * R;
+                const float* x = xl + r0 * C;
+                tbeg(TC_LN_FWD, 0, st);
+                ln_forward_bf16(a.ln1 + r0 * C, a.ln1_mean + r0, a.ln1_rstd + r0, x, P(P_LN1W, l), P(P_LN1B, l), R, C, st);
+                tend();
+                GemmArgs q;
+                q.A = a.ln1 + r0 * C; q.lda = C; q.B = W(P_QKVW, l); q.ldb = C; q.C = a.qkv + r0 * 3 * C;
+                q.ldc = 3 * C; q.bias = P(P_QKVB, l); q.M = (int)R; q.N = 3 * C; q.K = C; q.epi = EPI_BF16_STORE;
+                gemm(TC_QKV_FWD, q, true, st);
+                tbeg(TC_ATTN_FWD, 4.0 * Bm * (double)T * T * C, st);
+                attn_forward_fused(a.atty + r0 * C, a.lse + (long long)mb * Bm * NH * T, a.qkv + r0 * 3 * C, Bm, T, C, NH, st);
+                tend();
+                GemmArgs pr;
+                pr.A = a.atty + r0 * C; pr.lda = C; pr.B = W(P_ATTPROJW, l); pr.ldb = C; pr.C = a.res2 + r0 * C;
+                pr.ldc = C; pr.bias = P(P_ATTPROJB, l); pr.aux = x; pr.ldaux = C;
+                pr.M = (int)R; pr.N = C; pr.K = C; pr.epi = EPI_F32_RESID;
+                gemm(TC_PROJ_FWD, pr, true, st);
+                tbeg(TC_LN_FWD, 0, st);
+                ln_forward_bf16(a.ln2 + r0 * C, a.ln2_mean + r0, a.ln2_rstd + r0, a.res2 + r0 * C, P(P_LN2W, l),
+                                P(P_LN2B, l), R, C, st);
+                tend();
+                GemmArgs f;
+                f.A = a.ln2 + r0 * C; f.lda = C; f.B = W(P_FCW, l); f.ldb = C; f.C = a.fch + r0 * 4 * C;
+                f.C2 = a.fchg + r0 * 4 * C; f.ldc = 4 * C; f.bias = P(P_FCB, l); f.M = (int)R; f.N = 4 * C;
+                f.K = C; f.epi = EPI_BF16_GELU;
+                gemm(TC_FC_FWD, f, true, st);
+                GemmArgs fp;
+                fp.A = a.fchg + r0 * 4 * C; fp.lda = 4 * C; fp.B = W(P_FCPROJW, l); fp.ldb = 4 * C;
+                fp.C = a.res3 + r0 * C; fp.ldc = C; fp.bias = P(P_FCPROJB, l); fp.aux = a.res2 + r0 * C;
+                fp.ldaux = C; fp.M = (int)R; fp.N = C; fp.K = 4 * C; fp.epi = EPI_F32_RESID;
+                gemm(TC_FCPROJ_FWD, fp, true, st);
+            }
         }
-        (void)BTd;
+        mb_join();
         head_forward();
     }
 
-    // dW[OC,Cin] += dout^T . inp (reduction over B*T rows, split-K slabs) on the weight-gradient
-    // stream once `ready` (recorded on the main stream when dout is final) has passed; `done`
-    // marks the end of its reads of dout / inp
-    void wgrad(int cls, const bf16_t* dout, int OC, const bf16_t* inp, int Cin, float* dW,
-               hipEvent_t ready, hipEvent_t done) {
+    // dW[OC,Cin] += dout^T . inp (reduction over all B*T rows, split-K slabs) on the weight-
+    // gradient stream once every micro-batch stream has passed `ready` (dout final there); the
+    // event `done` marks the end of its reads of dout / inp
+    void wgrad(int cls, const bf16_t* dout, int OC, const bf16_t* inp, int Cin, float* dW, int ready,
+               int done) {
         GemmArgs w;
         w.A = dout; w.lda = OC; w.a_kcontig = false;
         w.B = inp; w.ldb = Cin; w.b_kcontig = false;
@@ -528,17 +583,19 @@ struct Trainer {
         w.ws = gemm_ws; w.ws_bytes = gemm_ws_bytes;
         hipStream_t st = two_streams ? s2 : s;
         if (two_streams) {
-            VIT_HIP(hipEventRecord(ready, s));
-            VIT_HIP(hipStreamWaitEvent(s2, ready, 0));
+            for (int mb = 0; mb < nmb; mb++) {
+                VIT_HIP(hipEventRecord(mev[mb][ready], ms[mb]));
+                VIT_HIP(hipStreamWaitEvent(s2, mev[mb][ready], 0));
+            }
         }
         tbeg(cls, 2.0 * w.M * (double)w.N * w.K, st);
         gemm_bf16(w, st);
         tend();
-        if (two_streams) VIT_HIP(hipEventRecord(done, s2));
+        if (two_streams) VIT_HIP(hipEventRecord(bev[done], s2));
     }
-    // the main stream may overwrite a buffer once the wgrad that reads it (`done`) has finished
-    void after_wgrad(hipEvent_t done) {
-        if (two_streams) VIT_HIP(hipStreamWaitEvent(s, done, 0));
+    // a micro-batch stream may overwrite a buffer once the wgrad that reads it (`done`) finished
+    void after_wgrad(int done, hipStream_t st) {
+        if (two_streams) VIT_HIP(hipStreamWaitEvent(st, bev[done], 0));
     }
 
     void backward_bf16() {
@@ -555,59 +612,77 @@ struct Trainer {
         //   attproj_b+= colsum(dres2): LN2-backward
         //   qkv_b    += colsum(dqkv):  attention backward
         colsum_f32(G(P_FCPROJB, L - 1), dcls_x, B, C, C, s);
+        mb_fork();
+        const int Bm = B / nmb;
+        const long long R = (long long)Bm * T;
         for (int l = L - 1; l >= 0; l--) {
             LayerActs& a = la[l];
-            const float* x = l == 0 ? encoded : la[l - 1].res3;
+            const float* xl = l == 0 ? encoded : la[l - 1].res3;
             // fcproj: dfch = (dres3 . fcprojw) * gelu'(fch);  fcprojw += dres3^T . fchg
-            wgrad(TC_FCPROJ_WGRAD, rbA, C, a.fchg, 4 * C, G(P_FCPROJW, l), bev[EV_RESA], bev[EV_W1]);
-            after_wgrad(bev[EV_W2]);  // the previous layer's fc wgrad has read dfch
-            GemmArgs d1;
-            d1.A = rbA; d1.lda = C; d1.B = W(P_FCPROJW, l); d1.ldb = 4 * C; d1.b_kcontig = false;
-            d1.C = dfch; d1.ldc = 4 * C; d1.aux = a.fch; d1.ldaux = 4 * C;
-            d1.M = (int)BT; d1.N = 4 * C; d1.K = C; d1.epi = EPI_BF16_DGELU;
-            d1.colsum_out = G(P_FCB, l);
-            gemm(TC_FCPROJ_DGRAD, d1, true);
+            wgrad(TC_FCPROJ_WGRAD, rbA, C, a.fchg, 4 * C, G(P_FCPROJW, l), EV_RESA, EV_W1);
+            for (int mb = 0; mb < nmb; mb++) {
+                const long long r0 = mb * R;
+                after_wgrad(EV_W2, ms[mb]);  // the previous layer's fc wgrad has read dfch
+                GemmArgs d1;
+                d1.A = rbA + r0 * C; d1.lda = C; d1.B = W(P_FCPROJW, l); d1.ldb = 4 * C; d1.b_kcontig = false;
+                d1.C = dfch + r0 * 4 * C; d1.ldc = 4 * C; d1.aux = a.fch + r0 * 4 * C; d1.ldaux = 4 * C;
+                d1.M = (int)R; d1.N = 4 * C; d1.K = C; d1.epi = EPI_BF16_DGELU;
+                d1.colsum_out = G(P_FCB, l);
+                gemm(TC_FCPROJ_DGRAD, d1, true, ms[mb]);
+            }
             // fc: dln2 = dfch . fcw;  fcw += dfch^T . ln2
-            wgrad(TC_FC_WGRAD, dfch, 4 * C, a.ln2, C, G(P_FCW, l), bev[EV_DFCH], bev[EV_W2]);
-            GemmArgs d2;
-            d2.A = dfch; d2.lda = 4 * C; d2.B = W(P_FCW, l); d2.ldb = C; d2.b_kcontig = false;
-            d2.C = dln; d2.ldc = C; d2.M = (int)BT; d2.N = C; d2.K = 4 * C; d2.epi = EPI_F32_STORE;
-            gemm(TC_FC_DGRAD, d2, true);
-            // ln2 backward + residual: dres2 = dres3 + LN2'(dln2); attproj_b += colsum(dres2)
-            after_wgrad(bev[EV_W3]);  // the previous layer's attproj wgrad has read rbB
-            tbeg(TC_LN_BWD, 0);
-            ln_backward_fused(dnxt, rbB, dcur, G(P_LN2W, l), G(P_LN2B, l), G(P_ATTPROJB, l), dln,
-                              a.res2, P(P_LN2W, l), a.ln2_mean, a.ln2_rstd, BT, C, s);
-            tend();
+            wgrad(TC_FC_WGRAD, dfch, 4 * C, a.ln2, C, G(P_FCW, l), EV_DFCH, EV_W2);
+            for (int mb = 0; mb < nmb; mb++) {
+                const long long r0 = mb * R;
+                GemmArgs d2;
+                d2.A = dfch + r0 * 4 * C; d2.lda = 4 * C; d2.B = W(P_FCW, l); d2.ldb = C; d2.b_kcontig = false;
+                d2.C = dln + r0 * C; d2.ldc = C; d2.M = (int)R; d2.N = C; d2.K = 4 * C; d2.epi = EPI_F32_STORE;
+                gemm(TC_FC_DGRAD, d2, true, ms[mb]);
+                // ln2 backward + residual: dres2 = dres3 + LN2'(dln2); attproj_b += colsum(dres2)
+                after_wgrad(EV_W3, ms[mb]);  // the previous layer's attproj wgrad has read rbB
+                tbeg(TC_LN_BWD, 0, ms[mb]);
+                ln_backward_fused(dnxt + r0 * C, rbB + r0 * C, dcur + r0 * C, G(P_LN2W, l), G(P_LN2B, l),
+                                  G(P_ATTPROJB, l), dln + r0 * C, a.res2 + r0 * C, P(P_LN2W, l),
+                                  a.ln2_mean + r0, a.ln2_rstd + r0, R, C, ms[mb]);
+                tend();
+            }
             std::swap(dcur, dnxt);
             // attproj
-            wgrad(TC_PROJ_WGRAD, rbB, C, a.atty, C, G(P_ATTPROJW, l), bev[EV_RESB], bev[EV_W3]);
-            GemmArgs d3;
-            d3.A = rbB; d3.lda = C; d3.B = W(P_ATTPROJW, l); d3.ldb = C; d3.b_kcontig = false;
-            d3.C = datty; d3.ldc = C; d3.M = (int)BT; d3.N = C; d3.K = C; d3.epi = EPI_BF16_STORE;
-            gemm(TC_PROJ_DGRAD, d3, true);
-            // attention (+ qkv_b)
-            after_wgrad(bev[EV_W4]);  // the previous layer's qkv wgrad has read dqkv
-            tbeg(TC_ATTN_BWD, 8.0 * B * (double)T * T * C);
-            attn_backward_fused(dqkv, datty, a.qkv, a.atty, a.lse, B, T, C, NH, s, G(P_QKVB, l),
-                                attn_part);
-            tend();
+            wgrad(TC_PROJ_WGRAD, rbB, C, a.atty, C, G(P_ATTPROJW, l), EV_RESB, EV_W3);
+            for (int mb = 0; mb < nmb; mb++) {
+                const long long r0 = mb * R;
+                GemmArgs d3;
+                d3.A = rbB + r0 * C; d3.lda = C; d3.B = W(P_ATTPROJW, l); d3.ldb = C; d3.b_kcontig = false;
+                d3.C = datty + r0 * C; d3.ldc = C; d3.M = (int)R; d3.N = C; d3.K = C; d3.epi = EPI_BF16_STORE;
+                gemm(TC_PROJ_DGRAD, d3, true, ms[mb]);
+                // attention (+ qkv_b)
+                after_wgrad(EV_W4, ms[mb]);  // the previous layer's qkv wgrad has read dqkv
+                tbeg(TC_ATTN_BWD, 8.0 * Bm * (double)T * T * C, ms[mb]);
+                attn_backward_fused(dqkv + r0 * 3 * C, datty + r0 * C, a.qkv + r0 * 3 * C, a.atty + r0 * C,
+                                    a.lse + (long long)mb * Bm * NH * T, Bm, T, C, NH, ms[mb], G(P_QKVB, l),
+                                    attn_part + (long long)mb * Bm * NH * 3 * 64);
+                tend();
+            }
             // qkv
-            wgrad(TC_QKV_WGRAD, dqkv, 3 * C, a.ln1, C, G(P_QKVW, l), bev[EV_DQKV], bev[EV_W4]);
-            GemmArgs d4;
-            d4.A = dqkv; d4.lda = 3 * C; d4.B = W(P_QKVW, l); d4.ldb = C; d4.b_kcontig = false;
-            d4.C = dln; d4.ldc = C; d4.M = (int)BT; d4.N = C; d4.K = 3 * C; d4.epi = EPI_F32_STORE;
-            gemm(TC_QKV_DGRAD, d4, true);
-            // ln1 backward: dres = dres2 + LN1'(dln1); fcproj_b of layer l-1 += colsum(dres)
-            after_wgrad(bev[EV_W1]);  // this layer's fcproj wgrad has read rbA
-            tbeg(TC_LN_BWD, 0);
-            ln_backward_fused(dnxt, rbA, dcur, G(P_LN1W, l), G(P_LN1B, l),
-                              l > 0 ? G(P_FCPROJB, l - 1) : nullptr, dln, x, P(P_LN1W, l),
-                              a.ln1_mean, a.ln1_rstd, BT, C, s);
-            tend();
+            wgrad(TC_QKV_WGRAD, dqkv, 3 * C, a.ln1, C, G(P_QKVW, l), EV_DQKV, EV_W4);
+            for (int mb = 0; mb < nmb; mb++) {
+                const long long r0 = mb * R;
+                GemmArgs d4;
+                d4.A = dqkv + r0 * 3 * C; d4.lda = 3 * C; d4.B = W(P_QKVW, l); d4.ldb = C; d4.b_kcontig = false;
+                d4.C = dln + r0 * C; d4.ldc = C; d4.M = (int)R; d4.N = C; d4.K = 3 * C; d4.epi = EPI_F32_STORE;
+                gemm(TC_QKV_DGRAD, d4, true, ms[mb]);
+                // ln1 backward: dres = dres2 + LN1'(dln1); fcproj_b of layer l-1 += colsum(dres)
+                after_wgrad(EV_W1, ms[mb]);  // this layer's fcproj wgrad has read rbA
+                tbeg(TC_LN_BWD, 0, ms[mb]);
+                ln_backward_fused(dnxt + r0 * C, rbA + r0 * C, dcur + r0 * C, G(P_LN1W, l), G(P_LN1B, l),
+                                  l > 0 ? G(P_FCPROJB, l - 1) : nullptr, dln + r0 * C, xl + r0 * C,
+                                  P(P_LN1W, l), a.ln1_mean + r0, a.ln1_rstd + r0, R, C, ms[mb]);
+                tend();
+            }
             std::swap(dcur, dnxt);
             chunk_done(L - l);
         }
+        mb_join();
         if (two_streams) {  // every wgrad done before the slab workspace / grads are reused
             VIT_HIP(hipEventRecord(bev[EV_JOIN], s2));
             VIT_HIP(hipStreamWaitEvent(s, bev[EV_JOIN], 0));
@@ -718,9 +793,14 @@ struct Trainer {
         if (!comm || !overlap) return;
         VIT_HIP(hipEventRecord(chunk_ev[c], s));
         VIT_HIP(hipStreamWaitEvent(s_comm, chunk_ev[c], 0));
-        if (two_streams && prec == VIT_BF16) {  // the chunk's weight gradients come from s2
+        if (two_streams && prec == VIT_BF16) {  // the chunk's gradients also come from s2 / ms[]
             VIT_HIP(hipEventRecord(chunk_ev2[c], s2));
             VIT_HIP(hipStreamWaitEvent(s_comm, chunk_ev2[c], 0));
+            for (int k = 1; k < nmb; k++) {
+                hipEvent_t e = chunk_evm[(size_t)c * MAXMB + k];
+                VIT_HIP(hipEventRecord(e, ms[k]));
+                VIT_HIP(hipStreamWaitEvent(s_comm, e, 0));
+            }
         }
         const long long o = chunk_off[c], n = chunk_off[c + 1] - chunk_off[c];
         ncclResult_t r = ncclAllReduce(grads + o, grads + o, (size_t)n, ncclFloat32, ncclSum, comm, s_comm);
