@@ -66,6 +66,9 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true", help="one all-reduce after backward")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events")
+    ap.add_argument("--serial", action="store_true",
+                    help="run every pass with stream concurrency off (the profile command of the "
+                         "per-kernel roofline pass)")
     return ap.parse_args()
 
 
@@ -181,6 +184,8 @@ def main():
         dist.broadcast_object_list(uid, src=0)
         m.dp_init(rank, world, uid[0], overlap=not args.no_overlap)
     b_global = B * world
+    if args.serial:
+        m.set_concurrency(False)
 
     for _ in range(args.warmup):
         m.train_step(args.lr, b_global)
@@ -206,12 +211,16 @@ def main():
             dt = float(t.item())
         return dt
 
-    # the timed region: K plain steps (no per-kernel events: ~70 event pairs per step cost ~3 %)
+    # the timed region: K plain steps with the production stream concurrency (two micro-batch
+    # streams + the weight-gradient stream) and no per-kernel events (~3 % of a step)
     dt = timed(args.steps)
-    # then the same K steps again with HIP events around every kernel class on the stream it is
-    # launched on, for the per-kernel breakdown and the roofline of the dominant kernel
+    # then the same K steps again, kernels one at a time (concurrency off), with HIP events
+    # around every kernel class: the per-kernel breakdown and the roofline of the dominant kernel
+    # (durations of kernels that share the GPU with another stream's kernels mean nothing)
     kern = {}
     if not args.no_timing:
+        m.set_concurrency(False)
+        timed(1)
         m.timing_reset()
         m.set_timing(True)
         timed(args.steps)
@@ -250,8 +259,8 @@ def main():
             "train_gflop_per_image": round(gflop_img, 3),
             "loss_after_warmup": round(loss_w, 4),
             "roofline": roof, "kernels": ksum,
-            "kernels_note": "per-kernel ms from HIP events over a second pass of the same steps; "
-                            "wgrad GEMMs run on a second stream beside the main stream",
+            "kernels_note": "per-kernel ms from HIP events over a second pass of the same steps run "
+                            "with stream concurrency off (kernels one at a time)",
         }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg)

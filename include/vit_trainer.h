@@ -70,7 +70,12 @@ int vit_dp_get_unique_id(char* out);   /* rank 0 creates; broadcast the bytes ou
  *         1 = per-layer chunks on a side stream overlapped with backward (default) */
 int vit_trainer_dp_init(vit_trainer_t* t, int rank, int world, const char* unique_id, int overlap);
 
-/* ---- per-kernel-class timing with HIP events on the trainer's stream ---- */
+/* ---- stream concurrency (bf16 mode): on (default) = the batch runs as two micro-batch row halves
+ *      on two streams and the weight-gradient GEMMs on a third; off = one stream, kernels one at a
+ *      time (per-kernel roofline timing).  Call between steps. ---- */
+int vit_trainer_set_concurrency(vit_trainer_t* t, int on);
+
+/* ---- per-kernel-class timing with HIP events on the stream each kernel runs on ---- */
 int vit_trainer_set_timing(vit_trainer_t* t, int on);
 /* fills up to max entries; returns the number of classes. names point to static strings */
 int vit_trainer_timing(vit_trainer_t* t, const char** names, double* total_ms, long long* calls,

@@ -1003,6 +1003,14 @@ int vit_trainer_dp_init(vit_trainer_t* h, int rank, int world, const char* uid, 
     }
     return 0;
 }
+int vit_trainer_set_concurrency(vit_trainer_t* h, int on) {
+    auto& t = h->t;
+    VIT_HIP(hipStreamSynchronize(t.s2));
+    for (int k = 0; k < vit::Trainer::MAXMB; k++) if (t.ms[k]) VIT_HIP(hipStreamSynchronize(t.ms[k]));
+    t.two_streams = on != 0;
+    t.nmb = (on && t.B % 2 == 0) ? 2 : 1;
+    return vit::has_error();
+}
 int vit_trainer_set_timing(vit_trainer_t* h, int on) {
     h->t.timing = on != 0;
     return 0;
