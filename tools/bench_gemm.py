@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--C", type=int, default=768)
     ap.add_argument("--variants", default="2,4")
     ap.add_argument("--no-epi", action="store_true")
+    ap.add_argument("--modes", default=None,
+                    help="comma-separated gemm_bf16_set_debug flag sets to A/B (2 = no epilogue, "
+                         "4 = g2 prefetch depth 3); default 0 (and 2 with --no-epi)")
     ap.add_argument("--only", default=None, help="comma-separated GEMM names")
     args = ap.parse_args()
     L = vit.lib()
@@ -67,7 +70,7 @@ def main():
         keep = set(args.only.split(","))
         g = [x for x in g if x[0] in keep]
     variants = [int(v) for v in args.variants.split(",")]
-    modes = [0, 2] if args.no_epi else [0]
+    modes = [int(x) for x in args.modes.split(",")] if args.modes else ([0, 2] if args.no_epi else [0])
 
     def run(name, M, N, K, ak, lda, bk, ldb, epi):
         if epi == 2:
@@ -100,7 +103,7 @@ def main():
     L.gemm_bf16_set_debug(0)
     tot = {}
     print(f"{'gemm':14s} {'M':>6s} {'N':>5s} {'K':>6s} epi " +
-          " ".join(f"{'v%d%s' % (v, '/noepi' if m else ''):>16s}" for v in variants for m in modes))
+          " ".join(f"{'v%d/f%d' % (v, m):>16s}" for v in variants for m in modes))
     for sh in g:
         name, M, N, K = sh[:4]
         fl = 2.0 * M * N * K
@@ -113,7 +116,7 @@ def main():
         print(f"{name:14s} {M:6d} {N:5d} {K:6d} {sh[8]:3d} " + " ".join(f"{c:>16s}" for c in cells), flush=True)
     fl_all = sum(2.0 * x[1] * x[2] * x[3] for x in g)
     print("total per layer: " + "  ".join(
-        f"v{v}{'/noepi' if m else ''} {tot[(v, m)]:.3f} ms ({fl_all / tot[(v, m)] / 1e9:.0f} TF/s)"
+        f"v{v}/f{m} {tot[(v, m)]:.3f} ms ({fl_all / tot[(v, m)] / 1e9:.0f} TF/s)"
         for v in variants for m in modes))
 
 

@@ -60,7 +60,8 @@ void gemm_f32(const GemmArgs& a, hipStream_t s);
 void gemm_bf16(const GemmArgs& a, hipStream_t s);
 bool gemm_bf16_supported(const GemmArgs& a);
 // engine selection for A/B measurements in one process: 1 = 128x128, 2 = 256x256 (1 WG/CU, default),
-// 4 = 256x128 (2 WG/CU); anything else = 2 (the default); debug flag 2 = skip epilogues (main loop only)
+// 4 = 256x128 (2 WG/CU); anything else = 2 (the default); debug flags: 2 = skip epilogues (main
+// loop only), 4 = 256x256 engine with LDS-DMA prefetch depth 3 instead of 2
 void gemm_set_variant(int v);
 void gemm_set_debug(int flags);
 

@@ -441,7 +441,6 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmParams p) {
 // clamped on load (they only feed masked outputs); K must be a multiple of 64.
 namespace g2 {
 constexpr int BM = 256, BN = 256, BK = 32, NT = 512;
-constexpr int NSLOT = 4;                   // LDS ring slots (DMA 2 steps ahead)
 constexpr int IMG_BYTES = 256 * BK * 2;    // 16 KiB per operand per slot
 constexpr int SLOT_BYTES = 2 * IMG_BYTES;  // 32 KiB (A | B)
 constexpr int KTILE = 64;                  // K granularity required of callers (and split chunks)
@@ -525,10 +524,30 @@ __device__ __forceinline__ void barrier_lds() {
 // NSLOT slots, DMA two steps ahead; a wave retires its own pieces of step s+1 (vmcnt) in phase 1
 // of step s, two barriers (three with the stagger) before anyone reads them; a slot is refilled
 // >= 6 barriers after its last read; every barrier is preceded by lgkmcnt(0).
-constexpr int SMEM_BYTES = NSLOT * SLOT_BYTES > 8 * STG_WAVE_BYTES ? NSLOT * SLOT_BYTES : 8 * STG_WAVE_BYTES;
-template <bool AK, bool BKC, int EPI, bool SCHED>
+// DEPTH = K-steps of LDS-DMA in flight ahead of the step being read (ring of DEPTH + 2 slots:
+// a slot is refilled >= 2 steps after its last read).  Depth 2 (4 x 32 KiB) is the default:
+// depth 3 (5 slots, 160 KiB) measured ~10 % slower on every trainer GEMM (tools/bench_gemm.py
+// --modes 0,4).  The DMA of steps past the tile's K range is not issued, so the counted waits
+// below drop to the pieces that are.
+template <int DEPTH>
+constexpr int smem_bytes() {
+    return (DEPTH + 2) * SLOT_BYTES > 8 * STG_WAVE_BYTES ? (DEPTH + 2) * SLOT_BYTES : 8 * STG_WAVE_BYTES;
+}
+// s_waitcnt vmcnt(n) for the counts the pipeline uses (the immediate must be a literal)
+__device__ __forceinline__ void wait_vm(int n) {
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+}
+template <bool AK, bool BKC, int EPI, int DEPTH>
 __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
-    __shared__ __attribute__((aligned(1024))) char smem[SMEM_BYTES];
+    constexpr int NS = DEPTH + 2;
+    __shared__ __attribute__((aligned(1024))) char smem[smem_bytes<DEPTH>()];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
@@ -551,12 +570,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
 #pragma unroll
         for (int b = 0; b < 4; b++) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    auto slot_of = [&](int st) { return smem + (st % NSLOT) * SLOT_BYTES; };
-    auto issue_a = [&](int st) {  // A-image pieces of step st (clamped: re-stage the last step)
-        stage<AK>(A, p.lda, tm0, p.M, kbeg + min(st, nk - 1) * BK, slot_of(st), wave, lane);
+    auto slot_of = [&](int st) { return smem + (st % NS) * SLOT_BYTES; };
+    auto issue_a = [&](int st) {  // A-image pieces of step st (none past the K range)
+        if (st < nk) stage<AK>(A, p.lda, tm0, p.M, kbeg + st * BK, slot_of(st), wave, lane);
     };
     auto issue_b = [&](int st) {
-        stage<BKC>(B, p.ldb, tn0, p.N, kbeg + min(st, nk - 1) * BK, slot_of(st) + IMG_BYTES, wave, lane);
+        if (st < nk) stage<BKC>(B, p.ldb, tn0, p.N, kbeg + st * BK, slot_of(st) + IMG_BYTES, wave, lane);
     };
     auto bar = [&]() {
         __builtin_amdgcn_sched_barrier(0);
@@ -590,8 +609,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
 
     const bool lagging = wave >= 4;
     if (nk > 0) {
-        issue_a(0); issue_b(0); issue_a(1); issue_b(1);
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // own pieces of step 0
+#pragma unroll
+        for (int st = 0; st < DEPTH; st++) { issue_a(st); issue_b(st); }
+        wait_vm(4 * (min(DEPTH, nk) - 1));  // own pieces of step 0
         bar();
         if (lagging) {
             __builtin_amdgcn_s_setprio(1);  // static priority for the younger half (T5)
@@ -606,7 +626,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
         for (int b = 0; b < 4; b++) fb[b] = frag<BKC>(img + IMG_BYTES, wn * 64 + b * 16, lane);
 #pragma unroll
         for (int a = 0; a < 4; a++) alo[a] = frag<AK>(img, wm * 128 + a * 16, lane);
-        issue_a(kt + 2);
+        issue_a(kt + DEPTH);
         bar();
         mfma_half(0, alo, fb);
         bar();
@@ -614,8 +634,10 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
 #pragma unroll
         for (int a = 0; a < 4; a++) ahi[a] = frag<AK>(img, wm * 128 + (4 + a) * 16, lane);
         bias_sum(kt);
-        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // own pieces of step kt+1 landed
-        issue_b(kt + 2);
+        // own pieces of step kt+1 landed: the younger ones are steps kt+2 .. kt+DEPTH-1 (4 each)
+        // and the A half of step kt+DEPTH (2), as far as they were issued
+        wait_vm(4 * max(0, min(kt + DEPTH, nk) - (kt + 2)) + (kt + DEPTH < nk ? 2 : 0));
+        issue_b(kt + DEPTH);
         bar();
         mfma_half(1, ahi, fb);
         bar();
@@ -666,7 +688,7 @@ using g2::BM;
 using g2::BN;
 using g2::BK;
 using g2::NT;
-using g2::NSLOT;
+constexpr int NSLOT = 4;  // g3 keeps the 4-slot ring (160 KiB with its 32 KiB staging area)
 using g2::IMG_BYTES;
 using g2::SLOT_BYTES;
 constexpr int RING_BYTES = NSLOT * SLOT_BYTES;        // 128 KiB
@@ -1258,12 +1280,12 @@ static void launch_bf16(const GemmArgs& a, const GemmParams& p, dim3 grid, hipSt
 
 template <bool AK, bool BKC>
 static void launch_g2(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStream_t s) {
-    static const int sched = getenv("VIT_G2_SCHED") ? atoi(getenv("VIT_G2_SCHED")) : 1;
+    const bool deep = (g_debug_flags & 4) != 0;  // debug flag 4: prefetch depth 3 (A/B)
     switch (a.epi) {
 #define VIT_CASE(E) \
     case E:                                                                    \
-        if (sched) g2::gemm_kernel<AK, BKC, E, true><<<grid, g2::NT, 0, s>>>(p);  \
-        else g2::gemm_kernel<AK, BKC, E, false><<<grid, g2::NT, 0, s>>>(p);       \
+        if (deep) g2::gemm_kernel<AK, BKC, E, 3><<<grid, g2::NT, 0, s>>>(p);      \
+        else g2::gemm_kernel<AK, BKC, E, 2><<<grid, g2::NT, 0, s>>>(p);           \
         break;
         VIT_CASE(EPI_F32_STORE)
         VIT_CASE(EPI_F32_ACC)

@@ -201,13 +201,21 @@ __global__ __launch_bounds__(256) void ln_fwd_vec_k(TO* __restrict__ out, float*
     }
 }
 
-template <int NV>
+// 4 consecutive values k*4 .. k*4+3 of a row (fp32 or bf16 storage) as fp32
+__device__ __forceinline__ float4 ld4(const float* p, int k) { return reinterpret_cast<const float4*>(p)[k]; }
+__device__ __forceinline__ float4 ld4(const bf16_t* p, int k) {
+    const uint2 u = reinterpret_cast<const uint2*>(p)[k];
+    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                       __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+}
+
+template <int NV, typename TD>
 __global__ __launch_bounds__(256) void ln_bwd_vec_k(float* __restrict__ dinp, bf16_t* __restrict__ dinp_bf,
                                                     const float* __restrict__ dres_in,
                                                     float* __restrict__ dweight,
                                                     float* __restrict__ dbias,
                                                     float* __restrict__ dsum,
-                                                    const float* __restrict__ dout,
+                                                    const TD* __restrict__ dout,
                                                     const float* __restrict__ inp,
                                                     const float* __restrict__ weight,
                                                     const float* __restrict__ mean,
@@ -223,14 +231,14 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_k(float* __restrict__ dinp, bf
     }
     const long long nwaves = (long long)gridDim.x * 4;
     for (long long row = blockIdx.x * 4LL + wave; row < rows; row += nwaves) {
-        const float4* dy4 = reinterpret_cast<const float4*>(dout + row * C);
+        const TD* dyr = dout + row * C;
         const float4* x4 = reinterpret_cast<const float4*>(inp + row * C);
         const float mu = mean[row], rs = rstd[row];
         float4 dy[NV], nr[NV];
         float a = 0.f, bs = 0.f;
 #pragma unroll
         for (int j = 0; j < NV; j++) {
-            dy[j] = dy4[lane + 64 * j];
+            dy[j] = ld4(dyr, lane + 64 * j);
             const float4 x = x4[lane + 64 * j];
             nr[j] = make_float4((x.x - mu) * rs, (x.y - mu) * rs, (x.z - mu) * rs, (x.w - mu) * rs);
             const float d0 = w4[j].x * dy[j].x, d1 = w4[j].y * dy[j].y, d2 = w4[j].z * dy[j].z, d3 = w4[j].w * dy[j].w;
@@ -421,8 +429,9 @@ static int ln_bwd_grid(long long rows) {
     long long g = (rows + 31) / 32;  // ~8 rows per wave
     return (int)(g < 1 ? 1 : (g > 2048 ? 2048 : g));
 }
+template <typename TD>
 static void ln_backward_any(float* dinp, bf16_t* dinp_bf, const float* dres_in, float* dw,
-                            float* db, float* dsum, const float* dout, const float* inp,
+                            float* db, float* dsum, const TD* dout, const float* inp,
                             const float* w, const float* mean, const float* rstd, long long rows,
                             int C, hipStream_t s) {
     if (rows <= 0) return;
@@ -430,7 +439,7 @@ static void ln_backward_any(float* dinp, bf16_t* dinp_bf, const float* dres_in, 
                      (((uintptr_t)dinp | (uintptr_t)dout | (uintptr_t)inp | (uintptr_t)w |
                        (uintptr_t)dres_in | (uintptr_t)dinp_bf) & 15) == 0;
     if (!vec) {
-        ln_bwd_k<float><<<ln_bwd_grid(rows), 256, 2 * C * sizeof(float), s>>>(
+        ln_bwd_k<TD><<<ln_bwd_grid(rows), 256, 2 * C * sizeof(float), s>>>(
             dinp, dinp_bf, dres_in, dw, db, dout, inp, w, mean, rstd, rows, C);
         after_launch("layernorm_backward");
         if (dsum) colsum_f32(dsum, dinp, (int)rows, C, C, s);
@@ -440,7 +449,7 @@ static void ln_backward_any(float* dinp, bf16_t* dinp_bf, const float* dres_in, 
     const int grid = (int)(g < 1 ? 1 : (g > 1024 ? 1024 : g));
     const size_t lds = 12 * (size_t)C * sizeof(float);
     if (dsum && !dres_in) { set_error("layernorm_backward: output column sum needs dres_in"); return; }
-#define VIT_LNB(NV) ln_bwd_vec_k<NV><<<grid, 256, lds, s>>>(dinp, dinp_bf, dres_in, dw, db, dsum, dout, inp, w, mean, rstd, rows, C)
+#define VIT_LNB(NV) ln_bwd_vec_k<NV, TD><<<grid, 256, lds, s>>>(dinp, dinp_bf, dres_in, dw, db, dsum, dout, inp, w, mean, rstd, rows, C)
     switch (C / 256) {
         case 1: VIT_LNB(1); break;
         case 2: VIT_LNB(2); break;
@@ -463,6 +472,13 @@ void ln_backward_fused(float* dres_out, bf16_t* dres_out_bf, const float* dres_i
                        float* db, float* dres_colsum, const float* dout, const float* inp,
                        const float* w, const float* mean, const float* rstd, long long rows, int C,
                        hipStream_t s) {
+    ln_backward_any(dres_out, dres_out_bf, dres_in, dw, db, dres_colsum, dout, inp, w, mean, rstd,
+                    rows, C, s);
+}
+void ln_backward_fused_bf16(float* dres_out, bf16_t* dres_out_bf, const float* dres_in, float* dw,
+                            float* db, float* dres_colsum, const bf16_t* dout, const float* inp,
+                            const float* w, const float* mean, const float* rstd, long long rows,
+                            int C, hipStream_t s) {
     ln_backward_any(dres_out, dres_out_bf, dres_in, dw, db, dres_colsum, dout, inp, w, mean, rstd,
                     rows, C, s);
 }

@@ -19,6 +19,11 @@ void ln_backward_fused(float* dres_out, bf16_t* dres_out_bf, const float* dres_i
                        float* db, float* dres_colsum, const float* dout, const float* inp,
                        const float* w, const float* mean, const float* rstd, long long rows, int C,
                        hipStream_t s);
+// the same with the LN-output gradient in bf16 (the dgrad GEMM writes it as bf16)
+void ln_backward_fused_bf16(float* dres_out, bf16_t* dres_out_bf, const float* dres_in, float* dw,
+                            float* db, float* dres_colsum, const bf16_t* dout, const float* inp,
+                            const float* w, const float* mean, const float* rstd, long long rows,
+                            int C, hipStream_t s);
 void convert_f2bf(bf16_t* out, const float* inp, long long n, hipStream_t s);
 void sgd(float* p, const float* g, long long n, float lr, hipStream_t s);
 void softmax_rows(float* probs, const float* logits, long long rows, int V, hipStream_t s);

@@ -137,6 +137,7 @@ struct Trainer {
     // grads scratch
     float *dlosses = nullptr, *dlogits = nullptr, *dlnf = nullptr, *dcls_x = nullptr;
     float *dres_a = nullptr, *dres_b = nullptr, *dln = nullptr;
+    bf16_t* dln_bf = nullptr;  // bf16 mode: LN-output gradient from the fc / qkv dgrad GEMMs
     bf16_t *dres_bf = nullptr, *dres_bf2 = nullptr, *dfch = nullptr, *datty = nullptr, *dqkv = nullptr, *dpatch_bf = nullptr;
     float* dpatch_f = nullptr;
     // fp32-mode per-layer grad scratch (one layer, zeroed per layer)
@@ -387,7 +388,7 @@ struct Trainer {
                 a.fchg = alloc<bf16_t>(BT * 4 * C);
                 a.res3 = alloc<float>(BT * C);
             }
-            dln = alloc<float>(BT * C);
+            dln_bf = alloc<bf16_t>(BT * C);
             dres_bf = alloc<bf16_t>(BT * C);
             dres_bf2 = alloc<bf16_t>(BT * C);
             dfch = alloc<bf16_t>(BT * 4 * C);
@@ -636,13 +637,13 @@ struct Trainer {
                 const long long r0 = mb * R;
                 GemmArgs d2;
                 d2.A = dfch + r0 * 4 * C; d2.lda = 4 * C; d2.B = W(P_FCW, l); d2.ldb = C; d2.b_kcontig = false;
-                d2.C = dln + r0 * C; d2.ldc = C; d2.M = (int)R; d2.N = C; d2.K = 4 * C; d2.epi = EPI_F32_STORE;
+                d2.C = dln_bf + r0 * C; d2.ldc = C; d2.M = (int)R; d2.N = C; d2.K = 4 * C; d2.epi = EPI_BF16_STORE;
                 gemm(TC_FC_DGRAD, d2, true, ms[mb]);
                 // ln2 backward + residual: dres2 = dres3 + LN2'(dln2); attproj_b += colsum(dres2)
                 after_wgrad(EV_W3, ms[mb]);  // the previous layer's attproj wgrad has read rbB
                 tbeg(TC_LN_BWD, 0, ms[mb]);
-                ln_backward_fused(dnxt + r0 * C, rbB + r0 * C, dcur + r0 * C, G(P_LN2W, l), G(P_LN2B, l),
-                                  G(P_ATTPROJB, l), dln + r0 * C, a.res2 + r0 * C, P(P_LN2W, l),
+                ln_backward_fused_bf16(dnxt + r0 * C, rbB + r0 * C, dcur + r0 * C, G(P_LN2W, l), G(P_LN2B, l),
+                                  G(P_ATTPROJB, l), dln_bf + r0 * C, a.res2 + r0 * C, P(P_LN2W, l),
                                   a.ln2_mean + r0, a.ln2_rstd + r0, R, C, ms[mb]);
                 tend();
             }
@@ -669,13 +670,13 @@ struct Trainer {
                 const long long r0 = mb * R;
                 GemmArgs d4;
                 d4.A = dqkv + r0 * 3 * C; d4.lda = 3 * C; d4.B = W(P_QKVW, l); d4.ldb = C; d4.b_kcontig = false;
-                d4.C = dln + r0 * C; d4.ldc = C; d4.M = (int)R; d4.N = C; d4.K = 3 * C; d4.epi = EPI_F32_STORE;
+                d4.C = dln_bf + r0 * C; d4.ldc = C; d4.M = (int)R; d4.N = C; d4.K = 3 * C; d4.epi = EPI_BF16_STORE;
                 gemm(TC_QKV_DGRAD, d4, true, ms[mb]);
                 // ln1 backward: dres = dres2 + LN1'(dln1); fcproj_b of layer l-1 += colsum(dres)
                 after_wgrad(EV_W1, ms[mb]);  // this layer's fcproj wgrad has read rbA
                 tbeg(TC_LN_BWD, 0, ms[mb]);
-                ln_backward_fused(dnxt + r0 * C, rbA + r0 * C, dcur + r0 * C, G(P_LN1W, l), G(P_LN1B, l),
-                                  l > 0 ? G(P_FCPROJB, l - 1) : nullptr, dln + r0 * C, xl + r0 * C,
+                ln_backward_fused_bf16(dnxt + r0 * C, rbA + r0 * C, dcur + r0 * C, G(P_LN1W, l), G(P_LN1B, l),
+                                  l > 0 ? G(P_FCPROJB, l - 1) : nullptr, dln_bf + r0 * C, xl + r0 * C,
                                   P(P_LN1W, l), a.ln1_mean + r0, a.ln1_rstd + r0, R, C, ms[mb]);
                 tend();
             }
