@@ -482,6 +482,43 @@ void ln_backward_fused_bf16(float* dres_out, bf16_t* dres_out_bf, const float* d
     ln_backward_any(dres_out, dres_out_bf, dres_in, dw, db, dres_colsum, dout, inp, w, mean, rstd,
                     rows, C, s);
 }
+// out[c][r] = in[r][c] for `count` matrices of R x Cc bf16 spaced `stride` elements apart
+// (in and out use the same stride); 64 x 64 tiles through LDS, 16-B global accesses.
+__global__ __launch_bounds__(256) void transpose_bf16_k(bf16_t* __restrict__ out,
+                                                        const bf16_t* __restrict__ in, int R, int Cc,
+                                                        long long stride) {
+    __shared__ uint16_t tile[64][64 + 2];
+    const long long mo = (long long)blockIdx.z * stride;
+    const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+    const int t = threadIdx.x, tr = t >> 2, tc = (t & 3) * 16;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {  // 256 threads x 2 x 8 elements = the 64 x 64 tile
+        const int r = r0 + tr, c = c0 + tc + h * 8;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (r < R && c < Cc) v = *reinterpret_cast<const uint4*>(in + mo + (long long)r * Cc + c);
+        const uint16_t* e = reinterpret_cast<const uint16_t*>(&v);
+#pragma unroll
+        for (int j = 0; j < 8; j++) tile[tr][tc + h * 8 + j] = e[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int oc = c0 + tr, orr = r0 + tc + h * 8;  // output row = input column
+        if (oc >= Cc || orr >= R) continue;
+        uint16_t e[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) e[j] = tile[tc + h * 8 + j][tr];
+        *reinterpret_cast<uint4*>(out + mo + (long long)oc * R + orr) = *reinterpret_cast<const uint4*>(e);
+    }
+}
+void transpose_bf16(bf16_t* out, const bf16_t* in, int R, int Cc, int count, long long stride,
+                    hipStream_t s) {
+    if (R <= 0 || Cc <= 0 || count <= 0) return;
+    if (R % 8 || Cc % 8) { set_error("transpose_bf16: dims must be multiples of 8 (%d x %d)", R, Cc); return; }
+    dim3 grid(cdiv(Cc, 64), cdiv(R, 64), count);
+    transpose_bf16_k<<<grid, 256, 0, s>>>(out, in, R, Cc, stride);
+    after_launch("transpose_bf16");
+}
 void convert_f2bf(bf16_t* out, const float* inp, long long n, hipStream_t s) {
     if (n <= 0) return;
     f2bf_k<<<grid_for(n, 256), 256, 0, s>>>(out, inp, n);

@@ -35,6 +35,9 @@ void im2col_f32(float* out, const float* px, int B, int IMG, int P, hipStream_t 
 void im2col_bf16(bf16_t* out, const float* px, int B, int IMG, int P, hipStream_t s);
 void patch_assemble(float* enc, const float* emb, const float* cls, const float* wpe, int B,
                     int NP, int C, hipStream_t s);
+// out[c][r] = in[r][c] for `count` R x Cc bf16 matrices `stride` elements apart (in and out)
+void transpose_bf16(bf16_t* out, const bf16_t* in, int R, int Cc, int count, long long stride,
+                    hipStream_t s);
 void patch_gather_f32(float* out, const float* denc, int B, int NP, int C, hipStream_t s);
 void patch_gather_bf16(bf16_t* out, const float* denc, int B, int NP, int C, hipStream_t s);
 void patch_small_grads(float* dcls, float* dwpe, float* dpb, const float* denc, int B, int T,

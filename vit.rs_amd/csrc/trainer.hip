@@ -98,8 +98,14 @@ struct Trainer {
     // micro-batches: the batch is processed as NMB row ranges on NMB streams (ms[0] = s), so the
     // kernels of one half (GEMM epilogue bursts, LayerNorm, attention) overlap the other's GEMM
     // main loops; wgrads (on s2) still reduce over the whole batch
-    static constexpr int MAXMB = 2;
-    int nmb = 1;
+    static constexpr int MAXMB = 4;
+    int nmb = 1, mb_want = 2;
+    int pick_nmb(int want) const {
+        if (!two_streams) return 1;
+        for (int k = want < MAXMB ? want : MAXMB; k >= 2; k--)
+            if (B % k == 0) return k;
+        return 1;
+    }
     hipStream_t ms[MAXMB]{};
     hipEvent_t mev[MAXMB][EV_COUNT]{};
     hipEvent_t fork_ev = nullptr, join_ev[MAXMB]{};
@@ -114,6 +120,7 @@ struct Trainer {
     float* attn_part = nullptr;   // per-(b,h) qkv-bias partial sums of the attention backward
     size_t gemm_ws_bytes = 0;
     bf16_t* pbf = nullptr;
+    bf16_t* pbfT = nullptr;  // same offsets as pbf; only the four layer weight tensors are used
     float* pixels = nullptr;
     int* labels = nullptr;
     std::vector<DevBuf> allocs;
@@ -180,6 +187,8 @@ struct Trainer {
     float* P(int ti, int l = 0) const { return params + off[ti * L + l]; }
     float* G(int ti, int l = 0) const { return grads + off[ti * L + l]; }
     bf16_t* W(int ti, int l = 0) const { return pbf + off[ti * L + l]; }
+    // transposed bf16 copy of a layer weight ([Cin][OC]): the dgrad GEMMs read it K-contiguous
+    bf16_t* WT(int ti, int l = 0) const { return pbfT + off[ti * L + l]; }
 
     void build_layout() {
         const long long C_ = C, K = KP;
@@ -334,8 +343,8 @@ struct Trainer {
         for (auto& e : join_ev) VIT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         {
             const char* e = getenv("VIT_MICROBATCH");
-            const int want = e ? atoi(e) : 2;
-            nmb = (want >= 2 && B % 2 == 0 && two_streams) ? 2 : 1;
+            mb_want = e ? atoi(e) : 2;
+            nmb = pick_nmb(mb_want);
         }
         chunk_evm.resize((size_t)(L + 2) * MAXMB);
         for (auto& e : chunk_evm) VIT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -371,6 +380,7 @@ struct Trainer {
                 return false;
             }
             pbf = alloc<bf16_t>(arena_elems);
+            pbfT = alloc<bf16_t>(arena_elems);
             patches_bf = alloc<bf16_t>((long long)B * NP * KP);
             for (int l = 0; l < L; l++) {
                 LayerActs& a = la[l];
@@ -468,6 +478,19 @@ struct Trainer {
         if (prec != VIT_BF16) return;
         to_bf16_k<<<grid_for(arena_elems, 256), 256, 0, s>>>(pbf, params, arena_elems);
         after_launch("params_to_bf16");
+        refresh_transposed();
+    }
+    // pbfT <- transposes of the layer weights in pbf (after every SGD step): one launch per
+    // weight kind over all L layers (the layers of a kind are a constant stride apart)
+    void refresh_transposed() {
+        const int kinds[4] = {P_QKVW, P_ATTPROJW, P_FCW, P_FCPROJW};
+        const int rows[4] = {3 * C, C, 4 * C, C}, cols[4] = {C, C, C, 4 * C};
+        for (int k = 0; k < 4; k++) {
+            const long long stride = L > 1 ? off[kinds[k] * L + 1] - off[kinds[k] * L] : 0;
+            // negative stride: pass the lowest-addressed layer (layers are stored in reverse)
+            const int l0 = stride < 0 ? L - 1 : 0;
+            transpose_bf16(WT(kinds[k], l0), W(kinds[k], l0), rows[k], cols[k], L, stride < 0 ? -stride : stride, s);
+        }
     }
 
     // ------------------------------------------------------------------ head (both modes)
@@ -625,7 +648,7 @@ struct Trainer {
                 const long long r0 = mb * R;
                 after_wgrad(EV_W2, ms[mb]);  // the previous layer's fc wgrad has read dfch
                 GemmArgs d1;
-                d1.A = rbA + r0 * C; d1.lda = C; d1.B = W(P_FCPROJW, l); d1.ldb = 4 * C; d1.b_kcontig = false;
+                d1.A = rbA + r0 * C; d1.lda = C; d1.B = WT(P_FCPROJW, l); d1.ldb = C;
                 d1.C = dfch + r0 * 4 * C; d1.ldc = 4 * C; d1.aux = a.fch + r0 * 4 * C; d1.ldaux = 4 * C;
                 d1.M = (int)R; d1.N = 4 * C; d1.K = C; d1.epi = EPI_BF16_DGELU;
                 d1.colsum_out = G(P_FCB, l);
@@ -636,7 +659,7 @@ struct Trainer {
             for (int mb = 0; mb < nmb; mb++) {
                 const long long r0 = mb * R;
                 GemmArgs d2;
-                d2.A = dfch + r0 * 4 * C; d2.lda = 4 * C; d2.B = W(P_FCW, l); d2.ldb = C; d2.b_kcontig = false;
+                d2.A = dfch + r0 * 4 * C; d2.lda = 4 * C; d2.B = WT(P_FCW, l); d2.ldb = 4 * C;
                 d2.C = dln_bf + r0 * C; d2.ldc = C; d2.M = (int)R; d2.N = C; d2.K = 4 * C; d2.epi = EPI_BF16_STORE;
                 gemm(TC_FC_DGRAD, d2, true, ms[mb]);
                 // ln2 backward + residual: dres2 = dres3 + LN2'(dln2); attproj_b += colsum(dres2)
@@ -653,7 +676,7 @@ struct Trainer {
             for (int mb = 0; mb < nmb; mb++) {
                 const long long r0 = mb * R;
                 GemmArgs d3;
-                d3.A = rbB + r0 * C; d3.lda = C; d3.B = W(P_ATTPROJW, l); d3.ldb = C; d3.b_kcontig = false;
+                d3.A = rbB + r0 * C; d3.lda = C; d3.B = WT(P_ATTPROJW, l); d3.ldb = C;
                 d3.C = datty + r0 * C; d3.ldc = C; d3.M = (int)R; d3.N = C; d3.K = C; d3.epi = EPI_BF16_STORE;
                 gemm(TC_PROJ_DGRAD, d3, true, ms[mb]);
                 // attention (+ qkv_b)
@@ -669,7 +692,7 @@ struct Trainer {
             for (int mb = 0; mb < nmb; mb++) {
                 const long long r0 = mb * R;
                 GemmArgs d4;
-                d4.A = dqkv + r0 * 3 * C; d4.lda = 3 * C; d4.B = W(P_QKVW, l); d4.ldb = C; d4.b_kcontig = false;
+                d4.A = dqkv + r0 * 3 * C; d4.lda = 3 * C; d4.B = WT(P_QKVW, l); d4.ldb = 3 * C;
                 d4.C = dln_bf + r0 * C; d4.ldc = C; d4.M = (int)R; d4.N = C; d4.K = 3 * C; d4.epi = EPI_BF16_STORE;
                 gemm(TC_QKV_DGRAD, d4, true, ms[mb]);
                 // ln1 backward: dres = dres2 + LN1'(dln1); fcproj_b of layer l-1 += colsum(dres)
@@ -824,6 +847,7 @@ struct Trainer {
         if (prec == VIT_BF16) {
             sgd_bf16_k<<<grid_for(arena_elems / 4, 256), 256, 0, s>>>(params, pbf, grads, arena_elems, lr);
             after_launch("sgd_bf16");
+            refresh_transposed();
         } else {
             sgd(params, grads, arena_elems, lr, s);
         }
@@ -1009,7 +1033,7 @@ int vit_trainer_set_concurrency(vit_trainer_t* h, int on) {
     VIT_HIP(hipStreamSynchronize(t.s2));
     for (int k = 0; k < vit::Trainer::MAXMB; k++) if (t.ms[k]) VIT_HIP(hipStreamSynchronize(t.ms[k]));
     t.two_streams = on != 0;
-    t.nmb = (on && t.B % 2 == 0) ? 2 : 1;
+    t.nmb = t.pick_nmb(t.mb_want);
     return vit::has_error();
 }
 int vit_trainer_set_timing(vit_trainer_t* h, int on) {
