@@ -74,6 +74,11 @@ int vit_trainer_dp_init(vit_trainer_t* t, int rank, int world, const char* uniqu
  *      on two streams and the weight-gradient GEMMs on a third; off = one stream, kernels one at a
  *      time (per-kernel roofline timing).  Call between steps. ---- */
 int vit_trainer_set_concurrency(vit_trainer_t* t, int on);
+/* ---- tuning options for A/B measurements in one process (call between steps):
+ *      "microbatch" = number of micro-batch streams wanted (1 .. 4; the largest divisor of B),
+ *      "dgrad_transposed" = 1 (default): dgrad GEMMs read the transposed weight copy.
+ *      Returns non-zero (and sets the error) for an unknown name. ---- */
+int vit_trainer_set_option(vit_trainer_t* t, const char* name, int value);
 
 /* ---- per-kernel-class timing with HIP events on the stream each kernel runs on ---- */
 int vit_trainer_set_timing(vit_trainer_t* t, int on);

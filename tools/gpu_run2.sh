@@ -1,5 +1,4 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_model.py -x -q --timeout 120 --timeout-method thread > gpurun_out/t2.log 2>&1 &&
-timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/bench_wt.log 2>&1
+timeout -k 10 500 python -u tools/ab_step.py "dgrad_transposed=1|dgrad_transposed=0|microbatch=1|microbatch=2,concurrency=0|concurrency=1" --rounds 4 --steps 3 > gpurun_out/ab1.log 2>&1

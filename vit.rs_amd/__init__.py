@@ -97,6 +97,7 @@ _SIGS = {
     "vit_dp_unique_id_size": (I, []), "vit_dp_get_unique_id": (I, [ctypes.c_char_p]),
     "vit_trainer_dp_init": (I, [P, I, I, ctypes.c_char_p, I]),
     "vit_trainer_set_timing": (I, [P, I]), "vit_trainer_set_concurrency": (I, [P, I]),
+    "vit_trainer_set_option": (I, [P, ctypes.c_char_p, I]),
     "vit_trainer_timing": (I, [P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
                                ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double), I]),
 }
@@ -335,6 +336,9 @@ class ViT:
     # ---- stream concurrency (micro-batch streams + weight-gradient stream), on by default
     def set_concurrency(self, on=True):
         self._ok(lib().vit_trainer_set_concurrency(self.h, int(on)), "set_concurrency")
+
+    def set_option(self, name, value):
+        self._ok(lib().vit_trainer_set_option(self.h, name.encode(), int(value)), f"set_option {name}")
 
     # ---- per-kernel-class timing (HIP events on the stream each kernel runs on)
     def set_timing(self, on=True):

@@ -189,6 +189,12 @@ struct Trainer {
     bf16_t* W(int ti, int l = 0) const { return pbf + off[ti * L + l]; }
     // transposed bf16 copy of a layer weight ([Cin][OC]): the dgrad GEMMs read it K-contiguous
     bf16_t* WT(int ti, int l = 0) const { return pbfT + off[ti * L + l]; }
+    bool dgrad_wt = true;  // option "dgrad_transposed": dgrad B operand from pbfT (K-contig)
+    // dgrad B operand: the transposed copy (K-contiguous, ldb = OC) or W itself (N-contiguous)
+    void dgrad_b(GemmArgs& g, int ti, int l, int OC, int Cin) const {
+        if (dgrad_wt) { g.B = WT(ti, l); g.ldb = OC; g.b_kcontig = true; }
+        else { g.B = W(ti, l); g.ldb = Cin; g.b_kcontig = false; }
+    }
 
     void build_layout() {
         const long long C_ = C, K = KP;
@@ -648,7 +654,7 @@ struct Trainer {
                 const long long r0 = mb * R;
                 after_wgrad(EV_W2, ms[mb]);  // the previous layer's fc wgrad has read dfch
                 GemmArgs d1;
-                d1.A = rbA + r0 * C; d1.lda = C; d1.B = WT(P_FCPROJW, l); d1.ldb = C;
+                d1.A = rbA + r0 * C; d1.lda = C; dgrad_b(d1, P_FCPROJW, l, C, 4 * C);
                 d1.C = dfch + r0 * 4 * C; d1.ldc = 4 * C; d1.aux = a.fch + r0 * 4 * C; d1.ldaux = 4 * C;
                 d1.M = (int)R; d1.N = 4 * C; d1.K = C; d1.epi = EPI_BF16_DGELU;
                 d1.colsum_out = G(P_FCB, l);
@@ -659,7 +665,7 @@ struct Trainer {
             for (int mb = 0; mb < nmb; mb++) {
                 const long long r0 = mb * R;
                 GemmArgs d2;
-                d2.A = dfch + r0 * 4 * C; d2.lda = 4 * C; d2.B = WT(P_FCW, l); d2.ldb = 4 * C;
+                d2.A = dfch + r0 * 4 * C; d2.lda = 4 * C; dgrad_b(d2, P_FCW, l, 4 * C, C);
                 d2.C = dln_bf + r0 * C; d2.ldc = C; d2.M = (int)R; d2.N = C; d2.K = 4 * C; d2.epi = EPI_BF16_STORE;
                 gemm(TC_FC_DGRAD, d2, true, ms[mb]);
                 // ln2 backward + residual: dres2 = dres3 + LN2'(dln2); attproj_b += colsum(dres2)
@@ -676,7 +682,7 @@ struct Trainer {
             for (int mb = 0; mb < nmb; mb++) {
                 const long long r0 = mb * R;
                 GemmArgs d3;
-                d3.A = rbB + r0 * C; d3.lda = C; d3.B = WT(P_ATTPROJW, l); d3.ldb = C;
+                d3.A = rbB + r0 * C; d3.lda = C; dgrad_b(d3, P_ATTPROJW, l, C, C);
                 d3.C = datty + r0 * C; d3.ldc = C; d3.M = (int)R; d3.N = C; d3.K = C; d3.epi = EPI_BF16_STORE;
                 gemm(TC_PROJ_DGRAD, d3, true, ms[mb]);
                 // attention (+ qkv_b)
@@ -692,7 +698,7 @@ struct Trainer {
             for (int mb = 0; mb < nmb; mb++) {
                 const long long r0 = mb * R;
                 GemmArgs d4;
-                d4.A = dqkv + r0 * 3 * C; d4.lda = 3 * C; d4.B = WT(P_QKVW, l); d4.ldb = 3 * C;
+                d4.A = dqkv + r0 * 3 * C; d4.lda = 3 * C; dgrad_b(d4, P_QKVW, l, 3 * C, C);
                 d4.C = dln_bf + r0 * C; d4.ldc = C; d4.M = (int)R; d4.N = C; d4.K = 3 * C; d4.epi = EPI_BF16_STORE;
                 gemm(TC_QKV_DGRAD, d4, true, ms[mb]);
                 // ln1 backward: dres = dres2 + LN1'(dln1); fcproj_b of layer l-1 += colsum(dres)
@@ -1034,6 +1040,21 @@ int vit_trainer_set_concurrency(vit_trainer_t* h, int on) {
     for (int k = 0; k < vit::Trainer::MAXMB; k++) if (t.ms[k]) VIT_HIP(hipStreamSynchronize(t.ms[k]));
     t.two_streams = on != 0;
     t.nmb = t.pick_nmb(t.mb_want);
+    return vit::has_error();
+}
+int vit_trainer_set_option(vit_trainer_t* h, const char* name, int value) {
+    auto& t = h->t;
+    VIT_HIP(hipDeviceSynchronize());
+    const std::string n = name ? name : "";
+    if (n == "microbatch") {
+        t.mb_want = value;
+        t.nmb = t.pick_nmb(value);
+    } else if (n == "dgrad_transposed") {
+        t.dgrad_wt = value != 0;
+    } else {
+        set_error("vit_trainer_set_option: unknown option '%s'", n.c_str());
+        return 1;
+    }
     return vit::has_error();
 }
 int vit_trainer_set_timing(vit_trainer_t* h, int on) {
