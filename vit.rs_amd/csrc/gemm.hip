@@ -1211,13 +1211,16 @@ static GemmParams make_params(const GemmArgs& a, int kchunk) {
 
 // split-K for one-block-per-CU kernels: the smallest split whose last wave of blocks fills
 // >= 90% of the 256 CUs (or the best fill up to 32), keeping >= 16 K-tiles per split
+// slots: the CUs the launch may fill (256; fewer when it shares the GPU with other streams, debug
+// flag 8 / 16: a half / a quarter)
 static int choose_split_waves(int tiles, int nk) {
+    const int slots = (g_debug_flags & 16) ? 64 : ((g_debug_flags & 8) ? 128 : 256);
     int best = 1;
     double best_eff = 0.0;
     for (int s = 1; s <= 32 && nk / s >= 16; s++) {
         const int blocks = tiles * s;
-        const int waves = (blocks + 255) / 256;
-        const double eff = (double)blocks / (waves * 256.0) * (blocks >= 128 ? 1.0 : blocks / 128.0);
+        const int waves = (blocks + slots - 1) / slots;
+        const double eff = (double)blocks / (waves * (double)slots) * (blocks >= slots / 2 ? 1.0 : blocks / (slots / 2.0));
         if (eff > best_eff + 1e-9) { best_eff = eff; best = s; }
         if (eff >= 0.9) break;
     }
