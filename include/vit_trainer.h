@@ -46,7 +46,9 @@ long long vit_trainer_device_bytes(const vit_trainer_t* t);
 int vit_trainer_set_params(vit_trainer_t* t, const float* host_params);
 int vit_trainer_get_params(vit_trainer_t* t, float* host_params);
 int vit_trainer_get_grads(vit_trainer_t* t, float* host_grads);
-/* pixels [batch,3,img,img] fp32, labels [batch] int32 (host); synchronous upload */
+/* pixels [batch,3,img,img] fp32, labels [batch] int32 (host); synchronous upload.
+ * labels NULL = a forward-only batch (the reference's targets == null branch, train_vit.rs:
+ * 254-266): no loss, vit_trainer_mean_loss returns -1, vit_trainer_backward fails */
 int vit_trainer_set_batch(vit_trainer_t* t, const float* host_pixels, const int* host_labels);
 /* same from device pointers (stream-ordered device copy) */
 int vit_trainer_set_batch_device(vit_trainer_t* t, const float* dev_pixels, const int* dev_labels);
@@ -55,9 +57,23 @@ int vit_trainer_forward(vit_trainer_t* t, int b_global);
 int vit_trainer_zero_grad(vit_trainer_t* t);
 int vit_trainer_backward(vit_trainer_t* t);   /* also launches the overlapped all-reduce (DP) */
 int vit_trainer_step(vit_trainer_t* t, float lr); /* waits for the all-reduce, then SGD */
+/* AdamW: the update the reference's m_memory / v_memory (train_vit.rs:73-74)
+ * were allocated for, which its SGD optimizer_step (:737) never runs.  t = number of AdamW steps
+ * so far + 1 (kept by the trainer, saved in checkpoints); m, v are allocated and zeroed on the
+ * first call.  Decoupled weight decay on every parameter:
+ *   m = b1 m + (1-b1) g;  v = b2 v + (1-b2) g g;  p -= lr (m/(1-b1^t) / (sqrt(v/(1-b2^t)) + eps) + wd p) */
+int vit_trainer_step_adamw(vit_trainer_t* t, float lr, float beta1, float beta2, float eps,
+                           float weight_decay);
+/* canonical host copies of m, v (either may be NULL) and the step count; synchronous */
+int vit_trainer_get_adamw_state(vit_trainer_t* t, float* m, float* v, int* step);
+/* eval: forward of the current batch, then top-1 per image on the device.
+ * host_pred [batch] (nullable) gets the predicted classes (first maximum, as numpy.argmax);
+ * host_correct (nullable) gets the number equal to the labels, or -1 when the batch was set
+ * without labels.  Synchronous. */
+int vit_trainer_eval(vit_trainer_t* t, int* host_pred, int* host_correct);
 /* zero_grad + forward + backward + step */
 int vit_trainer_train_step(vit_trainer_t* t, float lr, int b_global);
-/* synchronous readbacks */
+/* synchronous readbacks; mean_loss = -1 for a batch without labels */
 float vit_trainer_mean_loss(vit_trainer_t* t);
 int vit_trainer_get_logits(vit_trainer_t* t, float* host_logits); /* [batch, num_classes] */
 int vit_trainer_sync(vit_trainer_t* t);

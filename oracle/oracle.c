@@ -385,6 +385,25 @@ void ref_sgd_step(real* params, const real* grads, long long n, real lr) {
     for (i64 i = 0; i < n; i++) params[i] -= lr * grads[i];
 }
 
+/* AdamW over the flat arena: the reference allocates m_memory / v_memory
+ * (train_vit.rs:73-74, rusty_vit.rs:225-226) but its optimizer_step (train_vit.rs:737-743) is
+ * plain SGD; this is the llm.c AdamW those buffers belong to, t = 1-based step.  Each line rounds
+ * like the HIP kernel (no contraction): m, v, bias corrections, update with decoupled decay. */
+void ref_adamw_step(real* params, const real* grads, real* m, real* v, long long n, real lr,
+                    real beta1, real beta2, real eps, real weight_decay, int t) {
+    const real bc1 = (real)1 - (real)pow((double)beta1, (double)t);
+    const real bc2 = (real)1 - (real)pow((double)beta2, (double)t);
+    for (i64 i = 0; i < n; i++) {
+        const real g = grads[i];
+        const real mi = beta1 * m[i] + ((real)1 - beta1) * g;
+        const real vi = beta2 * v[i] + ((real)1 - beta2) * g * g;
+        m[i] = mi;
+        v[i] = vi;
+        const real mh = mi / bc1, vh = vi / bc2;
+        params[i] -= lr * (mh / (R_SQRT(vh) + eps) + weight_decay * params[i]);
+    }
+}
+
 /* ------------------------------- model ------------------------------- */
 
 long long ref_vit_param_sizes(const VitConfig* cfg, long long s[VIT_NUM_PARAM_TENSORS]) {

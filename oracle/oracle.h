@@ -74,6 +74,8 @@ void ref_patch_embed_backward(real* dpatch_w, real* dpatch_b, real* dcls, real* 
                               int B, int IMG, int P, int C);
 /* optimizer_step (train_vit.rs:737-743): p -= lr * g */
 void ref_sgd_step(real* params, const real* grads, long long n, real lr);
+void ref_adamw_step(real* params, const real* grads, real* m, real* v, long long n, real lr,
+                    real beta1, real beta2, real eps, real weight_decay, int t);
 
 /* ---- model level (train_vit.rs:9-86 structs, :188-373 forward/backward) ---- */
 typedef struct {

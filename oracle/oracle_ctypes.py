@@ -55,6 +55,7 @@ class Oracle:
         L.ref_vit_param_sizes.restype = ctypes.c_longlong
         L.ref_vit_param_sizes.argtypes = [ctypes.POINTER(VitConfig), P]
         L.ref_sgd_step.argtypes = [P, P, ctypes.c_longlong, self.ctype]
+        L.ref_adamw_step.argtypes = [P, P, P, P, ctypes.c_longlong] + [self.ctype] * 5 + [ctypes.c_int]
 
     # -- helpers --------------------------------------------------------------------------
     def _p(self, a):
@@ -87,6 +88,10 @@ class Oracle:
 
     def sgd_step(self, params, grads, lr):
         self.lib.ref_sgd_step(self._p(params), self._p(grads), params.size, self.ctype(lr))
+
+    def adamw_step(self, params, grads, m, v, lr, beta1, beta2, eps, wd, t):
+        self.lib.ref_adamw_step(self._p(params), self._p(grads), self._p(m), self._p(v), params.size,
+                                *(self.ctype(x) for x in (lr, beta1, beta2, eps, wd)), int(t))
 
 
 class RefViT:

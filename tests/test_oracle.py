@@ -259,3 +259,63 @@ def test_sgd_step(oracle32):
     p, g = o.arr(np.arange(5.0)), o.arr(np.ones(5))
     o.sgd_step(p, g, 0.5)
     assert np.allclose(p, np.arange(5.0) - 0.5)
+
+
+def _adamw_np(p, g, m, v, lr, b1, b2, eps, wd, t, dt):
+    """The AdamW formula (oracle.c ref_adamw_step) restated in numpy at dtype dt, line by line."""
+    one = dt(1)
+    b1, b2, lr, eps, wd = dt(b1), dt(b2), dt(lr), dt(eps), dt(wd)
+    bc1 = one - dt(np.float64(b1) ** t)
+    bc2 = one - dt(np.float64(b2) ** t)
+    m[:] = b1 * m + (one - b1) * g
+    v[:] = b2 * v + (one - b2) * g * g
+    p[:] = p - lr * ((m / bc1) / (np.sqrt(v / bc2) + eps) + wd * p)
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_adamw_step_matches_numpy(prec, oracle32, oracle64):
+    """f32: bit-exact against numpy's fp32 evaluation of the same expression order."""
+    o = oracle32 if prec == "f32" else oracle64
+    dt = np.float32 if prec == "f32" else np.float64
+    rng = np.random.default_rng(5)
+    n = 4099
+    p = o.arr(rng.standard_normal(n)); m = o.arr(np.zeros(n)); v = o.arr(np.zeros(n))
+    pr, mr, vr = p.copy(), m.copy(), v.copy()
+    for t in (1, 2, 3):
+        g = o.arr(rng.standard_normal(n) * 1e-2)
+        o.adamw_step(p, g, m, v, 1e-3, 0.9, 0.999, 1e-8, 0.01, t)
+        _adamw_np(pr, g, mr, vr, 1e-3, 0.9, 0.999, 1e-8, 0.01, t, dt)
+    if prec == "f32":
+        assert np.array_equal(p, pr) and np.array_equal(m, mr) and np.array_equal(v, vr)
+    else:
+        assert np.allclose(p, pr, rtol=1e-14, atol=0)
+
+
+def test_adamw_matches_torch_adamw(oracle64, tmp_path):
+    """Pin against a published AdamW: torch.optim.AdamW (decoupled decay) in float64.  torch runs
+    in a child process: loaded after libvit_hip.so it would bring a second HIP runtime into this
+    one (the package must be imported after torch)."""
+    import subprocess
+    import sys
+    o = oracle64
+    rng = np.random.default_rng(6)
+    n, steps = 1000, 5
+    p0 = rng.standard_normal(n)
+    gs = rng.standard_normal((steps, n))
+    np.save(tmp_path / "in.npy", np.concatenate([p0[None], gs]))
+    script = (
+        "import sys, numpy as np, torch\n"
+        "a = np.load(sys.argv[1]); p = torch.tensor(a[0], dtype=torch.float64, requires_grad=True)\n"
+        "opt = torch.optim.AdamW([p], lr=1e-2, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)\n"
+        "for g in a[1:]:\n"
+        "    p.grad = torch.tensor(g, dtype=torch.float64); opt.step()\n"
+        "np.save(sys.argv[2], p.detach().numpy())\n")
+    r = subprocess.run([sys.executable, "-c", script, str(tmp_path / "in.npy"), str(tmp_path / "out.npy")],
+                       capture_output=True, text=True, timeout=300)
+    if r.returncode != 0 and "No module named 'torch'" in r.stderr:
+        pytest.skip("torch not importable")
+    assert r.returncode == 0, r.stderr[-2000:]
+    p = o.arr(p0); m = o.arr(np.zeros(n)); v = o.arr(np.zeros(n))
+    for t in range(1, steps + 1):
+        o.adamw_step(p, o.arr(gs[t - 1]), m, v, 1e-2, 0.9, 0.95, 1e-8, 0.1, t)
+    assert np.allclose(p, np.load(tmp_path / "out.npy"), rtol=1e-12, atol=1e-14)

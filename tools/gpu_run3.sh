@@ -1,5 +1,4 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/tl -o run -- python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-timing > gpurun_out/tl.log 2>&1
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_gpu_next.py > gpurun_out/next.log 2>&1

@@ -35,6 +35,21 @@ class VitConfigC(ctypes.Structure):
                 ("num_heads", ctypes.c_int), ("num_classes", ctypes.c_int)]
 
 
+class AdamWC(ctypes.Structure):
+    _fields_ = [("beta1", ctypes.c_float), ("beta2", ctypes.c_float), ("eps", ctypes.c_float),
+                ("weight_decay", ctypes.c_float)]
+
+
+class CheckpointInfoC(ctypes.Structure):
+    _fields_ = [("cfg", VitConfigC), ("num_params", ctypes.c_longlong), ("has_opt", ctypes.c_int),
+                ("step", ctypes.c_int), ("adamw", AdamWC)]
+
+
+def _cfg_c(cfg):
+    return VitConfigC(cfg.img, cfg.patch, cfg.in_ch, cfg.channels, cfg.num_layers, cfg.num_heads,
+                      cfg.num_classes)
+
+
 def build(quiet=True):
     """Compile libvit_hip.so in place (hipcc, gfx950)."""
     import subprocess
@@ -100,6 +115,16 @@ _SIGS = {
     "vit_trainer_set_option": (I, [P, ctypes.c_char_p, I]),
     "vit_trainer_timing": (I, [P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
                                ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double), I]),
+    "vit_trainer_step_adamw": (I, [P, F, F, F, F, F]),
+    "vit_trainer_get_adamw_state": (I, [P, P, P, ctypes.POINTER(I)]),
+    "vit_trainer_eval": (I, [P, P, ctypes.POINTER(I)]),
+    # checkpoints (include/vit_checkpoint.h; host-only)
+    "vit_config_num_params": (LL, [ctypes.POINTER(VitConfigC)]),
+    "vit_checkpoint_read_info": (I, [ctypes.c_char_p, P]),
+    "vit_checkpoint_write": (I, [ctypes.c_char_p, ctypes.POINTER(VitConfigC), P, P, P, I, P]),
+    "vit_checkpoint_read": (I, [ctypes.c_char_p, ctypes.POINTER(VitConfigC), P, P, P]),
+    "vit_trainer_save_checkpoint": (I, [P, ctypes.c_char_p]),
+    "vit_trainer_load_checkpoint": (I, [P, ctypes.c_char_p]),
 }
 
 
@@ -216,6 +241,54 @@ def call(name, *args):
     check(name)
 
 
+# --------------------------------------------------------------------------- checkpoints
+def checkpoint_info(path):
+    """Header of a checkpoint file (include/vit_checkpoint.h) as a dict; host-only."""
+    info = CheckpointInfoC()
+    if lib().vit_checkpoint_read_info(os.fsencode(path), ctypes.byref(info)):
+        check("checkpoint_info")
+    c = info.cfg
+    cfg = data.VitCfg("checkpoint", c.img, c.patch, c.channels, c.num_layers, c.num_heads,
+                      c.num_classes, c.in_ch)
+    return {"cfg": cfg, "num_params": int(info.num_params), "has_opt": bool(info.has_opt),
+            "step": int(info.step),
+            "adamw": (info.adamw.beta1, info.adamw.beta2, info.adamw.eps, info.adamw.weight_decay)}
+
+
+def write_checkpoint(path, cfg, params, m=None, v=None, step=0, adamw=None):
+    """Write canonical fp32 params (+ AdamW m, v) in the checkpoint format; host-only."""
+    params = np.ascontiguousarray(params, dtype=np.float32)
+    assert params.size == cfg.num_params()
+    ptrs = [params.ctypes.data_as(P)]
+    keep = []
+    for a in (m, v):
+        if a is None:
+            ptrs.append(None)
+        else:
+            a = np.ascontiguousarray(a, dtype=np.float32)
+            assert a.size == params.size
+            keep.append(a)
+            ptrs.append(a.ctypes.data_as(P))
+    hp = AdamWC(*adamw) if adamw is not None else None
+    if lib().vit_checkpoint_write(os.fsencode(path), ctypes.byref(_cfg_c(cfg)), *ptrs, int(step),
+                                  ctypes.byref(hp) if hp is not None else None):
+        check("write_checkpoint")
+
+
+def read_checkpoint(path, cfg):
+    """(params, m, v) of a checkpoint written for cfg; m, v None without optimizer state."""
+    info = checkpoint_info(path)
+    n = cfg.num_params()
+    p = np.empty(n, np.float32)
+    m = np.empty(n, np.float32) if info["has_opt"] else None
+    v = np.empty(n, np.float32) if info["has_opt"] else None
+    if lib().vit_checkpoint_read(os.fsencode(path), ctypes.byref(_cfg_c(cfg)), p.ctypes.data_as(P),
+                                 m.ctypes.data_as(P) if m is not None else None,
+                                 v.ctypes.data_as(P) if v is not None else None):
+        check("read_checkpoint")
+    return p, m, v
+
+
 # --------------------------------------------------------------------------- model
 class ViT:
     """Mirror of the reference's `struct ViT` (train_vit.rs:65-86) over the native trainer.
@@ -280,10 +353,15 @@ class ViT:
         return out
 
     def set_batch(self, pixels, labels):
+        """labels None = a forward-only batch (train_vit.rs:254-266: mean_loss = -1)."""
         px = np.ascontiguousarray(pixels, dtype=np.float32)
-        lb = np.ascontiguousarray(labels, dtype=np.int32)
-        assert px.shape == (self.B, 3, self.cfg.img, self.cfg.img) and lb.shape == (self.B,)
-        self._ok(lib().vit_trainer_set_batch(self.h, px.ctypes.data_as(P), lb.ctypes.data_as(P)),
+        assert px.shape == (self.B, 3, self.cfg.img, self.cfg.img)
+        lb = None
+        if labels is not None:
+            lb = np.ascontiguousarray(labels, dtype=np.int32)
+            assert lb.shape == (self.B,)
+        self._ok(lib().vit_trainer_set_batch(self.h, px.ctypes.data_as(P),
+                                             lb.ctypes.data_as(P) if lb is not None else None),
                  "set_batch")
 
     def forward(self, pixels=None, targets=None, b_global=None):
@@ -305,6 +383,35 @@ class ViT:
 
     def optimizer_step(self, lr):
         self._ok(lib().vit_trainer_step(self.h, float(lr)), "optimizer_step")
+
+    def optimizer_step_adamw(self, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0):
+        """AdamW (vit_trainer_step_adamw)."""
+        self._ok(lib().vit_trainer_step_adamw(self.h, float(lr), float(beta1), float(beta2),
+                                              float(eps), float(weight_decay)), "step_adamw")
+
+    def adamw_state(self):
+        """(m, v, t) in canonical order."""
+        m = np.empty(self.num_parameters, np.float32)
+        v = np.empty(self.num_parameters, np.float32)
+        t = ctypes.c_int()
+        self._ok(lib().vit_trainer_get_adamw_state(self.h, m.ctypes.data_as(P), v.ctypes.data_as(P),
+                                                   ctypes.byref(t)), "get_adamw_state")
+        return m, v, t.value
+
+    def evaluate(self, pixels=None, labels=None):
+        """Forward + device top-1: (predictions [B], number correct or -1 without labels)."""
+        if pixels is not None:
+            self.set_batch(pixels, labels)
+        pred = np.empty(self.B, np.int32)
+        correct = ctypes.c_int()
+        self._ok(lib().vit_trainer_eval(self.h, pred.ctypes.data_as(P), ctypes.byref(correct)), "eval")
+        return pred, correct.value
+
+    def save_checkpoint(self, path):
+        self._ok(lib().vit_trainer_save_checkpoint(self.h, os.fsencode(path)), "save_checkpoint")
+
+    def load_checkpoint(self, path):
+        self._ok(lib().vit_trainer_load_checkpoint(self.h, os.fsencode(path)), "load_checkpoint")
 
     def train_step(self, lr, b_global=None):
         self._ok(lib().vit_trainer_train_step(self.h, float(lr), int(b_global or self.B)),

@@ -99,6 +99,24 @@ __device__ __forceinline__ float sgd_update(float p, float g, float lr) {
     return p - lr * g;
 }
 
+// AdamW (oracle ref_adamw_step): one element, every operation rounded like the
+// oracle's line-by-line C (no contraction, correctly rounded sqrt / divide).  omb1 = 1-beta1, omb2 = 1-beta2,
+// bc1/bc2 = the bias corrections 1 - beta^t, computed on the host exactly as the oracle does.
+__device__ __forceinline__ float adamw_update(float p, float g, float& m, float& v, float lr,
+                                              float b1, float b2, float omb1, float omb2,
+                                              float bc1, float bc2, float eps, float wd) {
+#pragma clang fp contract(off)
+    const float mi = b1 * m + omb1 * g;
+    const float vi = b2 * v + omb2 * g * g;
+    m = mi;
+    v = vi;
+    // '/' and __builtin_sqrtf are IEEE-rounded under hipcc's default
+    // -fhip-fp32-correctly-rounded-divide-sqrt; __fsqrt_rn is NOT (it maps to the native,
+    // approximate v_sqrt unless OCML_BASIC_ROUNDED_OPERATIONS is defined)
+    const float mh = mi / bc1, vh = vi / bc2;
+    return p - lr * (mh / (__builtin_sqrtf(vh) + eps) + wd * p);
+}
+
 // XCD-aware bijective remap of a linear workgroup id (cdna_hip_programming.md §5, "XCD swizzle
 // must be bijective"): blocks dealt round-robin over 8 XCDs get contiguous tile ranges per XCD.
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {

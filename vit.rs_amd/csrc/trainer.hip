@@ -11,6 +11,7 @@
 //   * optional per-kernel-class HIP-event timing on the compute stream.
 #include <rccl/rccl.h>
 
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -18,6 +19,7 @@
 
 #include "ops_internal.h"
 #include "../../include/vit_trainer.h"
+#include "../../include/vit_checkpoint.h"
 
 namespace vit {
 namespace {
@@ -61,6 +63,59 @@ __global__ void sgd_bf16_k(float* __restrict__ p, bf16_t* __restrict__ pbf,
          i += (long long)gridDim.x * blockDim.x) {
         p[i] = sgd_update(p[i], g[i], lr);
         pbf[i] = f2bf(p[i]);
+    }
+}
+// AdamW over the whole arena (oracle ref_adamw_step), + the bf16 shadow.  One
+// pass: reads p, g, m, v and writes p, m, v (+ pbf) = 7 x 4 B (+2 B) per parameter, HBM-bound.
+__global__ void adamw_k(float* __restrict__ p, bf16_t* __restrict__ pbf, const float* __restrict__ g,
+                        float* __restrict__ m, float* __restrict__ v, long long n, float lr, float b1,
+                        float b2, float omb1, float omb2, float bc1, float bc2, float eps, float wd) {
+    const long long n4 = n / 4;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4;
+         i += (long long)gridDim.x * blockDim.x) {
+        float4 pv = reinterpret_cast<float4*>(p)[i];
+        const float4 gv = reinterpret_cast<const float4*>(g)[i];
+        float4 mv = reinterpret_cast<float4*>(m)[i];
+        float4 vv = reinterpret_cast<float4*>(v)[i];
+        pv.x = adamw_update(pv.x, gv.x, mv.x, vv.x, lr, b1, b2, omb1, omb2, bc1, bc2, eps, wd);
+        pv.y = adamw_update(pv.y, gv.y, mv.y, vv.y, lr, b1, b2, omb1, omb2, bc1, bc2, eps, wd);
+        pv.z = adamw_update(pv.z, gv.z, mv.z, vv.z, lr, b1, b2, omb1, omb2, bc1, bc2, eps, wd);
+        pv.w = adamw_update(pv.w, gv.w, mv.w, vv.w, lr, b1, b2, omb1, omb2, bc1, bc2, eps, wd);
+        reinterpret_cast<float4*>(p)[i] = pv;
+        reinterpret_cast<float4*>(m)[i] = mv;
+        reinterpret_cast<float4*>(v)[i] = vv;
+        if (pbf)
+            reinterpret_cast<uint2*>(pbf)[i] = make_uint2(pack_bf16x2(pv.x, pv.y), pack_bf16x2(pv.z, pv.w));
+    }
+    for (long long i = n4 * 4 + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x) {
+        p[i] = adamw_update(p[i], g[i], m[i], v[i], lr, b1, b2, omb1, omb2, bc1, bc2, eps, wd);
+        if (pbf) pbf[i] = f2bf(p[i]);
+    }
+}
+// top-1 of each logits row (first index among equal maxima, as numpy.argmax) and the count of
+// rows whose prediction equals the label (eval path).  One wave per row.
+__global__ void argmax_rows_k(int* __restrict__ pred, int* __restrict__ correct,
+                              const float* __restrict__ logits, const int* __restrict__ labels,
+                              int B, int NC) {
+    const int row = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64, lane = threadIdx.x & 63;
+    if (row >= B) return;
+    const float* x = logits + (long long)row * NC;
+    float best = -INFINITY;
+    int bi = NC;  // sentinel above every real index
+    for (int j = lane; j < NC; j += 64) {
+        const float xv = x[j];
+        if (xv > best || bi == NC) { best = xv; bi = j; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float ob = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (oi < NC && (bi == NC || ob > best || (ob == best && oi < bi))) { best = ob; bi = oi; }
+    }
+    if (lane == 0) {
+        pred[row] = bi;
+        if (labels && bi == labels[row]) atomicAdd(correct, 1);
     }
 }
 __global__ void to_bf16_k(bf16_t* __restrict__ out, const float* __restrict__ in, long long n) {
@@ -123,6 +178,12 @@ struct Trainer {
     bf16_t* pbfT = nullptr;  // same offsets as pbf; only the four layer weight tensors are used
     float* pixels = nullptr;
     int* labels = nullptr;
+    bool has_targets = true;  // false after set_batch without labels: forward only (:264-266)
+    int* preds = nullptr;     // eval: [B] top-1 + one counter
+    // AdamW state (allocated on the first AdamW step / a checkpoint load with optimizer state)
+    float *adam_m = nullptr, *adam_v = nullptr;
+    int adam_t = 0;
+    vit_adamw_t adam_hp{};
     std::vector<DevBuf> allocs;
     size_t dev_bytes = 0;
     int b_global = 0;
@@ -364,6 +425,7 @@ struct Trainer {
         grads = alloc<float>(arena_elems);
         pixels = alloc<float>((long long)B * 3 * c->img * c->img);
         labels = alloc<int>(B);
+        preds = alloc<int>(B + 1);
         encoded = alloc<float>(BT * C);
         cls_x = alloc<float>((long long)B * C);
         lnf = alloc<float>((long long)B * C);
@@ -511,7 +573,7 @@ struct Trainer {
         a.bias = P(P_HEADB); a.M = B; a.N = NC; a.K = C; a.epi = EPI_F32_STORE;
         gemm_f32(a, s);
         softmax_rows(probs, logits, B, NC, s);
-        ce_forward(losses, probs, labels, B, NC, s);
+        if (has_targets) ce_forward(losses, probs, labels, B, NC, s);
         tend();
     }
     // dres_cur (zeroed) <- lnf backward on CLS rows
@@ -847,6 +909,34 @@ struct Trainer {
         VIT_HIP(hipStreamWaitEvent(s, comm_done, 0));
     }
 
+    bool ensure_adam() {
+        if (adam_m) return true;
+        adam_m = alloc<float>(arena_elems);
+        adam_v = alloc<float>(arena_elems);
+        if (!adam_m || !adam_v) return false;
+        VIT_HIP(hipMemsetAsync(adam_m, 0, arena_elems * 4, s));
+        VIT_HIP(hipMemsetAsync(adam_v, 0, arena_elems * 4, s));
+        return true;
+    }
+    // AdamW update t = adam_t + 1 (llm.c's update, which the reference's m/v buffers —
+    // train_vit.rs:73-74 — were allocated for; its optimizer_step :737 is SGD)
+    void step_adamw(float lr, const vit_adamw_t& hp) {
+        finish_allreduce();
+        if (!ensure_adam()) return;
+        adam_t += 1;
+        adam_hp = hp;
+        // bias corrections and 1-beta exactly as the oracle rounds them (pow in double -> fp32)
+        const float bc1 = 1.0f - (float)pow((double)hp.beta1, (double)adam_t);
+        const float bc2 = 1.0f - (float)pow((double)hp.beta2, (double)adam_t);
+        tbeg(TC_SGD, 0);
+        adamw_k<<<grid_for(arena_elems / 4, 256), 256, 0, s>>>(
+            params, prec == VIT_BF16 ? pbf : nullptr, grads, adam_m, adam_v, arena_elems, lr,
+            hp.beta1, hp.beta2, 1.0f - hp.beta1, 1.0f - hp.beta2, bc1, bc2, hp.eps, hp.weight_decay);
+        after_launch("adamw");
+        if (prec == VIT_BF16) refresh_transposed();
+        tend();
+    }
+
     void step(float lr) {
         finish_allreduce();
         tbeg(TC_SGD, 0);
@@ -939,14 +1029,16 @@ int vit_trainer_get_grads(vit_trainer_t* h, float* hg) {
 int vit_trainer_set_batch(vit_trainer_t* h, const float* px, const int* lab) {
     auto& t = h->t;
     VIT_HIP(hipMemcpyAsync(t.pixels, px, (size_t)t.B * 3 * t.cfg.img * t.cfg.img * 4, hipMemcpyHostToDevice, t.s));
-    VIT_HIP(hipMemcpyAsync(t.labels, lab, (size_t)t.B * 4, hipMemcpyHostToDevice, t.s));
+    t.has_targets = lab != nullptr;
+    if (lab) VIT_HIP(hipMemcpyAsync(t.labels, lab, (size_t)t.B * 4, hipMemcpyHostToDevice, t.s));
     VIT_HIP(hipStreamSynchronize(t.s));
     return vit::has_error();
 }
 int vit_trainer_set_batch_device(vit_trainer_t* h, const float* px, const int* lab) {
     auto& t = h->t;
     VIT_HIP(hipMemcpyAsync(t.pixels, px, (size_t)t.B * 3 * t.cfg.img * t.cfg.img * 4, hipMemcpyDeviceToDevice, t.s));
-    VIT_HIP(hipMemcpyAsync(t.labels, lab, (size_t)t.B * 4, hipMemcpyDeviceToDevice, t.s));
+    t.has_targets = lab != nullptr;
+    if (lab) VIT_HIP(hipMemcpyAsync(t.labels, lab, (size_t)t.B * 4, hipMemcpyDeviceToDevice, t.s));
     return vit::has_error();
 }
 int vit_trainer_forward(vit_trainer_t* h, int b_global) {
@@ -967,6 +1059,10 @@ int vit_trainer_zero_grad(vit_trainer_t* h) {
 }
 int vit_trainer_backward(vit_trainer_t* h) {
     auto& t = h->t;
+    if (!t.has_targets) {
+        set_error("vit_trainer_backward: the batch has no targets (forward-only batch)");
+        return 1;
+    }
     if (t.prec == VIT_BF16) t.backward_bf16(); else t.backward_f32();
     return vit::has_error();
 }
@@ -981,8 +1077,88 @@ int vit_trainer_train_step(vit_trainer_t* h, float lr, int b_global) {
     vit_trainer_step(h, lr);
     return vit::has_error();
 }
+int vit_trainer_step_adamw(vit_trainer_t* h, float lr, float beta1, float beta2, float eps,
+                           float weight_decay) {
+    h->t.step_adamw(lr, vit_adamw_t{beta1, beta2, eps, weight_decay});
+    return vit::has_error();
+}
+int vit_trainer_get_adamw_state(vit_trainer_t* h, float* m, float* v, int* step) {
+    auto& t = h->t;
+    if (step) *step = t.adam_t;
+    if (!t.adam_m) {
+        set_error("vit_trainer_get_adamw_state: no AdamW step has run");
+        return 1;
+    }
+    VIT_HIP(hipDeviceSynchronize());
+    if (m) t.device_to_canon(t.adam_m, m);
+    if (v) t.device_to_canon(t.adam_v, v);
+    return vit::has_error();
+}
+int vit_trainer_eval(vit_trainer_t* h, int* host_pred, int* host_correct) {
+    auto& t = h->t;
+    if (host_correct) *host_correct = -1;
+    t.b_global = t.B;
+    if (t.prec == VIT_BF16) t.forward_bf16(); else t.forward_f32();
+    VIT_HIP(hipMemsetAsync(t.preds + t.B, 0, 4, t.s));
+    vit::argmax_rows_k<<<cdiv(t.B, 4), 256, 0, t.s>>>(t.preds, t.preds + t.B, t.logits,
+                                                 t.has_targets ? t.labels : nullptr, t.B, t.NC);
+    vit::after_launch("argmax_rows");
+    std::vector<int> out(t.B + 1);
+    VIT_HIP(hipMemcpyAsync(out.data(), t.preds, (size_t)(t.B + 1) * 4, hipMemcpyDeviceToHost, t.s));
+    VIT_HIP(hipStreamSynchronize(t.s));
+    if (vit::has_error()) return 1;
+    if (host_pred) memcpy(host_pred, out.data(), (size_t)t.B * 4);
+    if (host_correct && t.has_targets) *host_correct = out[t.B];
+    return 0;
+}
+int vit_trainer_save_checkpoint(vit_trainer_t* h, const char* path) {
+    auto& t = h->t;
+    VIT_HIP(hipDeviceSynchronize());
+    if (vit::has_error()) return 1;
+    std::vector<float> p((size_t)t.n_params), m, v;
+    t.device_to_canon(t.params, p.data());
+    if (t.adam_m) {
+        m.resize((size_t)t.n_params);
+        v.resize((size_t)t.n_params);
+        t.device_to_canon(t.adam_m, m.data());
+        t.device_to_canon(t.adam_v, v.data());
+    }
+    if (vit::has_error()) return 1;
+    return vit_checkpoint_write(path, &t.cfg, p.data(), t.adam_m ? m.data() : nullptr,
+                                t.adam_m ? v.data() : nullptr, t.adam_t, &t.adam_hp);
+}
+int vit_trainer_load_checkpoint(vit_trainer_t* h, const char* path) {
+    auto& t = h->t;
+    vit_checkpoint_info_t info;
+    if (vit_checkpoint_read_info(path, &info)) return 1;
+    std::vector<float> p((size_t)t.n_params), m, v;
+    if (info.has_opt) {
+        m.resize((size_t)t.n_params);
+        v.resize((size_t)t.n_params);
+    }
+    if (vit_checkpoint_read(path, &t.cfg, p.data(), info.has_opt ? m.data() : nullptr,
+                            info.has_opt ? v.data() : nullptr))
+        return 1;
+    VIT_HIP(hipDeviceSynchronize());
+    t.canon_to_device(p.data(), t.params);
+    t.refresh_bf16();
+    if (info.has_opt) {
+        if (!t.ensure_adam()) return 1;
+        t.canon_to_device(m.data(), t.adam_m);
+        t.canon_to_device(v.data(), t.adam_v);
+        t.adam_t = info.step;
+        t.adam_hp = info.adamw;
+    } else if (t.adam_m) {  // a parameters-only file restarts the optimizer
+        VIT_HIP(hipMemsetAsync(t.adam_m, 0, t.arena_elems * 4, t.s));
+        VIT_HIP(hipMemsetAsync(t.adam_v, 0, t.arena_elems * 4, t.s));
+        t.adam_t = 0;
+    }
+    VIT_HIP(hipStreamSynchronize(t.s));
+    return vit::has_error();
+}
 float vit_trainer_mean_loss(vit_trainer_t* h) {
     auto& t = h->t;
+    if (!t.has_targets) return -1.0f;  // train_vit.rs:264-266
     std::vector<float> l(t.B);
     VIT_HIP(hipMemcpyAsync(l.data(), t.losses, t.B * 4, hipMemcpyDeviceToHost, t.s));
     VIT_HIP(hipStreamSynchronize(t.s));
