@@ -132,3 +132,35 @@ def test_checkpoint_resume(gpu, tmp_path):
     b.load_checkpoint(tmp_path / "p.bin")
     assert np.array_equal(b.params(), params)
     a.close(); b.close()
+
+
+@pytest.mark.parametrize("prec_name", ["fp32", "bf16"])
+def test_u8_input_pipeline_matches_host_normalisation(gpu, tmp_path, prec_name):
+    """Loader (pinned ring) -> vit_trainer_set_batch_u8 (async upload + device normalise) gives
+    the same logits / loss as uploading the numpy-normalised fp32 batch (bit-identical pixels)."""
+    v = gpu
+    cfg = v.data.CONFIGS["test_h64"]
+    prec = v.VIT_FP32 if prec_name == "fp32" else v.VIT_BF16
+    B, n = 4, 19
+    rng = np.random.default_rng(3)
+    imgs = rng.integers(0, 256, size=(n, cfg.img, cfg.img, 3), dtype=np.uint8)
+    labs = rng.integers(0, cfg.num_classes, size=n, dtype=np.int32)
+    imgs.tofile(tmp_path / "i.u8")
+    labs.tofile(tmp_path / "l.i32")
+    ld = v.Loader(tmp_path / "i.u8", tmp_path / "l.i32", cfg.img, B, seed=5, pinned=True)
+    params = v.data.init_params(cfg, "parity", seed=4)
+    a = v.ViT.build(cfg, B, prec, params=params)
+    b = v.ViT.build(cfg, B, prec, params=params)
+    for seq in range(6):  # past the 2-slot device staging ring and into epoch 2
+        ip, lp, ep, st = ld.next_raw()
+        ids, _, _ = v.data.loader_batch_records(n, B, 1, 0, 5, seq)
+        a.set_batch_u8(ip, lp)
+        la = a.forward()
+        px = v.data.normalize_u8(imgs[ids], v.IMAGENET_MEAN, v.IMAGENET_STD)
+        lb = b.forward(px, labs[ids])
+        assert la == lb, (seq, la, lb)
+        assert np.array_equal(a.logits(), b.logits())
+    # forward-only u8 batch
+    a.set_batch_u8(imgs[:B])
+    assert a.forward() == -1.0
+    ld.close(); a.close(); b.close()

@@ -60,7 +60,8 @@ def build(quiet=True):
 
 _VOID = [("vit_clear_error", []), ("vit_set_stream", [ctypes.c_void_p]),
          ("vit_free", [ctypes.c_void_p]), ("vit_event_destroy", [ctypes.c_void_p]),
-         ("vit_trainer_destroy", [ctypes.c_void_p]), ("vit_trainer_timing_reset", [ctypes.c_void_p])]
+         ("vit_trainer_destroy", [ctypes.c_void_p]), ("vit_trainer_timing_reset", [ctypes.c_void_p]),
+         ("vit_loader_close", [ctypes.c_void_p])]
 
 # name -> (restype, argtypes)
 P, I, LL, F, S = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_size_t
@@ -123,6 +124,11 @@ _SIGS = {
     "vit_checkpoint_read_info": (I, [ctypes.c_char_p, P]),
     "vit_checkpoint_write": (I, [ctypes.c_char_p, ctypes.POINTER(VitConfigC), P, P, P, I, P]),
     "vit_checkpoint_read": (I, [ctypes.c_char_p, ctypes.POINTER(VitConfigC), P, P, P]),
+    # input pipeline (include/vit_data.h)
+    "vit_loader_open": (P, [ctypes.c_char_p, ctypes.c_char_p, I, I, ctypes.c_ulonglong, I, I, I, I, I]),
+    "vit_loader_num_records": (LL, [P]), "vit_loader_steps_per_epoch": (I, [P]),
+    "vit_loader_next": (I, [P, ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(LL), ctypes.POINTER(I)]),
+    "vit_trainer_set_batch_u8": (I, [P, P, P, P, P]),
     "vit_trainer_save_checkpoint": (I, [P, ctypes.c_char_p]),
     "vit_trainer_load_checkpoint": (I, [P, ctypes.c_char_p]),
 }
@@ -289,6 +295,54 @@ def read_checkpoint(path, cfg):
     return p, m, v
 
 
+# --------------------------------------------------------------------------- input pipeline
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+class Loader:
+    """Native record loader (include/vit_data.h): uint8 [N, img, img, 3] + int32 [N] files,
+    seeded per-epoch shuffle, the batch of DP rank `rank` of `world`, background assembly."""
+
+    def __init__(self, images_path, labels_path, img, batch, seed=1337, rank=0, world=1,
+                 shuffle=True, pinned=True, depth=3):
+        self.img, self.B = img, batch
+        self.h = lib().vit_loader_open(os.fsencode(images_path), os.fsencode(labels_path), img, batch,
+                                       seed, rank, world, int(shuffle), int(pinned), depth)
+        if not self.h:
+            check("vit_loader_open")
+            raise VitError("vit_loader_open failed")
+        self.num_records = int(lib().vit_loader_num_records(self.h))
+        self.steps_per_epoch = int(lib().vit_loader_steps_per_epoch(self.h))
+
+    def next_raw(self):
+        """(images_ptr, labels_ptr, epoch, step): host pointers valid until the next call."""
+        ip, lp, ep, st = P(), P(), LL(), I()
+        if lib().vit_loader_next(self.h, ctypes.byref(ip), ctypes.byref(lp), ctypes.byref(ep),
+                                 ctypes.byref(st)):
+            check("vit_loader_next")
+        return ip.value, lp.value, ep.value, st.value
+
+    def next(self):
+        """(images uint8 [B, img, img, 3], labels int32 [B], epoch, step) — copies."""
+        ip, lp, ep, st = self.next_raw()
+        n = self.B * self.img * self.img * 3
+        img = np.ctypeslib.as_array((ctypes.c_ubyte * n).from_address(ip)).copy()
+        lab = np.ctypeslib.as_array((ctypes.c_int * self.B).from_address(lp)).copy()
+        return img.reshape(self.B, self.img, self.img, 3), lab, ep, st
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().vit_loader_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 # --------------------------------------------------------------------------- model
 class ViT:
     """Mirror of the reference's `struct ViT` (train_vit.rs:65-86) over the native trainer.
@@ -363,6 +417,27 @@ class ViT:
         self._ok(lib().vit_trainer_set_batch(self.h, px.ctypes.data_as(P),
                                              lb.ctypes.data_as(P) if lb is not None else None),
                  "set_batch")
+
+    def set_batch_u8(self, images, labels=None, mean=IMAGENET_MEAN, std=IMAGENET_STD):
+        """uint8 [B, img, img, 3] (numpy array, or a host pointer from Loader.next_raw) ->
+        normalised device pixels (vit_trainer_set_batch_u8)."""
+        if isinstance(images, np.ndarray):
+            images = np.ascontiguousarray(images, dtype=np.uint8)
+            assert images.shape == (self.B, self.cfg.img, self.cfg.img, 3)
+            iptr = images.ctypes.data_as(P)
+        else:
+            iptr = P(images)
+        lptr = None
+        if isinstance(labels, np.ndarray):
+            labels = np.ascontiguousarray(labels, dtype=np.int32)
+            assert labels.shape == (self.B,)
+            lptr = labels.ctypes.data_as(P)
+        elif labels is not None:
+            lptr = P(labels)
+        m = np.ascontiguousarray(mean, np.float32)
+        sd = np.ascontiguousarray(std, np.float32)
+        self._ok(lib().vit_trainer_set_batch_u8(self.h, iptr, lptr, m.ctypes.data_as(P),
+                                                sd.ctypes.data_as(P)), "set_batch_u8")
 
     def forward(self, pixels=None, targets=None, b_global=None):
         if pixels is not None:

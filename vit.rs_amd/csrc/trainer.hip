@@ -20,6 +20,7 @@
 #include "ops_internal.h"
 #include "../../include/vit_trainer.h"
 #include "../../include/vit_checkpoint.h"
+#include "../../include/vit_data.h"
 
 namespace vit {
 namespace {
@@ -118,6 +119,23 @@ __global__ void argmax_rows_k(int* __restrict__ pred, int* __restrict__ correct,
         if (labels && bi == labels[row]) atomicAdd(correct, 1);
     }
 }
+// input pipeline: uint8 HWC images -> normalised fp32 CHW pixels, and the
+// labels out of the staging buffer.  One thread per pixel: 3 B read, 3 x 4 B written (each channel
+// plane coalesced across the wave).  pixel = (x / 255 - mean[c]) / std[c], correctly rounded.
+__global__ void normalize_u8_k(float* __restrict__ px, int* __restrict__ lab_out,
+                               const unsigned char* __restrict__ u8, const int* __restrict__ lab_in,
+                               int B, int HW, float m0, float m1, float m2, float s0, float s1,
+                               float s2) {
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (lab_in && i < B) lab_out[i] = lab_in[i];
+    if (i >= (long long)B * HW) return;
+    const long long b = i / HW, pix = i - b * HW;
+    const unsigned char* src = u8 + i * 3;
+    float* dst = px + b * 3 * HW + pix;
+    dst[0] = ((float)src[0] / 255.0f - m0) / s0;
+    dst[HW] = ((float)src[1] / 255.0f - m1) / s1;
+    dst[2 * HW] = ((float)src[2] / 255.0f - m2) / s2;
+}
 __global__ void to_bf16_k(bf16_t* __restrict__ out, const float* __restrict__ in, long long n) {
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
          i += (long long)gridDim.x * blockDim.x)
@@ -180,6 +198,12 @@ struct Trainer {
     int* labels = nullptr;
     bool has_targets = true;  // false after set_batch without labels: forward only (:264-266)
     int* preds = nullptr;     // eval: [B] top-1 + one counter
+    // uint8 upload: double-buffered device staging filled on s_copy, normalised on s
+    hipStream_t s_copy = nullptr;
+    unsigned char* u8_stage[2]{};
+    int* lab_stage[2]{};
+    hipEvent_t u8_copied[2]{}, u8_used[2]{};
+    int u8_k = 0;
     // AdamW state (allocated on the first AdamW step / a checkpoint load with optimizer state)
     float *adam_m = nullptr, *adam_v = nullptr;
     int adam_t = 0;
@@ -520,6 +544,12 @@ struct Trainer {
     }
 
     void destroy() {
+        if (s_copy) (void)hipStreamSynchronize(s_copy);
+        for (int k = 0; k < 2; k++) {
+            if (u8_copied[k]) (void)hipEventDestroy(u8_copied[k]);
+            if (u8_used[k]) (void)hipEventDestroy(u8_used[k]);
+        }
+        if (s_copy) (void)hipStreamDestroy(s_copy);
         if (s) (void)hipStreamSynchronize(s);
         if (s_comm) (void)hipStreamSynchronize(s_comm);
         if (s2) (void)hipStreamSynchronize(s2);
@@ -909,6 +939,40 @@ struct Trainer {
         VIT_HIP(hipStreamWaitEvent(s, comm_done, 0));
     }
 
+    // upload one uint8 batch (host) and normalise it into `pixels` (include/vit_data.h)
+    bool set_batch_u8(const unsigned char* img, const int* lab, const float* mean, const float* sd) {
+        const int HW = cfg.img * cfg.img;
+        const size_t bytes = (size_t)B * HW * 3;
+        if (!s_copy) {
+            VIT_HIP(hipStreamCreateWithFlags(&s_copy, hipStreamNonBlocking));
+            for (int k = 0; k < 2; k++) {
+                u8_stage[k] = alloc<unsigned char>((long long)bytes);
+                lab_stage[k] = alloc<int>(B);
+                VIT_HIP(hipEventCreateWithFlags(&u8_copied[k], hipEventDisableTiming));
+                VIT_HIP(hipEventCreateWithFlags(&u8_used[k], hipEventDisableTiming));
+                VIT_HIP(hipEventRecord(u8_used[k], s));
+            }
+            if (has_error()) return false;
+        }
+        const int k = u8_k & 1;
+        u8_k++;
+        // the staging slot is free once the normalise of two uploads ago has run
+        VIT_HIP(hipStreamWaitEvent(s_copy, u8_used[k], 0));
+        VIT_HIP(hipMemcpyAsync(u8_stage[k], img, bytes, hipMemcpyHostToDevice, s_copy));
+        if (lab) VIT_HIP(hipMemcpyAsync(lab_stage[k], lab, (size_t)B * 4, hipMemcpyHostToDevice, s_copy));
+        VIT_HIP(hipEventRecord(u8_copied[k], s_copy));
+        VIT_HIP(hipStreamWaitEvent(s, u8_copied[k], 0));
+        has_targets = lab != nullptr;
+        const long long n = (long long)B * HW;
+        normalize_u8_k<<<cdiv(n, 256), 256, 0, s>>>(pixels, labels, u8_stage[k], lab ? lab_stage[k] : nullptr,
+                                                     B, HW, mean[0], mean[1], mean[2], sd[0], sd[1], sd[2]);
+        after_launch("normalize_u8");
+        VIT_HIP(hipEventRecord(u8_used[k], s));
+        // the host buffers may be reused once the DMA has read them (overlaps the GPU's queue)
+        VIT_HIP(hipEventSynchronize(u8_copied[k]));
+        return !has_error();
+    }
+
     bool ensure_adam() {
         if (adam_m) return true;
         adam_m = alloc<float>(arena_elems);
@@ -1076,6 +1140,14 @@ int vit_trainer_train_step(vit_trainer_t* h, float lr, int b_global) {
     vit_trainer_backward(h);
     vit_trainer_step(h, lr);
     return vit::has_error();
+}
+int vit_trainer_set_batch_u8(vit_trainer_t* h, const unsigned char* images, const int* labels,
+                             const float* mean3, const float* std3) {
+    if (!h || !images || !mean3 || !std3) {
+        set_error("vit_trainer_set_batch_u8: null argument");
+        return 1;
+    }
+    return h->t.set_batch_u8(images, labels, mean3, std3) ? 0 : 1;
 }
 int vit_trainer_step_adamw(vit_trainer_t* h, float lr, float beta1, float beta2, float eps,
                            float weight_decay) {

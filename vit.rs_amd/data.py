@@ -157,3 +157,33 @@ def synthetic_batch(cfg, B, seed=1337, offset_images=0):
     px = normal(seed, B * per_img, offset_images * per_img).astype(np.float32)
     lab = (splitmix64(seed + 7, B, offset_images) % np.uint64(cfg.num_classes)).astype(np.int32)
     return px.reshape(B, cfg.in_ch, cfg.img, cfg.img), lab
+
+
+# ------------------------------------------------------------------ input pipeline mirrors
+def epoch_permutation(n, seed, epoch, shuffle=True):
+    """The loader's per-epoch record order (include/vit_data.h): Fisher-Yates, i = n-1 .. 1,
+    swap(i, r mod (i+1)) with r the splitmix64 stream of seed + epoch at position n-1-i."""
+    perm = np.arange(n, dtype=np.int64)
+    if not shuffle or n < 2:
+        return perm
+    r = splitmix64((seed + epoch) & 0xFFFFFFFFFFFFFFFF, n - 1)
+    for i in range(n - 1, 0, -1):
+        j = int(r[n - 1 - i] % np.uint64(i + 1))
+        perm[i], perm[j] = perm[j], perm[i]
+    return perm
+
+
+def loader_batch_records(n, batch, world, rank, seed, seq, shuffle=True):
+    """Record ids of the loader's batch number `seq` (epochs run back to back) for `rank`."""
+    steps = n // (batch * world)
+    epoch, step = divmod(seq, steps)
+    perm = epoch_permutation(n, seed, epoch, shuffle)
+    base = (step * world + rank) * batch
+    return perm[base:base + batch], epoch, step
+
+
+def normalize_u8(images, mean, std):
+    """uint8 [B, H, W, 3] -> fp32 [B, 3, H, W]: (x / 255 - mean[c]) / std[c] in fp32."""
+    x = np.asarray(images, np.uint8).astype(np.float32) / np.float32(255)
+    x = (x - np.asarray(mean, np.float32)) / np.asarray(std, np.float32)
+    return np.ascontiguousarray(x.transpose(0, 3, 1, 2))
