@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true", help="one all-reduce after backward")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="skip the side measurement with the uint8 input pipeline in the loop")
     ap.add_argument("--serial", action="store_true",
                     help="run every pass with stream concurrency off (the profile command of the "
                          "per-kernel roofline pass)")
@@ -159,6 +161,42 @@ def cpu_baseline(cfg, reps=3):
                        f"oracle/oracle.c -O2 -ffp-contract=off, single thread")}
 
 
+def pipeline_rate(m, cfg, B, args):
+    """images/s of train steps whose batches come through vit.Loader -> set_batch_u8 (the
+    PCIe-inclusive rate of DESIGN.md; uint8 records, 2 batches' worth in a temp file)."""
+    import tempfile
+    d = tempfile.mkdtemp(prefix="vit_bench_")
+    try:
+        n = 2 * B
+        rng = np.random.default_rng(0)
+        rng.integers(0, 256, size=(n, cfg.img, cfg.img, 3), dtype=np.uint8).tofile(os.path.join(d, "i.u8"))
+        rng.integers(0, cfg.num_classes, size=n, dtype=np.int32).tofile(os.path.join(d, "l.i32"))
+        ld = vit.Loader(os.path.join(d, "i.u8"), os.path.join(d, "l.i32"), cfg.img, B, seed=1, pinned=True)
+
+        def step():
+            ip, lp, _, _ = ld.next_raw()
+            m.set_batch_u8(ip, lp)
+            m.train_step(args.lr, B)
+
+        for _ in range(2):
+            step()
+        m.sync()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        m.sync()
+        dt = time.perf_counter() - t0
+        ld.close()
+        return {"value": round(B * args.steps / dt, 2), "unit": "images/s",
+                "ms_per_step": round(dt / args.steps * 1e3, 3),
+                "what": "loader (mmap, pinned 3-slot ring, 1 thread) + uint8 upload on a copy stream + "
+                        "device normalise + train step, per step"}
+    finally:
+        for f in os.listdir(d):
+            os.remove(os.path.join(d, f))
+        os.rmdir(d)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -226,6 +264,12 @@ def main():
         timed(args.steps)
         m.set_timing(False)
         kern = m.timing()
+    # side measurement (N=1, not `value`): the same steps fed by the input pipeline — the native
+    # loader (pinned ring, background thread) + uint8 H2D upload + device normalise in the loop
+    pipe = None
+    if world == 1 and not args.no_pipeline:
+        m.set_concurrency(not args.serial)
+        pipe = pipeline_rate(m, cfg, B, args)
     ips = world * B * args.steps / dt
     _, gflop_img = cfg.train_gflop_per_image()
 
@@ -258,7 +302,7 @@ def main():
             "mfma_roofline_frac_step": round(ips * gflop_img / world / (PEAK_BF16_TFLOPS * 1e3), 4),
             "train_gflop_per_image": round(gflop_img, 3),
             "loss_after_warmup": round(loss_w, 4),
-            "roofline": roof, "kernels": ksum,
+            "roofline": roof, "kernels": ksum, "input_pipeline": pipe,
             "kernels_note": "per-kernel ms from HIP events over a second pass of the same steps run "
                             "with stream concurrency off (kernels one at a time)",
         }

@@ -1,5 +1,4 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/tall.log 2>&1 &&
-bash tools/profile.sh r01b
+timeout -k 10 400 python -u bench.py --no-cpu-baseline > gpurun_out/bench4.json 2> gpurun_out/bench4.err
