@@ -15,11 +15,11 @@ export TMPDIR=/tmp
 timeout -k 10 420 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" &&
 echo "bench ok" &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/ktrace" -o run --output-format csv \
-    -- python3 bench.py --serial --steps "$STEPS" --warmup 2 --no-cpu-baseline > "$OUT/ktrace_bench.json" 2> "$OUT/ktrace.err" &&
+    -- python3 bench.py --serial --steps "$STEPS" --warmup 2 --no-cpu-baseline --no-pipeline > "$OUT/ktrace_bench.json" 2> "$OUT/ktrace.err" &&
 echo "ktrace ok" &&
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv \
-    -- python3 bench.py --serial --steps 1 --warmup 1 --no-cpu-baseline --no-timing > /dev/null 2> "$OUT/pmc_fetch.err" &&
+    -- python3 bench.py --serial --steps 1 --warmup 1 --no-cpu-baseline --no-timing --no-pipeline > /dev/null 2> "$OUT/pmc_fetch.err" &&
 echo "pmc fetch ok" &&
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv \
-    -- python3 bench.py --serial --steps 1 --warmup 1 --no-cpu-baseline --no-timing > /dev/null 2> "$OUT/pmc_write.err" &&
+    -- python3 bench.py --serial --steps 1 --warmup 1 --no-cpu-baseline --no-timing --no-pipeline > /dev/null 2> "$OUT/pmc_write.err" &&
 echo "pmc write ok"
