@@ -32,6 +32,7 @@ struct GemmParams {
     int kchunk;  // K range per split (multiple of the K tile)
     int debug_same_tile;
     int no_epi;  // diagnostic (gemm_bf16_set_debug): skip the epilogue, keep the accumulators live
+    int epi_generic;  // A/B (debug flag 32): the generic (bounds-checked) staged epilogue everywhere
     int tiles;   // output tiles of the launch (the grid is tiles x K-splits)
 };
 
@@ -190,6 +191,92 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, flo
 // (every wave past the main loop and its LDS-DMA retired).
 constexpr int STG_LD = 68;                       // padded row (floats): conflict-free b128 access
 constexpr int STG_WAVE_BYTES = 64 * STG_LD * 4;  // 17,408 B per wave
+// Interior wave tiles (all 128 rows < M, all 64 columns < N): one pass of 64 rows with every
+// global load of the pass (aux rows, bias) issued before the first computation, and no branch
+// between loads and stores.  The generic loop below serialised load -> s_waitcnt vmcnt(0) ->
+// compute -> store per 8-row step (the wait also drained the previous step's stores), so the
+// DGELU / RESID epilogues ran one HBM round trip per step.
+template <int EPI>
+__device__ __forceinline__ void staged_pass_interior(const GemmParams& p, const float* st, int rr,
+                                                     int cc, int mrow, int n, float (&cs)[8]) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if constexpr (EPI != EPI_F32_ATOMIC && EPI != EPI_BF16_DGELU && EPI != EPI_F32_SLAB) {
+        if (p.bias) {
+            const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
+            const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
+            bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w;
+            bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+        }
+    }
+    constexpr bool AUX16 = EPI == EPI_BF16_DGELU;
+    constexpr bool AUX32 = EPI == EPI_F32_RESID || EPI == EPI_F32_ACC;
+    u32x4 ax[AUX16 ? 8 : (AUX32 ? 16 : 1)];
+    if constexpr (AUX16) {
+#pragma unroll
+        for (int it = 0; it < 8; it++)
+            ax[it] = *reinterpret_cast<const u32x4*>((const bf16_t*)p.aux + (long long)(mrow + it * 8 + rr) * p.ldaux + n);
+    } else if constexpr (AUX32) {
+        const float* src = EPI == EPI_F32_RESID ? (const float*)p.aux : (const float*)p.C;
+        const long long ld = EPI == EPI_F32_RESID ? p.ldaux : p.ldc;
+#pragma unroll
+        for (int it = 0; it < 8; it++) {
+            const u32x4* q = reinterpret_cast<const u32x4*>(src + (long long)(mrow + it * 8 + rr) * ld + n);
+            ax[2 * it] = q[0];
+            ax[2 * it + 1] = q[1];
+        }
+    }
+    float* slab = nullptr;
+    if constexpr (EPI == EPI_F32_SLAB) slab = (float*)p.C + (long long)split_index(p.tiles) * p.M * p.ldc;
+#pragma unroll
+    for (int it = 0; it < 8; it++) {
+        const int r = it * 8 + rr;
+        const f32x4_t lo = *reinterpret_cast<const f32x4_t*>(st + r * STG_LD + cc);
+        const f32x4_t hi = *reinterpret_cast<const f32x4_t*>(st + r * STG_LD + cc + 4);
+        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const long long off = (long long)(mrow + r) * p.ldc + n;
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] += bv[j];
+        auto pack8 = [](const float (&w)[8]) {
+            return u32x4{pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3]), pack_bf16x2(w[4], w[5]),
+                         pack_bf16x2(w[6], w[7])};
+        };
+        auto st_f32 = [&](float* q) {
+            reinterpret_cast<float4*>(q)[0] = make_float4(v[0], v[1], v[2], v[3]);
+            reinterpret_cast<float4*>(q)[1] = make_float4(v[4], v[5], v[6], v[7]);
+        };
+        if constexpr (EPI == EPI_F32_STORE) {
+            st_f32((float*)p.C + off);
+        } else if constexpr (EPI == EPI_F32_SLAB) {
+            st_f32(slab + off);
+        } else if constexpr (AUX32) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                v[j] += __uint_as_float(ax[2 * it][j]);
+                v[4 + j] += __uint_as_float(ax[2 * it + 1][j]);
+            }
+            st_f32((float*)p.C + off);
+        } else if constexpr (EPI == EPI_BF16_STORE) {
+            *reinterpret_cast<u32x4*>((bf16_t*)p.C + off) = pack8(v);
+        } else if constexpr (EPI == EPI_BF16_GELU) {
+            float gv[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) gv[j] = gelu_fast_f(v[j]);
+            *reinterpret_cast<u32x4*>((bf16_t*)p.C + off) = pack8(v);
+            *reinterpret_cast<u32x4*>((bf16_t*)p.C2 + off) = pack8(gv);
+        } else if constexpr (EPI == EPI_BF16_DGELU) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                v[2 * j] *= gelu_grad_fast_f(__uint_as_float(ax[it][j] << 16));
+                v[2 * j + 1] *= gelu_grad_fast_f(__uint_as_float(ax[it][j] & 0xffff0000u));
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++) cs[j] += v[j];
+            *reinterpret_cast<u32x4*>((bf16_t*)p.C + off) = pack8(v);
+        }
+    }
+}
+
 template <int EPI>
 __device__ __forceinline__ void staged_epilogue(const GemmParams& p, f32x4_t (&acc)[8][4],
                                                 char* stage, int lane, int m0, int n0) {
@@ -197,6 +284,7 @@ __device__ __forceinline__ void staged_epilogue(const GemmParams& p, f32x4_t (&a
     const int i = lane & 15, g = lane >> 4;
     const int rr = lane >> 3, cc = (lane & 7) * 8;
     float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const bool interior = EPI != EPI_F32_ATOMIC && !p.epi_generic && m0 + 128 <= p.M && n0 + 64 <= p.N;
 #pragma unroll
     for (int pass = 0; pass < 2; pass++) {
 #pragma unroll
@@ -204,6 +292,10 @@ __device__ __forceinline__ void staged_epilogue(const GemmParams& p, f32x4_t (&a
 #pragma unroll
             for (int b = 0; b < 4; b++)
                 *reinterpret_cast<f32x4_t*>(st + (a * 16 + i) * STG_LD + b * 16 + 4 * g) = acc[pass * 4 + a][b];
+        if (interior) {
+            staged_pass_interior<EPI>(p, st, rr, cc, m0 + pass * 64, n0 + cc, cs);
+            continue;
+        }
 #pragma unroll
         for (int it = 0; it < 8; it++) {
             const int r = it * 8 + rr;
@@ -1205,6 +1297,7 @@ static GemmParams make_params(const GemmArgs& a, int kchunk) {
     static const int same = getenv("VIT_DEBUG_SAME_TILE") ? 1 : 0;
     p.debug_same_tile = same;
     p.no_epi = (g_debug_flags & 2) ? 1 : 0;
+    p.epi_generic = (g_debug_flags & 32) ? 1 : 0;
     p.tiles = 1;
     return p;
 }
