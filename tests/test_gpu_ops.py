@@ -282,10 +282,10 @@ def test_error_channel(gpu):
 
 
 # ------------------------------------------------------------------ generic bf16 GEMM engine
-@pytest.fixture(params=[2, 3, 4])
+@pytest.fixture(params=[2, 3, 4, 5])
 def engine(request, gpu):
     """Run a test under each GEMM engine (2 = 256x256, 3 = its stream-K persistent form, 4 = 256x128
-    two per CU), then restore the default."""
+    two per CU, 5 = the persistent form over whole tiles), then restore the default."""
     gpu.lib().gemm_bf16_set_variant(request.param)
     yield request.param
     gpu.lib().gemm_bf16_set_variant(2)

@@ -847,8 +847,127 @@ __device__ __forceinline__ void staged_epilogue16(const GemmParams& p, f32x4_t (
     }
 }
 
+// Interior wave tiles (all 128 rows < M, all 64 columns < N): the aux rows of the first D passes
+// are loaded before the first pass and pass a issues the loads of pass a + D, so the epilogue waits
+// for about one HBM round trip instead of one per 16-row pass (the loop above serialises eight).
+template <int EPI>
+__device__ __forceinline__ void staged_epilogue16_interior(const GemmParams& p, f32x4_t (&acc)[8][4],
+                                                           char* stg, int lane, int m0, int n0) {
+    constexpr bool AUX16 = EPI == EPI_BF16_DGELU;
+    constexpr bool AUX32 = EPI == EPI_F32_RESID || EPI == EPI_F32_ACC;
+    constexpr int NL = AUX16 ? 2 : (AUX32 ? 4 : 1);  // 16-B aux loads per lane and pass
+    constexpr int D = AUX16 ? 2 : 2;                 // passes whose aux loads are in flight (VGPR budget: no spills)
+    const int i = lane & 15, g = lane >> 4;
+    const int rr = lane >> 3, c8 = lane & 7;
+    const int n = n0 + c8 * 8;
+    u32x4 ax[8][NL];
+    auto load_pass = [&](int a) {
+        if constexpr (AUX16) {
+#pragma unroll
+            for (int it = 0; it < 2; it++)
+                ax[a & 7][it] = *reinterpret_cast<const u32x4*>(
+                    (const bf16_t*)p.aux + (long long)(m0 + a * 16 + it * 8 + rr) * p.ldaux + n);
+        } else if constexpr (AUX32) {
+            const float* src = EPI == EPI_F32_RESID ? (const float*)p.aux : (const float*)p.C;
+            const long long ld = EPI == EPI_F32_RESID ? p.ldaux : p.ldc;
+#pragma unroll
+            for (int it = 0; it < 2; it++) {
+                const u32x4* q = reinterpret_cast<const u32x4*>(src + (long long)(m0 + a * 16 + it * 8 + rr) * ld + n);
+                ax[a & 7][2 * it] = q[0];
+                ax[a & 7][2 * it + 1] = q[1];
+            }
+        }
+    };
+#pragma unroll
+    for (int a = 0; a < D; a++) load_pass(a);
+    float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if constexpr (EPI != EPI_F32_ATOMIC && EPI != EPI_BF16_DGELU && EPI != EPI_F32_SLAB) {
+        if (p.bias) {
+            const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
+            const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
+            bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w;
+            bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+        }
+    }
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    auto pack8 = [](const float (&w)[8]) {
+        return u32x4{pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3]), pack_bf16x2(w[4], w[5]),
+                     pack_bf16x2(w[6], w[7])};
+    };
+#pragma unroll
+    for (int a = 0; a < 8; a++) {
+        __builtin_amdgcn_sched_barrier(0);  // pass a issues exactly the loads of pass a + D
+        if (a + D < 8) load_pass(a + D);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+            *reinterpret_cast<f32x4_t*>(stg + i * 256 + (((b * 4 + g) ^ i) << 4)) = acc[a][b];
+#pragma unroll
+        for (int it = 0; it < 2; it++) {
+            if (it) __builtin_amdgcn_sched_barrier(0);  // one row at a time (VGPR budget)
+            const int r = it * 8 + rr;
+            const f32x4_t lo = *reinterpret_cast<const f32x4_t*>(stg + r * 256 + (((2 * c8) ^ r) << 4));
+            const f32x4_t hi = *reinterpret_cast<const f32x4_t*>(stg + r * 256 + (((2 * c8 + 1) ^ r) << 4));
+            float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+            for (int j = 0; j < 8; j++) v[j] += bv[j];
+            const long long off = (long long)(m0 + a * 16 + r) * p.ldc + n;
+            auto st_f32 = [&](float* q) {
+                reinterpret_cast<float4*>(q)[0] = make_float4(v[0], v[1], v[2], v[3]);
+                reinterpret_cast<float4*>(q)[1] = make_float4(v[4], v[5], v[6], v[7]);
+            };
+            if constexpr (EPI == EPI_F32_STORE) {
+                st_f32((float*)p.C + off);
+            } else if constexpr (AUX32) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    v[j] += __uint_as_float(ax[a][2 * it][j]);
+                    v[4 + j] += __uint_as_float(ax[a][2 * it + 1][j]);
+                }
+                st_f32((float*)p.C + off);
+            } else if constexpr (EPI == EPI_BF16_STORE) {
+                *reinterpret_cast<u32x4*>((bf16_t*)p.C + off) = pack8(v);
+            } else if constexpr (EPI == EPI_BF16_GELU) {
+                float gv[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) gv[j] = gelu_fast_f(v[j]);
+                *reinterpret_cast<u32x4*>((bf16_t*)p.C + off) = pack8(v);
+                *reinterpret_cast<u32x4*>((bf16_t*)p.C2 + off) = pack8(gv);
+            } else if constexpr (EPI == EPI_BF16_DGELU) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    v[2 * j] *= gelu_grad_fast_f(__uint_as_float(ax[a][it][j] << 16));
+                    v[2 * j + 1] *= gelu_grad_fast_f(__uint_as_float(ax[a][it][j] & 0xffff0000u));
+                }
+#pragma unroll
+                for (int j = 0; j < 8; j++) cs[j] += v[j];
+                *reinterpret_cast<u32x4*>((bf16_t*)p.C + off) = pack8(v);
+            }
+        }
+    }
+    if constexpr (EPI == EPI_BF16_DGELU) {
+        if (p.colsum_out) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                float t = cs[j];
+                t += __shfl_xor(t, 8, 64);
+                t += __shfl_xor(t, 16, 64);
+                t += __shfl_xor(t, 32, 64);
+                cs[j] = t;
+            }
+            if (rr == 0) {
+#pragma unroll
+                for (int j = 0; j < 8; j++) atomicAdd(p.colsum_out + n + j, cs[j]);
+            }
+        }
+    }
+}
+
+// whole != 0: persistent launch over whole tiles (workgroup w takes tiles [T*w/P, T*(w+1)/P)), so
+// no tile is cut and no workgroup waits on another: safe beside other streams' kernels, which a
+// stream-K hand-off is not (its partner may not be resident).
 template <bool AK, bool BKC, int EPI>
-__global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p, char* __restrict__ sk_ws, int S) {
+__global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p, char* __restrict__ sk_ws, int S, int whole) {
     __shared__ __attribute__((aligned(1024))) char smem[SMEM_BYTES];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -857,7 +976,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p, char* __restr
     const int P = gridDim.x;
     const int w = xcd_remap(blockIdx.x, P);  // XCD-contiguous ranges: neighbouring tiles share L2
     const int Wtot = p.tiles * S;  // host guarantees < 2^31
-    const int g_begin = (int)((long long)Wtot * w / P), g_end = (int)((long long)Wtot * (w + 1) / P);
+    const int g_begin = whole ? (int)((long long)p.tiles * w / P) * S : (int)((long long)Wtot * w / P);
+    const int g_end = whole ? (int)((long long)p.tiles * (w + 1) / P) * S : (int)((long long)Wtot * (w + 1) / P);
     const bf16_t* A = (const bf16_t*)p.A;
     const bf16_t* B = (const bf16_t*)p.B;
     int* flags = reinterpret_cast<int*>(sk_ws);
@@ -986,7 +1106,11 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p, char* __restr
             if (lane == 0) __hip_atomic_fetch_add(flags + w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else if (!skip_epilogue(p, acc)) {
             const int m0 = (t / ntn) * BM + wm * 128, n0 = (t % ntn) * BN + wn * 64;
-            staged_epilogue16<EPI>(p, acc, stg, lane, m0, n0);
+            // DGELU keeps the generic loop: its interior form spills ~50 VGPRs in this kernel
+            if (EPI != EPI_BF16_DGELU && !p.epi_generic && m0 + 128 <= p.M && n0 + 64 <= p.N)
+                staged_epilogue16_interior<EPI>(p, acc, stg, lane, m0, n0);
+            else
+                staged_epilogue16<EPI>(p, acc, stg, lane, m0, n0);
         }
     }
     if (any && !lagging) bar();  // balance the stagger barrier
@@ -1275,18 +1399,20 @@ __global__ __launch_bounds__(256) void slab_reduce_k(float* __restrict__ C, long
 
 // engine selection (gemm_bf16_set_variant; default from VIT_GEMM, else 2):
 //   1 = 128x128 register-staged, 2 = 256x256 one workgroup per CU, 3 = 2 as stream-K persistent
-//   (launches with >= 1 tile per CU; the rest, e.g. split-K wgrad, take 2), 4 = 256x128 two per CU
+//   (launches with >= 1 tile per CU; the rest, e.g. split-K wgrad, take 2), 4 = 256x128 two per CU,
+//   5 = 2 as a persistent launch over whole tiles (no hand-offs; split-K wgrad takes 2)
 static int g_variant = -1;
 static int g_debug_flags = 0;
+static bool known_variant(int v) { return v == 1 || v == 3 || v == 4 || v == 5; }
 static int gemm_variant() {
     if (g_variant < 0) {
         const char* e = getenv("VIT_GEMM");
         g_variant = e ? atoi(e) : 2;
-        if (g_variant != 1 && g_variant != 3 && g_variant != 4) g_variant = 2;
+        if (!known_variant(g_variant)) g_variant = 2;
     }
     return g_variant;
 }
-void gemm_set_variant(int v) { g_variant = (v == 1 || v == 3 || v == 4) ? v : 2; }
+void gemm_set_variant(int v) { g_variant = known_variant(v) ? v : 2; }
 void gemm_set_debug(int flags) { g_debug_flags = flags; }
 
 static GemmParams make_params(const GemmArgs& a, int kchunk) {
@@ -1486,10 +1612,10 @@ static int num_cus() {
 size_t gemm_sk_bytes() { return g3::FLAG_BYTES + (size_t)num_cus() * g3::PART_BYTES; }
 
 template <bool AK, bool BKC>
-static void launch_g3(int epi, const GemmParams& p, int P, char* ws, int S, hipStream_t s) {
+static void launch_g3(int epi, const GemmParams& p, int P, char* ws, int S, int whole, hipStream_t s) {
     switch (epi) {
 #define VIT_CASE(E) \
-    case E: g3::gemm_kernel<AK, BKC, E><<<P, g3::NT, 0, s>>>(p, ws, S); break;
+    case E: g3::gemm_kernel<AK, BKC, E><<<P, g3::NT, 0, s>>>(p, ws, S, whole); break;
         VIT_CASE(EPI_F32_STORE)
         VIT_CASE(EPI_F32_ACC)
         VIT_CASE(EPI_BF16_STORE)
@@ -1501,22 +1627,28 @@ static void launch_g3(int epi, const GemmParams& p, int P, char* ws, int S, hipS
     }
 }
 
-// stream-K persistent launch (g3) when the launch has at least one tile per CU; false = not taken
-static bool gemm_bf16_g3(const GemmArgs& a, hipStream_t s) {
-    const int P = num_cus();
+// persistent launch (g3): stream-K when the launch has at least one tile per CU, or (whole) one
+// contiguous range of whole tiles per workgroup on min(tiles, CUs) workgroups; false = not taken
+static bool gemm_bf16_g3(const GemmArgs& a, hipStream_t s, bool whole) {
+    const int ncu = num_cus();
     const long long tiles = (long long)cdiv(a.M, g3::BM) * cdiv(a.N, g3::BN);
     const int S = a.K / g3::BK;
     if (a.epi == EPI_F32_ATOMIC || a.epi == EPI_F32_SLAB) return false;
-    if (tiles < P || a.K % g3::BK || S < 2 || tiles * S >= (1LL << 31)) return false;
-    char* ws = a.sk_ws ? a.sk_ws : (char*)sk_workspace(gemm_sk_bytes());
-    if (!ws) return true;  // error already set
+    if ((!whole && tiles < ncu) || a.K % g3::BK || S < 2 || tiles * S >= (1LL << 31)) return false;
+    char* ws = nullptr;
+    if (!whole) {
+        ws = a.sk_ws ? a.sk_ws : (char*)sk_workspace(gemm_sk_bytes());
+        if (!ws) return true;  // error already set
+    }
+    const int P = whole ? (int)std::min<long long>(tiles, ncu) : ncu;
     GemmParams p = make_params(a, a.K);
     p.tiles = (int)tiles;
-    if (a.a_kcontig && a.b_kcontig) launch_g3<true, true>(a.epi, p, P, ws, S, s);
-    else if (a.a_kcontig && !a.b_kcontig) launch_g3<true, false>(a.epi, p, P, ws, S, s);
-    else if (!a.a_kcontig && !a.b_kcontig) launch_g3<false, false>(a.epi, p, P, ws, S, s);
-    else launch_g3<false, true>(a.epi, p, P, ws, S, s);
-    after_launch("gemm_bf16_streamk");
+    const int wh = whole ? 1 : 0;
+    if (a.a_kcontig && a.b_kcontig) launch_g3<true, true>(a.epi, p, P, ws, S, wh, s);
+    else if (a.a_kcontig && !a.b_kcontig) launch_g3<true, false>(a.epi, p, P, ws, S, wh, s);
+    else if (!a.a_kcontig && !a.b_kcontig) launch_g3<false, false>(a.epi, p, P, ws, S, wh, s);
+    else launch_g3<false, true>(a.epi, p, P, ws, S, wh, s);
+    after_launch(whole ? "gemm_bf16_persistent" : "gemm_bf16_streamk");
     return true;
 }
 
@@ -1527,7 +1659,8 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s) {
                   a.M, a.N, a.K, a.lda, a.ldb);
         return;
     }
-    if (gemm_variant() == 3 && a.M >= 256 && a.N >= 256 && gemm_bf16_g3(a, s)) return;
+    if (gemm_variant() == 3 && a.M >= 256 && a.N >= 256 && gemm_bf16_g3(a, s, false)) return;
+    if (gemm_variant() == 5 && a.M >= 256 && a.N >= 256 && gemm_bf16_g3(a, s, true)) return;
     if (gemm_variant() == 4 && a.K % g4::KTILE == 0 && a.M >= 256 && a.N >= 128 &&
         (a.epi != EPI_F32_ATOMIC || a.N % 4 == 0)) {
         gemm_bf16_g4(a, s);
