@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--C", type=int, default=768)
     ap.add_argument("--variants", default="2,4")
     ap.add_argument("--no-epi", action="store_true")
-    ap.add_argument("--modes", default=None,
+    ap.add_argument("--modes", default=None,  # 256*n: first-round stagger of n s_sleep(127)
                     help="comma-separated gemm_bf16_set_debug flag sets to A/B (2 = no epilogue, "
                          "4 = g2 prefetch depth 3); default 0 (and 2 with --no-epi)")
     ap.add_argument("--only", default=None, help="comma-separated GEMM names")

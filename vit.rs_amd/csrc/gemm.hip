@@ -34,6 +34,7 @@ struct GemmParams {
     int no_epi;  // diagnostic (gemm_bf16_set_debug): skip the epilogue, keep the accumulators live
     int epi_generic;  // A/B (debug flag 32): the generic (bounds-checked) staged epilogue everywhere
     int tiles;   // output tiles of the launch (the grid is tiles x K-splits)
+    int stagger;  // first-round start delay of every other workgroup, in s_sleep(127) units
 };
 
 // (tile, K-split) of this workgroup.  Workgroups are dealt round-robin over the 8 XCDs in
@@ -640,6 +641,15 @@ template <bool AK, bool BKC, int EPI, int DEPTH>
 __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
     constexpr int NS = DEPTH + 2;
     __shared__ __attribute__((aligned(1024))) char smem[smem_bytes<DEPTH>()];
+    // Epilogue de-phasing: every CU runs the same tile time, so the first round's start sets the
+    // phase of the whole launch and all CUs hit their epilogue HBM bursts together.  Delaying
+    // every other first-round workgroup (alternating within each XCD) puts half the CUs in their
+    // main loop while the other half stores.
+    if (p.stagger) {
+        const int lin = blockIdx.y * gridDim.x + blockIdx.x;
+        if (lin < 256 && ((lin >> 3) & 1))
+            for (int k = 0; k < p.stagger; k++) __builtin_amdgcn_s_sleep(127);
+    }
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
@@ -1424,6 +1434,7 @@ static GemmParams make_params(const GemmArgs& a, int kchunk) {
     p.debug_same_tile = same;
     p.no_epi = (g_debug_flags & 2) ? 1 : 0;
     p.epi_generic = (g_debug_flags & 32) ? 1 : 0;
+    p.stagger = (g_debug_flags >> 8) & 63;
     p.tiles = 1;
     return p;
 }
