@@ -79,17 +79,24 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
 // fc / fcproj-dgrad epilogues VALU-bound:  0.5(1 + tanh a) = sigmoid(2a), 1 - tanh^2 a =
 // 4 sigmoid(2a)(1 - sigmoid(2a)).  One v_exp + one v_rcp per element; |error| <~ 1e-7
 // absolute against the tanh form, far below the bf16 rounding of the stored value.
+// bf16-epilogue forms: x * sigmoid(2a) with a = sqrt(2/pi)(x + 0.044715 x^3) (= 0.5 x (1 + tanh a)),
+// on the raw v_exp_f32 (2^x) and v_rcp_f32 (1 ulp) instructions.  __expf / __frcp_rn wrapped them
+// in range-reduction and correctly-rounded refinement sequences (~12 VALU per element, the bulk of
+// the GELU / GELU' epilogues); the results are rounded to bf16, so 1-ulp fp32 terms do not show.
+// x -> -inf: exp2 -> inf, rcp -> 0, product -> -0; x -> +inf: sigmoid -> 1.
 __device__ __forceinline__ float gelu_fast_f(float x) {
-    const float s2 = 2.0f * 0.7978845608028654f;
-    const float a2 = s2 * (x + 0.044715f * x * x * x);  // 2a
-    return x * __frcp_rn(1.0f + __expf(-a2));
+    const float k = -2.0f * 0.7978845608028654f * 1.4426950408889634f;  // -2 sqrt(2/pi) log2(e)
+    const float t = k * fmaf(0.044715f * x, x * x, x);
+    return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(t));
 }
+// derivative with sech^2 of the tanh argument (D4): sg + 2 s x sg (1 - sg) (1 + 3 * 0.044715 x^2)
 __device__ __forceinline__ float gelu_grad_fast_f(float x) {
     const float s = 0.7978845608028654f;
+    const float k = -2.0f * s * 1.4426950408889634f;
     const float x2 = x * x;
-    const float a2 = 2.0f * s * (x + 0.044715f * x2 * x);
-    const float sg = __frcp_rn(1.0f + __expf(-a2));  // 0.5(1 + tanh a)
-    return sg + 2.0f * x * sg * (1.0f - sg) * s * (1.0f + 3.0f * 0.044715f * x2);
+    const float sg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(k * fmaf(0.044715f * x, x2, x)));  // 0.5(1 + tanh a)
+    const float u = fmaf(-sg, sg, sg);                                // sg (1 - sg)
+    return fmaf((2.0f * s) * x * u, fmaf(3.0f * 0.044715f, x2, 1.0f), sg);
 }
 
 // optimizer_step (train_vit.rs:740): p -= lr*g with two roundings like the Rust reference
