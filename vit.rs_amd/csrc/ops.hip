@@ -221,25 +221,54 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_k(float* __restrict__ dinp, bf
                                                     const float* __restrict__ mean,
                                                     const float* __restrict__ rstd, long long rows,
                                                     int C) {
-    extern __shared__ float sm[];  // [4 waves][3][C]
+    extern __shared__ float sm[];  // [4 waves][3][C]: this wave's dweight / dbias / dsum partials
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    float4 w4[NV], dw[NV], db[NV], ds[NV];
+    // the column partials live in the wave's LDS rows (each lane owns its 4*NV columns, so the
+    // read-modify-writes need no synchronisation): 36 VGPRs freed for the row prefetch below
+    float4* pw = reinterpret_cast<float4*>(sm + wave * 3 * C);
+    float4* pb = reinterpret_cast<float4*>(sm + wave * 3 * C + C);
+    float4* ps = reinterpret_cast<float4*>(sm + wave * 3 * C + 2 * C);
+    float4 w4[NV];
 #pragma unroll
     for (int j = 0; j < NV; j++) {
         w4[j] = reinterpret_cast<const float4*>(weight)[lane + 64 * j];
-        dw[j] = db[j] = ds[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        pw[lane + 64 * j] = pb[lane + 64 * j] = ps[lane + 64 * j] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     const long long nwaves = (long long)gridDim.x * 4;
-    for (long long row = blockIdx.x * 4LL + wave; row < rows; row += nwaves) {
-        const TD* dyr = dout + row * C;
-        const float4* x4 = reinterpret_cast<const float4*>(inp + row * C);
-        const float mu = mean[row], rs = rstd[row];
-        float4 dy[NV], nr[NV];
+    // software pipeline over the wave's rows: the next row's dout / inp / dres_in / mean / rstd
+    // loads are in flight while this row reduces and stores (one HBM round trip per row
+    // otherwise: the row loop was latency-bound at ~85 % of the achievable bandwidth)
+    float4 pdy[NV], px[NV], pri[NV];
+    float pmu = 0.f, prs = 0.f;
+    auto fetch = [&](long long r) {
+        const TD* dyr = dout + r * C;
+        const float4* x4 = reinterpret_cast<const float4*>(inp + r * C);
+#pragma unroll
+        for (int j = 0; j < NV; j++) {
+            pdy[j] = ld4(dyr, lane + 64 * j);
+            px[j] = x4[lane + 64 * j];
+            pri[j] = dres_in ? reinterpret_cast<const float4*>(dres_in + r * C)[lane + 64 * j]
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        pmu = mean[r];
+        prs = rstd[r];
+    };
+    long long row = blockIdx.x * 4LL + wave;
+    if (row < rows) fetch(row);
+    for (; row < rows; row += nwaves) {
+        float4 dy[NV], xr[NV], ri[NV], nr[NV];
+#pragma unroll
+        for (int j = 0; j < NV; j++) {
+            dy[j] = pdy[j];
+            xr[j] = px[j];
+            ri[j] = pri[j];
+        }
+        const float mu = pmu, rs = prs;
+        if (row + nwaves < rows) fetch(row + nwaves);
         float a = 0.f, bs = 0.f;
 #pragma unroll
         for (int j = 0; j < NV; j++) {
-            dy[j] = ld4(dyr, lane + 64 * j);
-            const float4 x = x4[lane + 64 * j];
+            const float4 x = xr[j];
             nr[j] = make_float4((x.x - mu) * rs, (x.y - mu) * rs, (x.z - mu) * rs, (x.w - mu) * rs);
             const float d0 = w4[j].x * dy[j].x, d1 = w4[j].y * dy[j].y, d2 = w4[j].z * dy[j].z, d3 = w4[j].w * dy[j].w;
             a += (d0 + d1) + (d2 + d3);
@@ -249,9 +278,14 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_k(float* __restrict__ dinp, bf
 #pragma unroll
         for (int j = 0; j < NV; j++) {
             const int k = lane + 64 * j;
-            db[j].x += dy[j].x; db[j].y += dy[j].y; db[j].z += dy[j].z; db[j].w += dy[j].w;
-            dw[j].x += nr[j].x * dy[j].x; dw[j].y += nr[j].y * dy[j].y;
-            dw[j].z += nr[j].z * dy[j].z; dw[j].w += nr[j].w * dy[j].w;
+            {
+                float4 b = pb[k], w = pw[k];
+                b.x += dy[j].x; b.y += dy[j].y; b.z += dy[j].z; b.w += dy[j].w;
+                w.x += nr[j].x * dy[j].x; w.y += nr[j].y * dy[j].y;
+                w.z += nr[j].z * dy[j].z; w.w += nr[j].w * dy[j].w;
+                pb[k] = b;
+                pw[k] = w;
+            }
             float4 dv;
             dv.x = ((w4[j].x * dy[j].x - dm) - nr[j].x * dnm) * rs;
             dv.y = ((w4[j].y * dy[j].y - dm) - nr[j].y * dnm) * rs;
@@ -259,10 +293,11 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_k(float* __restrict__ dinp, bf
             dv.w = ((w4[j].w * dy[j].w - dm) - nr[j].w * dnm) * rs;
             float4* o = reinterpret_cast<float4*>(dinp + row * C) + k;
             if (dres_in) {
-                const float4 ri = reinterpret_cast<const float4*>(dres_in + row * C)[k];
-                const float4 t = make_float4(ri.x + dv.x, ri.y + dv.y, ri.z + dv.z, ri.w + dv.w);
+                const float4 t = make_float4(ri[j].x + dv.x, ri[j].y + dv.y, ri[j].z + dv.z, ri[j].w + dv.w);
                 *o = t;
-                ds[j].x += t.x; ds[j].y += t.y; ds[j].z += t.z; ds[j].w += t.w;
+                float4 u = ps[k];
+                u.x += t.x; u.y += t.y; u.z += t.z; u.w += t.w;
+                ps[k] = u;
                 if (dinp_bf)
                     reinterpret_cast<uint2*>(dinp_bf + row * C)[k] =
                         make_uint2(pack_bf16x2(t.x, t.y), pack_bf16x2(t.z, t.w));
@@ -272,13 +307,6 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_k(float* __restrict__ dinp, bf
                 *o = t;
             }
         }
-    }
-    float* mw = sm + wave * 3 * C;
-#pragma unroll
-    for (int j = 0; j < NV; j++) {
-        reinterpret_cast<float4*>(mw)[lane + 64 * j] = dw[j];
-        reinterpret_cast<float4*>(mw + C)[lane + 64 * j] = db[j];
-        reinterpret_cast<float4*>(mw + 2 * C)[lane + 64 * j] = ds[j];
     }
     __syncthreads();
     const int nsum = dsum ? 3 * C : 2 * C;
@@ -446,7 +474,8 @@ static void ln_backward_any(float* dinp, bf16_t* dinp_bf, const float* dres_in, 
         return;
     }
     long long g = (rows + 15) / 16;  // ~4 rows per wave
-    const int grid = (int)(g < 1 ? 1 : (g > 1024 ? 1024 : g));
+    // at most one round of resident blocks (3 per CU at 142-144 VGPRs; 256 CUs)
+    const int grid = (int)(g < 1 ? 1 : (g > 768 ? 768 : g));
     const size_t lds = 12 * (size_t)C * sizeof(float);
     if (dsum && !dres_in) { set_error("layernorm_backward: output column sum needs dres_in"); return; }
 #define VIT_LNB(NV) ln_bwd_vec_k<NV, TD><<<grid, 256, lds, s>>>(dinp, dinp_bf, dres_in, dw, db, dsum, dout, inp, w, mean, rstd, rows, C)
