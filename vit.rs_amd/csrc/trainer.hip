@@ -43,6 +43,11 @@ const char* kTimerNames[TC_COUNT] = {
     "gemm_qkv_dgrad", "gemm_qkv_wgrad", "layernorm_bwd", "bias_colsum", "patch_embed_bwd", "sgd",
     "misc"};
 
+// out[r][n] = vec[n] for r < rows (the bias start value of a split-K head GEMM)
+__global__ void bcast_rows_k(float* __restrict__ out, const float* __restrict__ vec, int rows, int n) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < (long long)rows * n) out[i] = vec[i % n];
+}
 __global__ void fill_k(float* p, float v, int n) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) p[i] = v;
@@ -601,6 +606,13 @@ struct Trainer {
         GemmArgs a;
         a.A = lnf; a.lda = C; a.B = P(P_HEADW); a.ldb = C; a.C = logits; a.ldc = NC;
         a.bias = P(P_HEADB); a.M = B; a.N = NC; a.K = C; a.epi = EPI_F32_STORE;
+        if (prec == VIT_BF16) {
+            // fast path: the M = B head GEMMs have 64 output tiles for 256 CUs, so they run
+            // split-K with float atomics onto the bias (fp32 mode keeps the ordered sums)
+            bcast_rows_k<<<cdiv((long long)B * NC, 256), 256, 0, s>>>(logits, P(P_HEADB), B, NC);
+            a.bias = nullptr;
+            a.epi = EPI_F32_ATOMIC;
+        }
         gemm_f32(a, s);
         softmax_rows(probs, logits, B, NC, s);
         if (has_targets) ce_forward(losses, probs, labels, B, NC, s);
@@ -616,12 +628,12 @@ struct Trainer {
         GemmArgs a;  // dlnf += dlogits . head_w
         a.A = dlogits; a.lda = NC; a.a_kcontig = true;
         a.B = P(P_HEADW); a.ldb = C; a.b_kcontig = false;
-        a.C = dlnf; a.ldc = C; a.M = B; a.N = C; a.K = NC; a.epi = EPI_F32_ACC;
+        a.C = dlnf; a.ldc = C; a.M = B; a.N = C; a.K = NC; a.epi = prec == VIT_BF16 ? EPI_F32_ATOMIC : EPI_F32_ACC;
         gemm_f32(a, s);
         GemmArgs w;  // dhead_w += dlogits^T . lnf
         w.A = dlogits; w.lda = NC; w.a_kcontig = false;
         w.B = lnf; w.ldb = C; w.b_kcontig = false;
-        w.C = G(P_HEADW); w.ldc = C; w.M = NC; w.N = C; w.K = B; w.epi = EPI_F32_ACC;
+        w.C = G(P_HEADW); w.ldc = C; w.M = NC; w.N = C; w.K = B; w.epi = prec == VIT_BF16 ? EPI_F32_ATOMIC : EPI_F32_ACC;
         gemm_f32(w, s);
         colsum_f32(G(P_HEADB), dlogits, B, NC, NC, s);
         VIT_HIP(hipMemsetAsync(dcls_x, 0, (size_t)B * C * 4, s));
