@@ -207,3 +207,85 @@ def test_dp_single_rank_rccl_is_identity(gpu, prec_name, overlap):
         m.close()
     assert rel_err(out[1][0], out[0][0]) <= 1e-6
     assert rel_err(out[1][1], out[0][1]) <= 1e-6
+
+
+def test_vit_l16_full_size_step(gpu):
+    """BASELINE config 4 shapes on one GPU (ViT-L/16, 224^2, C=1024, L=24, NH=16, B=256 per GPU,
+    bf16): the same size-independent properties as the B/16 step.  The DP=8 exchange is the
+    shape-independent arena all-reduce covered by the DP tests."""
+    v = gpu
+    cfg = v.data.CONFIGS["vit_l16"]
+    B = 256
+    params = v.data.init_params(cfg, "parity", seed=11)
+    px, lab = v.data.synthetic_batch(cfg, B, seed=12)
+    m = v.ViT.build(cfg, B, v.VIT_BF16, params=params)
+    m.set_batch(px, lab)
+    m.zero_grad()
+    loss0 = m.forward()
+    assert np.isfinite(loss0) and abs(loss0 - np.log(1000)) < 1.5
+    m.backward()
+    g = m.grads()
+    assert g.size == cfg.num_params()
+    assert np.all(np.isfinite(g))
+    gs = cfg.split(g)
+    for n in ("patch_w", "qkvw", "fcw", "fcprojw", "head_w", "wpe"):
+        assert np.abs(gs[n]).max() > 0, n
+    m.optimizer_step(0.05)
+    m.zero_grad()
+    loss1 = m.forward()
+    assert loss1 < loss0
+    m.close()
+
+
+def test_vit_l16_bf16_vs_fp32_trainer_two_layers(gpu):
+    """ViT-L/16 width (C=1024, NH=16, MLP 4096, T=197) at reduced depth and B=2: the bf16 fast
+    path against the fp32 path of the same trainer (itself pinned to the oracle at 1e-4 above),
+    bf16 tolerance 5e-2 on loss, logits and every gradient tensor."""
+    v = gpu
+    base = v.data.CONFIGS["vit_l16"]
+    cfg = v.data.VitCfg("vit_l16_l2", img=224, patch=16, channels=1024, num_layers=2,
+                        num_heads=16, num_classes=1000)
+    params = v.data.init_params(cfg, "parity", seed=13)
+    px, lab = v.data.synthetic_batch(cfg, 2, seed=14)
+    out = {}
+    for prec in (v.VIT_FP32, v.VIT_BF16):
+        m = v.ViT.build(cfg, 2, prec, params=params)
+        m.zero_grad()
+        loss = m.forward(px, lab)
+        m.backward()
+        out[prec] = (loss, m.logits(), m.grads())
+        m.close()
+    lf, zf, gf = out[v.VIT_FP32]
+    lb, zb, gb = out[v.VIT_BF16]
+    assert abs(lb - lf) <= 1e-2 * abs(lf)
+    assert rel_err(zb, zf) <= 5e-2
+    errs = per_tensor_errs(cfg, gb, gf)
+    assert max(errs.values()) <= 5e-2, errs
+    assert base.channels == cfg.channels
+
+
+def test_vit_h14_geometry_fp32_vs_oracle(gpu, oracle32):
+    """BASELINE config 5 geometry (ViT-H/14: patch 14 -> im2col K=588, T=257, C=1280, NH=16,
+    head size 80) at reduced depth, one image, fp32 parity mode: logits, loss and all gradient
+    tensors within 1e-4 of the CPU oracle.  The bf16 fused attention is built for head size 64
+    and T<=256, so bf16 mode must refuse this geometry loudly (no silent fallback)."""
+    import oracle_ctypes as oc
+    v = gpu
+    cfg = v.data.VitCfg("vit_h14_l1", img=224, patch=14, channels=1280, num_layers=1,
+                        num_heads=16, num_classes=1000)
+    assert cfg.T == 257 and cfg.head_size == 80
+    params = v.data.init_params(cfg, "parity", seed=21)
+    px, lab = v.data.synthetic_batch(cfg, 1, seed=22)
+    loss_r, logits_r, g_r = oracle_step(oc, oracle32, cfg, params, px, lab)
+    m = v.ViT.build(cfg, 1, v.VIT_FP32, params=params)
+    m.zero_grad()
+    loss = m.forward(px, lab)
+    m.backward()
+    g = m.grads()
+    assert abs(loss - loss_r) <= 1e-4 * abs(loss_r)
+    assert rel_err(m.logits(), logits_r) <= 1e-4
+    errs = per_tensor_errs(cfg, g, g_r)
+    assert max(errs.values()) <= 1e-4, errs
+    m.close()
+    with pytest.raises(v.VitError, match="head size 64"):
+        v.ViT.build(cfg, 1, v.VIT_BF16)
