@@ -239,10 +239,16 @@ def test_matmul_bf16(gpu, oracle64, M, N, K):
 
 
 # ------------------------------------------------------------------ fused bf16 attention
-@pytest.mark.parametrize("B,T,NH", [(2, 197, 3), (1, 1, 1), (2, 17, 2), (1, 64, 2), (1, 256, 1), (3, 33, 4)])
-def test_attention_fused_bf16(gpu, oracle64, B, T, NH):
+@pytest.mark.parametrize("B,T,NH,HS", [(2, 197, 3, 64), (1, 1, 1, 64), (2, 17, 2, 64), (1, 64, 2, 64),
+                                        (1, 256, 1, 64), (3, 33, 4, 64),
+                                        # generic VALU kernels: ViT-H/14 (hs 80, T 257), T > 256, hs 32 / 128
+                                        (2, 257, 2, 80), (1, 300, 1, 64), (2, 50, 3, 32), (1, 70, 1, 128),
+                                        (1, 1, 1, 80)])
+def test_attention_fused_bf16(gpu, oracle64, B, T, NH, HS):
+    """bf16 attention (fused MFMA kernels for head size 64 and T <= 256, generic kernels
+    otherwise) vs the fp64 oracle of the reference loops on the same bf16-rounded inputs."""
     v, o = gpu, oracle64
-    C = 64 * NH
+    C = HS * NH
     rng = np.random.default_rng(T * 7 + NH)
     qkv = rng.normal(size=B * T * 3 * C).astype(np.float32)
     qb = v.bf16_bits(qkv)
@@ -278,7 +284,7 @@ def test_error_channel(gpu):
     v = gpu
     out = Z(v, 64, np.uint16)
     with pytest.raises(v.VitError):
-        v.call("attention_forward_fused_bf16", out, Z(v, 64), Z(v, 3 * 64, np.uint16), 1, 1, 80, 1)
+        v.call("attention_forward_fused_bf16", out, Z(v, 64), Z(v, 3 * 81, np.uint16), 1, 1, 81, 1)
 
 
 # ------------------------------------------------------------------ generic bf16 GEMM engine

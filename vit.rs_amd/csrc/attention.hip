@@ -932,6 +932,234 @@ __global__ __launch_bounds__(1024) void attn_colsum_reduce_k(float* __restrict__
 }
 }  // namespace fa
 
+
+// ======================================================================= generic bf16 kernels
+// Shapes outside the fused kernels' tiling (head size != 64 or T > 256, e.g. ViT-H/14: hs = 80,
+// T = 257): the same math and the same outputs (O bf16, lse in the log2 domain, dqkv overwritten)
+// on the VALU.  One workgroup per ((b,h), row chunk) stages the head's two streamed operands in
+// LDS as bf16 (row stride hs+2 elements = an odd number of words, so lane-per-row reads are
+// conflict-free); each wave owns one row at a time, lanes over keys for the scores and over
+// head dims (d = lane, lane+64) for the products.  Correctness path, not the tuned one.
+namespace gen {
+constexpr int NW = 4;       // waves per workgroup
+constexpr int CHUNKS = 4;   // row chunks per (b,h)
+constexpr int HSMAX = 128;  // lanes own d = lane, lane + 64
+using fa::LOG2E;
+
+__host__ __device__ inline int stride(int hs) { return hs + 2; }
+__host__ inline size_t lds_bytes(int T, int hs) {
+    return (size_t)2 * T * stride(hs) * 2 + (size_t)NW * (2 * T + 3 * HSMAX) * 4 + (size_t)2 * T * 4;
+}
+
+__device__ __forceinline__ float dot_lds(const bf16_t* row, const float* v, int hs) {
+    const uint32_t* r = reinterpret_cast<const uint32_t*>(row);
+    float a = 0.f;
+    for (int i = 0; i < hs / 2; i++) {
+        const uint32_t w = r[i];
+        a += __uint_as_float(w << 16) * v[2 * i] + __uint_as_float(w & 0xffff0000u) * v[2 * i + 1];
+    }
+    return a;
+}
+
+// stage rows [0,T) of the operands at column offsets o0, o1 of qkv (head h of batch b)
+__device__ __forceinline__ void stage2(bf16_t* X0, bf16_t* X1, const bf16_t* base0,
+                                       const bf16_t* base1, long long ld, int T, int hs) {
+    const int st = stride(hs), hw = hs / 2;
+    for (int e = threadIdx.x; e < T * hw; e += blockDim.x) {
+        const int t = e / hw, i = e - t * hw;
+        reinterpret_cast<uint32_t*>(X0 + t * st)[i] = reinterpret_cast<const uint32_t*>(base0 + t * ld)[i];
+        reinterpret_cast<uint32_t*>(X1 + t * st)[i] = reinterpret_cast<const uint32_t*>(base1 + t * ld)[i];
+    }
+}
+
+__global__ __launch_bounds__(NW * 64) void fwd_k(bf16_t* __restrict__ out, float* __restrict__ lse,
+                                                  const bf16_t* __restrict__ qkv, int T, int C, int NH) {
+    extern __shared__ char lds[];
+    const int hs = C / NH, st = stride(hs);
+    const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const long long C3 = 3LL * C;
+    bf16_t* Ks = reinterpret_cast<bf16_t*>(lds);
+    bf16_t* Vs = Ks + T * st;
+    float* wb = reinterpret_cast<float*>(Vs + T * st) + w * (2 * T + 3 * HSMAX);
+    float* ps = wb;               // [T] probabilities
+    float* qv = wb + 2 * T;       // [hs] query row
+    const bf16_t* base = qkv + (long long)b * T * C3 + h * hs;
+    stage2(Ks, Vs, base + C, base + 2 * C, C3, T, hs);
+    __syncthreads();
+    const float c = LOG2E / sqrtf((float)hs);
+    for (int r0 = blockIdx.y * NW; r0 < T; r0 += CHUNKS * NW) {
+        const int t = r0 + w;
+        const bool live = t < T;  // wave-uniform; barriers below are hit by every wave
+        if (live)
+            for (int d = lane; d < hs; d += 64) qv[d] = bf2f(base[(long long)t * C3 + d]) * c;
+        __syncthreads();
+        float mx = -INFINITY, sum = 1.f;
+        if (live) {
+            for (int t2 = lane; t2 < T; t2 += 64) {
+                const float sc = dot_lds(Ks + t2 * st, qv, hs);
+                ps[t2] = sc;
+                mx = fmaxf(mx, sc);
+            }
+            mx = warp_max(mx);
+            sum = 0.f;
+            for (int t2 = lane; t2 < T; t2 += 64) {
+                const float p = exp2f(ps[t2] - mx);
+                ps[t2] = p;
+                sum += p;
+            }
+            sum = warp_sum(sum);
+        }
+        __syncthreads();
+        if (live) {
+            const float inv = 1.f / sum;
+            for (int d = lane; d < hs; d += 64) {
+                float o = 0.f;
+                for (int t2 = 0; t2 < T; t2++) o += ps[t2] * bf2f(Vs[t2 * st + d]);
+                out[((long long)b * T + t) * C + h * hs + d] = f2bf(o * inv);
+            }
+            if (lane == 0) lse[(long long)bh * T + t] = mx + log2f(sum);
+        }
+        __syncthreads();
+    }
+}
+
+// query side: delta = rowsum(dO*O) -> ws, dS row, dQ = scale * dS.K  (K, V staged)
+__global__ __launch_bounds__(NW * 64) void bwd_q_k(bf16_t* __restrict__ dqkv, float* __restrict__ delta,
+                                                    const bf16_t* __restrict__ dout,
+                                                    const bf16_t* __restrict__ qkv,
+                                                    const bf16_t* __restrict__ out,
+                                                    const float* __restrict__ lse, int T, int C, int NH) {
+    extern __shared__ char lds[];
+    const int hs = C / NH, st = stride(hs);
+    const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const long long C3 = 3LL * C;
+    bf16_t* Ks = reinterpret_cast<bf16_t*>(lds);
+    bf16_t* Vs = Ks + T * st;
+    float* wb = reinterpret_cast<float*>(Vs + T * st) + w * (2 * T + 3 * HSMAX);
+    float* ds = wb;
+    float* qv = wb + 2 * T;
+    float* gv = qv + HSMAX;
+    const bf16_t* base = qkv + (long long)b * T * C3 + h * hs;
+    stage2(Ks, Vs, base + C, base + 2 * C, C3, T, hs);
+    __syncthreads();
+    const float scale = 1.f / sqrtf((float)hs), c = LOG2E * scale;
+    for (int r0 = blockIdx.y * NW; r0 < T; r0 += CHUNKS * NW) {
+        const int t = r0 + w;
+        const bool live = t < T;  // wave-uniform; barriers below are hit by every wave
+        const long long row = (long long)b * T + t;
+        float dl = 0.f;
+        if (live) {
+            for (int d = lane; d < hs; d += 64) {
+                qv[d] = bf2f(base[(long long)t * C3 + d]) * c;
+                const float g = bf2f(dout[row * C + h * hs + d]);
+                gv[d] = g;
+                dl += g * bf2f(out[row * C + h * hs + d]);
+            }
+            dl = warp_sum(dl);
+        }
+        __syncthreads();
+        if (live) {
+            const float ls = lse[(long long)bh * T + t];
+            for (int t2 = lane; t2 < T; t2 += 64) {
+                const float p = exp2f(dot_lds(Ks + t2 * st, qv, hs) - ls);
+                const float dp = dot_lds(Vs + t2 * st, gv, hs);
+                ds[t2] = p * (dp - dl) * scale;
+            }
+            if (lane == 0) delta[(long long)bh * T + t] = dl;
+        }
+        __syncthreads();
+        if (live)
+            for (int d = lane; d < hs; d += 64) {
+                float a = 0.f;
+                for (int t2 = 0; t2 < T; t2++) a += ds[t2] * bf2f(Ks[t2 * st + d]);
+                dqkv[row * C3 + h * hs + d] = f2bf(a);
+            }
+        __syncthreads();
+    }
+}
+
+// key side: per key row t2, P and dS columns over all queries, dK = scale * dS^T.Q, dV = P^T.dO
+// (Q, dO staged; lse and delta of the head in LDS)
+__global__ __launch_bounds__(NW * 64) void bwd_kv_k(bf16_t* __restrict__ dqkv, const float* __restrict__ delta,
+                                                     const bf16_t* __restrict__ dout,
+                                                     const bf16_t* __restrict__ qkv,
+                                                     const float* __restrict__ lse, int T, int C, int NH) {
+    extern __shared__ char lds[];
+    const int hs = C / NH, st = stride(hs);
+    const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const long long C3 = 3LL * C;
+    bf16_t* Qs = reinterpret_cast<bf16_t*>(lds);
+    bf16_t* Gs = Qs + T * st;
+    float* wb = reinterpret_cast<float*>(Gs + T * st) + w * (2 * T + 3 * HSMAX);
+    float* ps = wb;
+    float* ds = wb + T;
+    float* kv = wb + 2 * T;
+    float* vv = kv + HSMAX;
+    float* ls_s = reinterpret_cast<float*>(Gs + T * st) + NW * (2 * T + 3 * HSMAX);
+    float* dl_s = ls_s + T;
+    const bf16_t* base = qkv + (long long)b * T * C3 + h * hs;
+    {
+        const int hw = hs / 2;
+        for (int e = threadIdx.x; e < T * hw; e += blockDim.x) {
+            const int t = e / hw, i = e - t * hw;
+            reinterpret_cast<uint32_t*>(Qs + t * st)[i] =
+                reinterpret_cast<const uint32_t*>(base + (long long)t * C3)[i];
+            reinterpret_cast<uint32_t*>(Gs + t * st)[i] =
+                reinterpret_cast<const uint32_t*>(dout + ((long long)b * T + t) * C + h * hs)[i];
+        }
+        for (int t = threadIdx.x; t < T; t += blockDim.x) {
+            ls_s[t] = lse[(long long)bh * T + t];
+            dl_s[t] = delta[(long long)bh * T + t];
+        }
+    }
+    __syncthreads();
+    const float scale = 1.f / sqrtf((float)hs), c = LOG2E * scale;
+    for (int r0 = blockIdx.y * NW; r0 < T; r0 += CHUNKS * NW) {
+        const int t2 = r0 + w;
+        const bool live = t2 < T;  // wave-uniform; barriers below are hit by every wave
+        const long long row = (long long)b * T + t2;
+        if (live)
+            for (int d = lane; d < hs; d += 64) {
+                kv[d] = bf2f(base[(long long)t2 * C3 + C + d]) * c;
+                vv[d] = bf2f(base[(long long)t2 * C3 + 2 * C + d]);
+            }
+        __syncthreads();
+        if (live)
+            for (int t = lane; t < T; t += 64) {
+                const float p = exp2f(dot_lds(Qs + t * st, kv, hs) - ls_s[t]);
+                const float dp = dot_lds(Gs + t * st, vv, hs);
+                ps[t] = p;
+                ds[t] = p * (dp - dl_s[t]) * scale;
+            }
+        __syncthreads();
+        if (live)
+            for (int d = lane; d < hs; d += 64) {
+                float dk = 0.f, dv = 0.f;
+                for (int t = 0; t < T; t++) {
+                    dk += ds[t] * bf2f(Qs[t * st + d]);
+                    dv += ps[t] * bf2f(Gs[t * st + d]);
+                }
+                dqkv[row * C3 + C + h * hs + d] = f2bf(dk);
+                dqkv[row * C3 + 2 * C + h * hs + d] = f2bf(dv);
+            }
+        __syncthreads();
+    }
+}
+}  // namespace gen
+
+bool attn_generic_supported(int T, int C, int NH) {
+    if (NH <= 0 || C % NH || T < 1) return false;
+    const int hs = C / NH;
+    return hs % 2 == 0 && hs <= gen::HSMAX && C % 2 == 0 && gen::lds_bytes(T, hs) <= 160 * 1024;
+}
+
+static bool gen_lds_attr(const void* k, size_t bytes) {
+    return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) == hipSuccess;
+}
+
 bool attn_fused_supported(int T, int C, int NH) {
     return NH > 0 && C % NH == 0 && C / NH == fa::HS && T >= 1 && T <= fa::TMAX && C % 8 == 0;
 }
@@ -965,7 +1193,14 @@ bool attn_fused_supported(int T, int C, int NH) {
 void attn_forward_fused(bf16_t* out, float* lse, const bf16_t* qkv, int B, int T, int C, int NH,
                         hipStream_t s) {
     if (!attn_fused_supported(T, C, NH)) {
-        set_error("attention_forward_fused: needs head size 64 and T<=256 (T=%d C=%d NH=%d)", T, C, NH);
+        if (!attn_generic_supported(T, C, NH)) {
+            set_error("attention_forward_fused: unsupported shape (T=%d C=%d NH=%d)", T, C, NH);
+            return;
+        }
+        const size_t lds = gen::lds_bytes(T, C / NH);
+        if (!gen_lds_attr((const void*)gen::fwd_k, lds)) { set_error("attention: LDS attribute"); return; }
+        gen::fwd_k<<<dim3(B * NH, gen::CHUNKS), gen::NW * 64, lds, s>>>(out, lse, qkv, T, C, NH);
+        after_launch("attention_forward_generic");
         return;
     }
     const int nkt = cdiv(T, 32) * 2;
@@ -978,7 +1213,24 @@ void attn_backward_fused(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, co
                          const float* lse, int B, int T, int C, int NH, hipStream_t s,
                          float* dqkv_colsum, float* ws) {
     if (!attn_fused_supported(T, C, NH)) {
-        set_error("attention_backward_fused: needs head size 64 and T<=256 (T=%d C=%d NH=%d)", T, C, NH);
+        if (!attn_generic_supported(T, C, NH)) {
+            set_error("attention_backward_fused: unsupported shape (T=%d C=%d NH=%d)", T, C, NH);
+            return;
+        }
+        // ws: [B*NH*T] delta = rowsum(dO*O)
+        const size_t need = (size_t)B * NH * T * sizeof(float);
+        if (!ws) ws = (float*)workspace(need);
+        if (!ws) return;
+        const size_t lds = gen::lds_bytes(T, C / NH);
+        if (!gen_lds_attr((const void*)gen::bwd_q_k, lds) || !gen_lds_attr((const void*)gen::bwd_kv_k, lds)) {
+            set_error("attention: LDS attribute");
+            return;
+        }
+        const dim3 g(B * NH, gen::CHUNKS);
+        gen::bwd_q_k<<<g, gen::NW * 64, lds, s>>>(dqkv, ws, dout, qkv, out, lse, T, C, NH);
+        gen::bwd_kv_k<<<g, gen::NW * 64, lds, s>>>(dqkv, ws, dout, qkv, lse, T, C, NH);
+        after_launch("attention_backward_generic");
+        if (dqkv_colsum) colsum_bf16(dqkv_colsum, dqkv, B * T, 3 * C, 3LL * C, s);
         return;
     }
     const int nkt = cdiv(T, 32) * 2;

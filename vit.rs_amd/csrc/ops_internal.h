@@ -49,6 +49,7 @@ void attn_backward_f32(float* dinp, float* dpreatt, float* datt, const float* do
                        const float* inp, const float* att, int B, int T, int C, int NH,
                        hipStream_t s);
 bool attn_fused_supported(int T, int C, int NH);
+bool attn_generic_supported(int T, int C, int NH);  // VALU bf16 kernels (other head sizes, T > 256)
 void attn_forward_fused(bf16_t* out, float* lse, const bf16_t* qkv, int B, int T, int C, int NH,
                         hipStream_t s);
 // dqkv_colsum (nullable, [3C]) += column sums of dqkv (the qkv bias gradient, fused)

@@ -226,6 +226,7 @@ struct Trainer {
     };
     std::vector<LayerActs> la;
     float* encoded = nullptr;
+    bool patch_f32 = false;  // bf16 mode, KP % 8 != 0: patch embedding on the fp32 GEMM
     bf16_t* patches_bf = nullptr;
     float* patches_f = nullptr;
     float* emb_tmp = nullptr;
@@ -472,13 +473,22 @@ struct Trainer {
         emb_tmp = alloc<float>((long long)B * NP * C);
         la.resize(L);
         if (prec == VIT_BF16) {
-            if (!attn_fused_supported(T, C, NH) || C % 8 || KP % 8) {
-                set_error("trainer: bf16 path needs head size 64, T<=256, C%%8==0 (T=%d C=%d NH=%d)", T, C, NH);
+            if (!(attn_fused_supported(T, C, NH) || attn_generic_supported(T, C, NH)) || C % 8) {
+                set_error("trainer: bf16 path needs an even head size <= 128 and C%%8==0 (T=%d C=%d NH=%d)", T, C, NH);
                 return false;
             }
+            // a patch whose im2col row (3*P*P) is not a multiple of 8 bf16 (ViT-H/14: 588) cannot
+            // feed the bf16 GEMM's 16-B loads: the patch embedding then runs on the fp32 GEMM
+            // (0.2 % of the step's flops) from the fp32 master weights
+            patch_f32 = KP % 8 != 0;
             pbf = alloc<bf16_t>(arena_elems);
             pbfT = alloc<bf16_t>(arena_elems);
-            patches_bf = alloc<bf16_t>((long long)B * NP * KP);
+            if (patch_f32) {
+                patches_f = alloc<float>((long long)B * NP * KP);
+                dpatch_f = alloc<float>((long long)B * NP * C);
+            } else {
+                patches_bf = alloc<bf16_t>((long long)B * NP * KP);
+            }
             for (int l = 0; l < L; l++) {
                 LayerActs& a = la[l];
                 a.ln1 = alloc<bf16_t>(BT * C);
@@ -501,7 +511,7 @@ struct Trainer {
             dfch = alloc<bf16_t>(BT * 4 * C);
             datty = alloc<bf16_t>(BT * C);
             dqkv = alloc<bf16_t>(BT * 3 * C);
-            dpatch_bf = alloc<bf16_t>((long long)B * NP * C);
+            if (!patch_f32) dpatch_bf = alloc<bf16_t>((long long)B * NP * C);
             // slabs: <= 32 splits of the largest weight gradient (4C x C)
             gemm_ws_bytes = (size_t)32 * 4 * C * (size_t)std::max(C, KP) * sizeof(float);
             gemm_ws = alloc<float>((long long)(gemm_ws_bytes / sizeof(float)));
@@ -653,13 +663,20 @@ struct Trainer {
             hipStream_t st = ms[mb];
             const long long img0 = (long long)mb * Bm;
             tbeg(TC_PATCH, 2.0 * Bm * NP * (double)KP * C, st);
-            im2col_bf16(patches_bf + img0 * NP * KP, pixels + img0 * 3 * cfg.img * cfg.img, Bm, cfg.img,
-                        cfg.patch, st);
             GemmArgs a;
-            a.A = patches_bf + img0 * NP * KP; a.lda = KP; a.B = W(P_PATCH_W); a.ldb = KP;
             a.C = emb_tmp + img0 * NP * C; a.ldc = C; a.bias = P(P_PATCH_B);
             a.M = Bm * NP; a.N = C; a.K = KP; a.epi = EPI_F32_STORE;
-            gemm_bf16(a, st);
+            if (patch_f32) {
+                im2col_f32(patches_f + img0 * NP * KP, pixels + img0 * 3 * cfg.img * cfg.img, Bm, cfg.img,
+                           cfg.patch, st);
+                a.A = patches_f + img0 * NP * KP; a.lda = KP; a.B = P(P_PATCH_W); a.ldb = KP;
+                gemm_f32(a, st);
+            } else {
+                im2col_bf16(patches_bf + img0 * NP * KP, pixels + img0 * 3 * cfg.img * cfg.img, Bm, cfg.img,
+                            cfg.patch, st);
+                a.A = patches_bf + img0 * NP * KP; a.lda = KP; a.B = W(P_PATCH_W); a.ldb = KP;
+                gemm_bf16(a, st);
+            }
             patch_assemble(encoded + img0 * T * C, emb_tmp + img0 * NP * C, P(P_CLS), P(P_WPE), Bm, NP, C, st);
             tend();
         }
@@ -794,7 +811,7 @@ struct Trainer {
                 tbeg(TC_ATTN_BWD, 8.0 * Bm * (double)T * T * C, ms[mb]);
                 attn_backward_fused(dqkv + r0 * 3 * C, datty + r0 * C, a.qkv + r0 * 3 * C, a.atty + r0 * C,
                                     a.lse + (long long)mb * Bm * NH * T, Bm, T, C, NH, ms[mb], G(P_QKVB, l),
-                                    attn_part + (long long)mb * Bm * NH * 3 * 64);
+                                    attn_part + (long long)mb * Bm * NH * (3 * 64 + T));
                 tend();
             }
             // qkv
@@ -823,8 +840,14 @@ struct Trainer {
         }
         // patch embedding backward (encoder_backward, train_vit.rs:371 -> ViT)
         tbeg(TC_PATCH_BWD, 2.0 * B * NP * (double)KP * C);
-        patch_gather_bf16(dpatch_bf, dcur, B, NP, C, s);
-        {
+        if (patch_f32) {
+            patch_gather_f32(dpatch_f, dcur, B, NP, C, s);
+            GemmArgs w;
+            w.A = dpatch_f; w.lda = C; w.a_kcontig = false; w.B = patches_f; w.ldb = KP; w.b_kcontig = false;
+            w.C = G(P_PATCH_W); w.ldc = KP; w.M = C; w.N = KP; w.K = B * NP; w.epi = EPI_F32_ATOMIC;
+            gemm_f32(w, s);
+        } else {
+            patch_gather_bf16(dpatch_bf, dcur, B, NP, C, s);
             GemmArgs w;
             w.A = dpatch_bf; w.lda = C; w.a_kcontig = false;
             w.B = patches_bf; w.ldb = KP; w.b_kcontig = false;
