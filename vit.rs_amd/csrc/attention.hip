@@ -941,211 +941,246 @@ __global__ __launch_bounds__(1024) void attn_colsum_reduce_k(float* __restrict__
 // conflict-free); each wave owns one row at a time, lanes over keys for the scores and over
 // head dims (d = lane, lane+64) for the products.  Correctness path, not the tuned one.
 namespace gen {
-constexpr int NW = 4;       // waves per workgroup
+// waves per workgroup: 16 for the forward up to hs 80 (123 VGPRs -> 4 waves/SIMD), 8 for the
+// backward kernels (~210 VGPRs -> 2 waves/SIMD); one workgroup per CU (the staged operands take
+// ~90 KiB of LDS at hs 80, T 257), so these wave counts are the latency hiding there is
+__host__ __device__ constexpr int nw_fwd(int hs) { return hs <= 80 ? 16 : 8; }
+__host__ __device__ constexpr int nw_bwd(int hs) { return hs <= 96 ? 8 : 4; }
 constexpr int CHUNKS = 4;   // row chunks per (b,h)
-constexpr int HSMAX = 128;  // lanes own d = lane, lane + 64
 using fa::LOG2E;
 
-__host__ __device__ inline int stride(int hs) { return hs + 2; }
-__host__ inline size_t lds_bytes(int T, int hs) {
-    return (size_t)2 * T * stride(hs) * 2 + (size_t)NW * (2 * T + 3 * HSMAX) * 4 + (size_t)2 * T * 4;
+// LDS row stride (elements): HS + 8 = an odd number of 16-B units, so lane-per-row b128 reads
+// are conflict-free
+__host__ __device__ constexpr int stride(int hs) { return hs + 8; }
+__host__ inline size_t lds_bytes(int T, int hs, int nw) {
+    return (size_t)2 * T * stride(hs) * 2 + (size_t)nw * 2 * T * 4 + (size_t)2 * T * 4;
 }
 
-__device__ __forceinline__ float dot_lds(const bf16_t* row, const float* v, int hs) {
-    const uint32_t* r = reinterpret_cast<const uint32_t*>(row);
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+// x[0..HS) (registers) . row[0..HS) (bf16, LDS or global), 8 elements per 16-B read
+// orders one wave's LDS writes before its other lanes read them (no workgroup barrier: the row
+// loops below have wave-dependent trip counts)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int HS>
+__device__ __forceinline__ float dot_row(const bf16_t* row, const float (&x)[HS]) {
     float a = 0.f;
-    for (int i = 0; i < hs / 2; i++) {
-        const uint32_t w = r[i];
-        a += __uint_as_float(w << 16) * v[2 * i] + __uint_as_float(w & 0xffff0000u) * v[2 * i + 1];
+#pragma unroll
+    for (int j = 0; j < HS / 8; j++) {
+        const u32x4_t w = *reinterpret_cast<const u32x4_t*>(row + 8 * j);
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            a += __uint_as_float(w[e] << 16) * x[8 * j + 2 * e];
+            a += __uint_as_float(w[e] & 0xffff0000u) * x[8 * j + 2 * e + 1];
+        }
     }
     return a;
 }
 
-// stage rows [0,T) of the operands at column offsets o0, o1 of qkv (head h of batch b)
-__device__ __forceinline__ void stage2(bf16_t* X0, bf16_t* X1, const bf16_t* base0,
-                                       const bf16_t* base1, long long ld, int T, int hs) {
-    const int st = stride(hs), hw = hs / 2;
-    for (int e = threadIdx.x; e < T * hw; e += blockDim.x) {
-        const int t = e / hw, i = e - t * hw;
-        reinterpret_cast<uint32_t*>(X0 + t * st)[i] = reinterpret_cast<const uint32_t*>(base0 + t * ld)[i];
-        reinterpret_cast<uint32_t*>(X1 + t * st)[i] = reinterpret_cast<const uint32_t*>(base1 + t * ld)[i];
+template <int HS>
+__device__ __forceinline__ void load_row(float (&x)[HS], const bf16_t* row, float scale) {
+#pragma unroll
+    for (int j = 0; j < HS / 8; j++) {
+        const u32x4_t w = *reinterpret_cast<const u32x4_t*>(row + 8 * j);
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            x[8 * j + 2 * e] = __uint_as_float(w[e] << 16) * scale;
+            x[8 * j + 2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u) * scale;
+        }
     }
 }
 
+// stage rows [0,T) of two [T][HS] bf16 operands (row strides ld0/ld1) into LDS, 16 B per copy
+template <int HS>
+__device__ __forceinline__ void stage2(bf16_t* X0, bf16_t* X1, const bf16_t* b0, long long ld0,
+                                       const bf16_t* b1, long long ld1, int T) {
+    constexpr int st = stride(HS), pr = HS / 8;
+    for (int e = threadIdx.x; e < T * pr; e += blockDim.x) {
+        const int t = e / pr, i = e - t * pr;
+        *reinterpret_cast<u32x4_t*>(X0 + t * st + 8 * i) = *reinterpret_cast<const u32x4_t*>(b0 + t * ld0 + 8 * i);
+        *reinterpret_cast<u32x4_t*>(X1 + t * st + 8 * i) = *reinterpret_cast<const u32x4_t*>(b1 + t * ld1 + 8 * i);
+    }
+}
+
+// lanes own a pair of head dims (2p, 2p+1) and a residue class of rows (lane / (HS/2)); the
+// partial sums over the classes are combined with xor shuffles.  out(d) = sum_t w[t] * X[t][d]
+template <int HS>
+struct Pairs {
+    static constexpr int NP = HS / 2;
+    static constexpr int NG = (64 % NP == 0) ? 64 / NP : 1;  // row classes
+    int p, g;
+    bool on;
+    __device__ Pairs(int lane) : p(lane % NP), g(lane / NP), on(lane < NP * NG) {}
+    __device__ __forceinline__ void acc(float& a0, float& a1, const float* w, const bf16_t* X, int T) const {
+        if (!on) return;
+        constexpr int st = stride(HS);
+        for (int t = g; t < T; t += NG) {
+            const uint32_t v = *reinterpret_cast<const uint32_t*>(X + t * st + 2 * p);
+            const float wt = w[t];
+            a0 += wt * __uint_as_float(v << 16);
+            a1 += wt * __uint_as_float(v & 0xffff0000u);
+        }
+    }
+    __device__ __forceinline__ void reduce(float& a0, float& a1) const {
+#pragma unroll
+        for (int o = NP; o < NP * NG; o <<= 1) {
+            a0 += __shfl_xor(a0, o, 64);
+            a1 += __shfl_xor(a1, o, 64);
+        }
+    }
+};
+
+template <int HS, int NW = nw_fwd(HS)>
 __global__ __launch_bounds__(NW * 64) void fwd_k(bf16_t* __restrict__ out, float* __restrict__ lse,
                                                   const bf16_t* __restrict__ qkv, int T, int C, int NH) {
     extern __shared__ char lds[];
-    const int hs = C / NH, st = stride(hs);
+    constexpr int st = stride(HS);
     const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const long long C3 = 3LL * C;
     bf16_t* Ks = reinterpret_cast<bf16_t*>(lds);
     bf16_t* Vs = Ks + T * st;
-    float* wb = reinterpret_cast<float*>(Vs + T * st) + w * (2 * T + 3 * HSMAX);
-    float* ps = wb;               // [T] probabilities
-    float* qv = wb + 2 * T;       // [hs] query row
-    const bf16_t* base = qkv + (long long)b * T * C3 + h * hs;
-    stage2(Ks, Vs, base + C, base + 2 * C, C3, T, hs);
+    float* ps = reinterpret_cast<float*>(Vs + T * st) + w * 2 * T;
+    const bf16_t* base = qkv + (long long)b * T * C3 + h * HS;
+    stage2<HS>(Ks, Vs, base + C, C3, base + 2 * C, C3, T);
     __syncthreads();
-    const float c = LOG2E / sqrtf((float)hs);
+    const Pairs<HS> pr(lane);
+    const float c = LOG2E / sqrtf((float)HS);
     for (int r0 = blockIdx.y * NW; r0 < T; r0 += CHUNKS * NW) {
         const int t = r0 + w;
-        const bool live = t < T;  // wave-uniform; barriers below are hit by every wave
-        if (live)
-            for (int d = lane; d < hs; d += 64) qv[d] = bf2f(base[(long long)t * C3 + d]) * c;
-        __syncthreads();
-        float mx = -INFINITY, sum = 1.f;
-        if (live) {
-            for (int t2 = lane; t2 < T; t2 += 64) {
-                const float sc = dot_lds(Ks + t2 * st, qv, hs);
-                ps[t2] = sc;
-                mx = fmaxf(mx, sc);
-            }
-            mx = warp_max(mx);
-            sum = 0.f;
-            for (int t2 = lane; t2 < T; t2 += 64) {
-                const float p = exp2f(ps[t2] - mx);
-                ps[t2] = p;
-                sum += p;
-            }
-            sum = warp_sum(sum);
+        if (t >= T) break;  // no barriers below: the rest of the loop is wave-local
+        float q[HS];
+        load_row<HS>(q, base + (long long)t * C3, c);
+        float mx = -INFINITY;
+        for (int t2 = lane; t2 < T; t2 += 64) {
+            const float sc = dot_row<HS>(Ks + t2 * st, q);
+            ps[t2] = sc;
+            mx = fmaxf(mx, sc);
         }
-        __syncthreads();
-        if (live) {
-            const float inv = 1.f / sum;
-            for (int d = lane; d < hs; d += 64) {
-                float o = 0.f;
-                for (int t2 = 0; t2 < T; t2++) o += ps[t2] * bf2f(Vs[t2 * st + d]);
-                out[((long long)b * T + t) * C + h * hs + d] = f2bf(o * inv);
-            }
-            if (lane == 0) lse[(long long)bh * T + t] = mx + log2f(sum);
+        mx = warp_max(mx);
+        float sum = 0.f;
+        for (int t2 = lane; t2 < T; t2 += 64) {
+            const float p = exp2f(ps[t2] - mx);
+            ps[t2] = p;
+            sum += p;
         }
-        __syncthreads();
+        sum = warp_sum(sum);
+        wave_lds_sync();
+        float o0 = 0.f, o1 = 0.f;
+        pr.acc(o0, o1, ps, Vs, T);
+        pr.reduce(o0, o1);
+        const float inv = 1.f / sum;
+        if (pr.on && pr.g == 0)
+            *reinterpret_cast<uint32_t*>(out + ((long long)b * T + t) * C + h * HS + 2 * pr.p) =
+                pack_bf16x2(o0 * inv, o1 * inv);
+        if (lane == 0) lse[(long long)bh * T + t] = mx + log2f(sum);
+        wave_lds_sync();  // ps is rewritten by the next row
     }
 }
 
 // query side: delta = rowsum(dO*O) -> ws, dS row, dQ = scale * dS.K  (K, V staged)
+template <int HS, int NW = nw_bwd(HS)>
 __global__ __launch_bounds__(NW * 64) void bwd_q_k(bf16_t* __restrict__ dqkv, float* __restrict__ delta,
                                                     const bf16_t* __restrict__ dout,
                                                     const bf16_t* __restrict__ qkv,
                                                     const bf16_t* __restrict__ out,
                                                     const float* __restrict__ lse, int T, int C, int NH) {
     extern __shared__ char lds[];
-    const int hs = C / NH, st = stride(hs);
+    constexpr int st = stride(HS);
     const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const long long C3 = 3LL * C;
     bf16_t* Ks = reinterpret_cast<bf16_t*>(lds);
     bf16_t* Vs = Ks + T * st;
-    float* wb = reinterpret_cast<float*>(Vs + T * st) + w * (2 * T + 3 * HSMAX);
-    float* ds = wb;
-    float* qv = wb + 2 * T;
-    float* gv = qv + HSMAX;
-    const bf16_t* base = qkv + (long long)b * T * C3 + h * hs;
-    stage2(Ks, Vs, base + C, base + 2 * C, C3, T, hs);
+    float* ds = reinterpret_cast<float*>(Vs + T * st) + w * 2 * T;
+    const bf16_t* base = qkv + (long long)b * T * C3 + h * HS;
+    stage2<HS>(Ks, Vs, base + C, C3, base + 2 * C, C3, T);
     __syncthreads();
-    const float scale = 1.f / sqrtf((float)hs), c = LOG2E * scale;
+    const Pairs<HS> pr(lane);
+    const float scale = 1.f / sqrtf((float)HS), c = LOG2E * scale;
     for (int r0 = blockIdx.y * NW; r0 < T; r0 += CHUNKS * NW) {
         const int t = r0 + w;
-        const bool live = t < T;  // wave-uniform; barriers below are hit by every wave
+        if (t >= T) break;
         const long long row = (long long)b * T + t;
+        float q[HS], g[HS];
+        load_row<HS>(q, base + (long long)t * C3, c);
+        load_row<HS>(g, dout + row * C + h * HS, 1.f);
         float dl = 0.f;
-        if (live) {
-            for (int d = lane; d < hs; d += 64) {
-                qv[d] = bf2f(base[(long long)t * C3 + d]) * c;
-                const float g = bf2f(dout[row * C + h * hs + d]);
-                gv[d] = g;
-                dl += g * bf2f(out[row * C + h * hs + d]);
-            }
-            dl = warp_sum(dl);
+        for (int d = lane; d < HS; d += 64) dl += bf2f(dout[row * C + h * HS + d]) * bf2f(out[row * C + h * HS + d]);
+        dl = warp_sum(dl);
+        const float ls = lse[(long long)bh * T + t];
+        for (int t2 = lane; t2 < T; t2 += 64) {
+            const float p = exp2f(dot_row<HS>(Ks + t2 * st, q) - ls);
+            const float dp = dot_row<HS>(Vs + t2 * st, g);
+            ds[t2] = p * (dp - dl) * scale;
         }
-        __syncthreads();
-        if (live) {
-            const float ls = lse[(long long)bh * T + t];
-            for (int t2 = lane; t2 < T; t2 += 64) {
-                const float p = exp2f(dot_lds(Ks + t2 * st, qv, hs) - ls);
-                const float dp = dot_lds(Vs + t2 * st, gv, hs);
-                ds[t2] = p * (dp - dl) * scale;
-            }
-            if (lane == 0) delta[(long long)bh * T + t] = dl;
-        }
-        __syncthreads();
-        if (live)
-            for (int d = lane; d < hs; d += 64) {
-                float a = 0.f;
-                for (int t2 = 0; t2 < T; t2++) a += ds[t2] * bf2f(Ks[t2 * st + d]);
-                dqkv[row * C3 + h * hs + d] = f2bf(a);
-            }
-        __syncthreads();
+        if (lane == 0) delta[(long long)bh * T + t] = dl;
+        wave_lds_sync();
+        float a0 = 0.f, a1 = 0.f;
+        pr.acc(a0, a1, ds, Ks, T);
+        pr.reduce(a0, a1);
+        if (pr.on && pr.g == 0)
+            *reinterpret_cast<uint32_t*>(dqkv + row * C3 + h * HS + 2 * pr.p) = pack_bf16x2(a0, a1);
+        wave_lds_sync();
     }
 }
 
 // key side: per key row t2, P and dS columns over all queries, dK = scale * dS^T.Q, dV = P^T.dO
 // (Q, dO staged; lse and delta of the head in LDS)
+template <int HS, int NW = nw_bwd(HS)>
 __global__ __launch_bounds__(NW * 64) void bwd_kv_k(bf16_t* __restrict__ dqkv, const float* __restrict__ delta,
                                                      const bf16_t* __restrict__ dout,
                                                      const bf16_t* __restrict__ qkv,
                                                      const float* __restrict__ lse, int T, int C, int NH) {
     extern __shared__ char lds[];
-    const int hs = C / NH, st = stride(hs);
+    constexpr int st = stride(HS);
     const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const long long C3 = 3LL * C;
     bf16_t* Qs = reinterpret_cast<bf16_t*>(lds);
     bf16_t* Gs = Qs + T * st;
-    float* wb = reinterpret_cast<float*>(Gs + T * st) + w * (2 * T + 3 * HSMAX);
-    float* ps = wb;
-    float* ds = wb + T;
-    float* kv = wb + 2 * T;
-    float* vv = kv + HSMAX;
-    float* ls_s = reinterpret_cast<float*>(Gs + T * st) + NW * (2 * T + 3 * HSMAX);
+    float* ps = reinterpret_cast<float*>(Gs + T * st) + w * 2 * T;
+    float* ds = ps + T;
+    float* ls_s = reinterpret_cast<float*>(Gs + T * st) + NW * 2 * T;
     float* dl_s = ls_s + T;
-    const bf16_t* base = qkv + (long long)b * T * C3 + h * hs;
-    {
-        const int hw = hs / 2;
-        for (int e = threadIdx.x; e < T * hw; e += blockDim.x) {
-            const int t = e / hw, i = e - t * hw;
-            reinterpret_cast<uint32_t*>(Qs + t * st)[i] =
-                reinterpret_cast<const uint32_t*>(base + (long long)t * C3)[i];
-            reinterpret_cast<uint32_t*>(Gs + t * st)[i] =
-                reinterpret_cast<const uint32_t*>(dout + ((long long)b * T + t) * C + h * hs)[i];
-        }
-        for (int t = threadIdx.x; t < T; t += blockDim.x) {
-            ls_s[t] = lse[(long long)bh * T + t];
-            dl_s[t] = delta[(long long)bh * T + t];
-        }
+    const bf16_t* base = qkv + (long long)b * T * C3 + h * HS;
+    stage2<HS>(Qs, Gs, base, C3, dout + (long long)b * T * C + h * HS, C, T);
+    for (int t = threadIdx.x; t < T; t += blockDim.x) {
+        ls_s[t] = lse[(long long)bh * T + t];
+        dl_s[t] = delta[(long long)bh * T + t];
     }
     __syncthreads();
-    const float scale = 1.f / sqrtf((float)hs), c = LOG2E * scale;
+    const Pairs<HS> pr(lane);
+    const float scale = 1.f / sqrtf((float)HS), c = LOG2E * scale;
     for (int r0 = blockIdx.y * NW; r0 < T; r0 += CHUNKS * NW) {
         const int t2 = r0 + w;
-        const bool live = t2 < T;  // wave-uniform; barriers below are hit by every wave
+        if (t2 >= T) break;
         const long long row = (long long)b * T + t2;
-        if (live)
-            for (int d = lane; d < hs; d += 64) {
-                kv[d] = bf2f(base[(long long)t2 * C3 + C + d]) * c;
-                vv[d] = bf2f(base[(long long)t2 * C3 + 2 * C + d]);
-            }
-        __syncthreads();
-        if (live)
-            for (int t = lane; t < T; t += 64) {
-                const float p = exp2f(dot_lds(Qs + t * st, kv, hs) - ls_s[t]);
-                const float dp = dot_lds(Gs + t * st, vv, hs);
-                ps[t] = p;
-                ds[t] = p * (dp - dl_s[t]) * scale;
-            }
-        __syncthreads();
-        if (live)
-            for (int d = lane; d < hs; d += 64) {
-                float dk = 0.f, dv = 0.f;
-                for (int t = 0; t < T; t++) {
-                    dk += ds[t] * bf2f(Qs[t * st + d]);
-                    dv += ps[t] * bf2f(Gs[t * st + d]);
-                }
-                dqkv[row * C3 + C + h * hs + d] = f2bf(dk);
-                dqkv[row * C3 + 2 * C + h * hs + d] = f2bf(dv);
-            }
-        __syncthreads();
+        float k[HS], v[HS];
+        load_row<HS>(k, base + (long long)t2 * C3 + C, c);
+        load_row<HS>(v, base + (long long)t2 * C3 + 2 * C, 1.f);
+        for (int t = lane; t < T; t += 64) {
+            const float p = exp2f(dot_row<HS>(Qs + t * st, k) - ls_s[t]);
+            const float dp = dot_row<HS>(Gs + t * st, v);
+            ps[t] = p;
+            ds[t] = p * (dp - dl_s[t]) * scale;
+        }
+        wave_lds_sync();
+        float k0 = 0.f, k1 = 0.f, v0 = 0.f, v1 = 0.f;
+        pr.acc(k0, k1, ds, Qs, T);
+        pr.acc(v0, v1, ps, Gs, T);
+        pr.reduce(k0, k1);
+        pr.reduce(v0, v1);
+        if (pr.on && pr.g == 0) {
+            *reinterpret_cast<uint32_t*>(dqkv + row * C3 + C + h * HS + 2 * pr.p) = pack_bf16x2(k0, k1);
+            *reinterpret_cast<uint32_t*>(dqkv + row * C3 + 2 * C + h * HS + 2 * pr.p) = pack_bf16x2(v0, v1);
+        }
+        wave_lds_sync();
     }
 }
 }  // namespace gen
@@ -1153,7 +1188,9 @@ __global__ __launch_bounds__(NW * 64) void bwd_kv_k(bf16_t* __restrict__ dqkv, c
 bool attn_generic_supported(int T, int C, int NH) {
     if (NH <= 0 || C % NH || T < 1) return false;
     const int hs = C / NH;
-    return hs % 2 == 0 && hs <= gen::HSMAX && C % 2 == 0 && gen::lds_bytes(T, hs) <= 160 * 1024;
+    const bool inst = hs == 32 || hs == 64 || hs == 80 || hs == 96 || hs == 128;  // template instances
+    return inst && C % 8 == 0 && gen::lds_bytes(T, hs, gen::nw_fwd(hs)) <= 160 * 1024 &&
+           gen::lds_bytes(T, hs, gen::nw_bwd(hs)) <= 160 * 1024;
 }
 
 static bool gen_lds_attr(const void* k, size_t bytes) {
@@ -1197,9 +1234,17 @@ void attn_forward_fused(bf16_t* out, float* lse, const bf16_t* qkv, int B, int T
             set_error("attention_forward_fused: unsupported shape (T=%d C=%d NH=%d)", T, C, NH);
             return;
         }
-        const size_t lds = gen::lds_bytes(T, C / NH);
-        if (!gen_lds_attr((const void*)gen::fwd_k, lds)) { set_error("attention: LDS attribute"); return; }
-        gen::fwd_k<<<dim3(B * NH, gen::CHUNKS), gen::NW * 64, lds, s>>>(out, lse, qkv, T, C, NH);
+        const size_t lds = gen::lds_bytes(T, C / NH, gen::nw_fwd(C / NH));
+        switch (C / NH) {
+#define VIT_GEN_FWD(HS)                                                                              \
+    case HS:                                                                                         \
+        if (!gen_lds_attr((const void*)gen::fwd_k<HS>, lds)) { set_error("attention: LDS attribute"); return; } \
+        gen::fwd_k<HS><<<dim3(B * NH, gen::CHUNKS), gen::nw_fwd(HS) * 64, lds, s>>>(out, lse, qkv, T, C, NH); \
+        break;
+            VIT_GEN_FWD(32) VIT_GEN_FWD(64) VIT_GEN_FWD(80) VIT_GEN_FWD(96) VIT_GEN_FWD(128)
+#undef VIT_GEN_FWD
+            default: set_error("attention: no generic kernel for head size %d", C / NH); return;
+        }
         after_launch("attention_forward_generic");
         return;
     }
@@ -1221,14 +1266,23 @@ void attn_backward_fused(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, co
         const size_t need = (size_t)B * NH * T * sizeof(float);
         if (!ws) ws = (float*)workspace(need);
         if (!ws) return;
-        const size_t lds = gen::lds_bytes(T, C / NH);
-        if (!gen_lds_attr((const void*)gen::bwd_q_k, lds) || !gen_lds_attr((const void*)gen::bwd_kv_k, lds)) {
-            set_error("attention: LDS attribute");
-            return;
-        }
+        const size_t lds = gen::lds_bytes(T, C / NH, gen::nw_bwd(C / NH));
         const dim3 g(B * NH, gen::CHUNKS);
-        gen::bwd_q_k<<<g, gen::NW * 64, lds, s>>>(dqkv, ws, dout, qkv, out, lse, T, C, NH);
-        gen::bwd_kv_k<<<g, gen::NW * 64, lds, s>>>(dqkv, ws, dout, qkv, lse, T, C, NH);
+        switch (C / NH) {
+#define VIT_GEN_BWD(HS)                                                                            \
+    case HS:                                                                                       \
+        if (!gen_lds_attr((const void*)gen::bwd_q_k<HS>, lds) ||                                   \
+            !gen_lds_attr((const void*)gen::bwd_kv_k<HS>, lds)) {                                  \
+            set_error("attention: LDS attribute");                                                 \
+            return;                                                                                \
+        }                                                                                          \
+        gen::bwd_q_k<HS><<<g, gen::nw_bwd(HS) * 64, lds, s>>>(dqkv, ws, dout, qkv, out, lse, T, C, NH);    \
+        gen::bwd_kv_k<HS><<<g, gen::nw_bwd(HS) * 64, lds, s>>>(dqkv, ws, dout, qkv, lse, T, C, NH);        \
+        break;
+            VIT_GEN_BWD(32) VIT_GEN_BWD(64) VIT_GEN_BWD(80) VIT_GEN_BWD(96) VIT_GEN_BWD(128)
+#undef VIT_GEN_BWD
+            default: set_error("attention: no generic kernel for head size %d", C / NH); return;
+        }
         after_launch("attention_backward_generic");
         if (dqkv_colsum) colsum_bf16(dqkv_colsum, dqkv, B * T, 3 * C, 3LL * C, s);
         return;
