@@ -1007,31 +1007,44 @@ __device__ __forceinline__ void stage2(bf16_t* X0, bf16_t* X1, const bf16_t* b0,
     }
 }
 
-// lanes own a pair of head dims (2p, 2p+1) and a residue class of rows (lane / (HS/2)); the
-// partial sums over the classes are combined with xor shuffles.  out(d) = sum_t w[t] * X[t][d]
+// lanes own four head dims (4p .. 4p+3) and a residue class of rows (g = lane / (HS/4)); the
+// partial sums of the NG classes are combined with lane permutes.  out(d) = sum_t w[t] * X[t][d]
 template <int HS>
 struct Pairs {
-    static constexpr int NP = HS / 2;
-    static constexpr int NG = (64 % NP == 0) ? 64 / NP : 1;  // row classes
+    static constexpr int NQ = HS / 4;
+    static constexpr int NG = 64 / NQ;  // row classes (3 at hs 80: lanes 60..63 idle)
     int p, g;
     bool on;
-    __device__ Pairs(int lane) : p(lane % NP), g(lane / NP), on(lane < NP * NG) {}
-    __device__ __forceinline__ void acc(float& a0, float& a1, const float* w, const bf16_t* X, int T) const {
+    __device__ Pairs(int lane) : p(lane % NQ), g(lane / NQ), on(lane < NQ * NG) {}
+    __device__ __forceinline__ void acc(f32x4_t& a, const float* w, const bf16_t* X, int T) const {
         if (!on) return;
         constexpr int st = stride(HS);
         for (int t = g; t < T; t += NG) {
-            const uint32_t v = *reinterpret_cast<const uint32_t*>(X + t * st + 2 * p);
+            const uint2 v = *reinterpret_cast<const uint2*>(X + t * st + 4 * p);
             const float wt = w[t];
-            a0 += wt * __uint_as_float(v << 16);
-            a1 += wt * __uint_as_float(v & 0xffff0000u);
+            a[0] += wt * __uint_as_float(v.x << 16);
+            a[1] += wt * __uint_as_float(v.x & 0xffff0000u);
+            a[2] += wt * __uint_as_float(v.y << 16);
+            a[3] += wt * __uint_as_float(v.y & 0xffff0000u);
         }
     }
-    __device__ __forceinline__ void reduce(float& a0, float& a1) const {
+    // after reduce, lanes with g == 0 hold the full sums
+    __device__ __forceinline__ void reduce(f32x4_t& a, int lane) const {
+        f32x4_t r = a;
 #pragma unroll
-        for (int o = NP; o < NP * NG; o <<= 1) {
-            a0 += __shfl_xor(a0, o, 64);
-            a1 += __shfl_xor(a1, o, 64);
+        for (int k = 1; k < NG; k++) {
+            const int src = (lane + k * NQ) & 63;
+#pragma unroll
+            for (int e = 0; e < 4; e++) r[e] += __shfl(a[e], src, 64);
         }
+        a = r;
+    }
+    __device__ __forceinline__ bool writer() const { return on && g == 0; }
+    __device__ __forceinline__ void store(bf16_t* dst, const f32x4_t& a, float scale) const {
+        uint2 o;
+        o.x = pack_bf16x2(a[0] * scale, a[1] * scale);
+        o.y = pack_bf16x2(a[2] * scale, a[3] * scale);
+        *reinterpret_cast<uint2*>(dst + 4 * p) = o;
     }
 };
 
@@ -1071,13 +1084,10 @@ __global__ __launch_bounds__(NW * 64) void fwd_k(bf16_t* __restrict__ out, float
         }
         sum = warp_sum(sum);
         wave_lds_sync();
-        float o0 = 0.f, o1 = 0.f;
-        pr.acc(o0, o1, ps, Vs, T);
-        pr.reduce(o0, o1);
-        const float inv = 1.f / sum;
-        if (pr.on && pr.g == 0)
-            *reinterpret_cast<uint32_t*>(out + ((long long)b * T + t) * C + h * HS + 2 * pr.p) =
-                pack_bf16x2(o0 * inv, o1 * inv);
+        f32x4_t o = {0.f, 0.f, 0.f, 0.f};
+        pr.acc(o, ps, Vs, T);
+        pr.reduce(o, lane);
+        if (pr.writer()) pr.store(out + ((long long)b * T + t) * C + h * HS, o, 1.f / sum);
         if (lane == 0) lse[(long long)bh * T + t] = mx + log2f(sum);
         wave_lds_sync();  // ps is rewritten by the next row
     }
@@ -1121,11 +1131,10 @@ __global__ __launch_bounds__(NW * 64) void bwd_q_k(bf16_t* __restrict__ dqkv, fl
         }
         if (lane == 0) delta[(long long)bh * T + t] = dl;
         wave_lds_sync();
-        float a0 = 0.f, a1 = 0.f;
-        pr.acc(a0, a1, ds, Ks, T);
-        pr.reduce(a0, a1);
-        if (pr.on && pr.g == 0)
-            *reinterpret_cast<uint32_t*>(dqkv + row * C3 + h * HS + 2 * pr.p) = pack_bf16x2(a0, a1);
+        f32x4_t a = {0.f, 0.f, 0.f, 0.f};
+        pr.acc(a, ds, Ks, T);
+        pr.reduce(a, lane);
+        if (pr.writer()) pr.store(dqkv + row * C3 + h * HS, a, 1.f);
         wave_lds_sync();
     }
 }
@@ -1171,14 +1180,14 @@ __global__ __launch_bounds__(NW * 64) void bwd_kv_k(bf16_t* __restrict__ dqkv, c
             ds[t] = p * (dp - dl_s[t]) * scale;
         }
         wave_lds_sync();
-        float k0 = 0.f, k1 = 0.f, v0 = 0.f, v1 = 0.f;
-        pr.acc(k0, k1, ds, Qs, T);
-        pr.acc(v0, v1, ps, Gs, T);
-        pr.reduce(k0, k1);
-        pr.reduce(v0, v1);
-        if (pr.on && pr.g == 0) {
-            *reinterpret_cast<uint32_t*>(dqkv + row * C3 + C + h * HS + 2 * pr.p) = pack_bf16x2(k0, k1);
-            *reinterpret_cast<uint32_t*>(dqkv + row * C3 + 2 * C + h * HS + 2 * pr.p) = pack_bf16x2(v0, v1);
+        f32x4_t ka = {0.f, 0.f, 0.f, 0.f}, va = {0.f, 0.f, 0.f, 0.f};
+        pr.acc(ka, ds, Qs, T);
+        pr.acc(va, ps, Gs, T);
+        pr.reduce(ka, lane);
+        pr.reduce(va, lane);
+        if (pr.writer()) {
+            pr.store(dqkv + row * C3 + C + h * HS, ka, 1.f);
+            pr.store(dqkv + row * C3 + 2 * C + h * HS, va, 1.f);
         }
         wave_lds_sync();
     }
