@@ -109,7 +109,9 @@ void matmul_backward_bf16(float* dinp, float* dweight, float* dbias, const uint1
                           const uint16_t* inp, const uint16_t* weight, int B, int T, int C,
                           int OC);
 /* fused attention: out_bf16 [B,T,C], lse [B,NH,T] (log2 domain), no T x T HBM traffic.
- * head size must be 64 and T <= 256. */
+ * Head size 64 with T <= 256 runs the MFMA kernels; head sizes 32/80/96/128 or T > 256 (e.g.
+ * ViT-H/14: hs 80, T 257) run generic VALU kernels with the same outputs; other shapes set
+ * vit_last_error. */
 void attention_forward_fused_bf16(uint16_t* out, float* lse, const uint16_t* inp,
                                   int B, int T, int C, int NH);
 /* dinp_bf16 [B,T,3C] is OVERWRITTEN (it is produced whole); recomputes P from lse */
