@@ -1016,16 +1016,38 @@ struct Pairs {
     int p, g;
     bool on;
     __device__ Pairs(int lane) : p(lane % NQ), g(lane / NQ), on(lane < NQ * NG) {}
+    __device__ __forceinline__ static void fma4(f32x4_t& a, float wt, uint2 v) {
+        a[0] += wt * __uint_as_float(v.x << 16);
+        a[1] += wt * __uint_as_float(v.x & 0xffff0000u);
+        a[2] += wt * __uint_as_float(v.y << 16);
+        a[3] += wt * __uint_as_float(v.y & 0xffff0000u);
+    }
+    // two rows per iteration into separate accumulators (independent LDS loads and FMA chains)
     __device__ __forceinline__ void acc(f32x4_t& a, const float* w, const bf16_t* X, int T) const {
         if (!on) return;
         constexpr int st = stride(HS);
+        f32x4_t b = {0.f, 0.f, 0.f, 0.f};
+        int t = g;
+        for (; t + NG < T; t += 2 * NG) {
+            const uint2 v0 = *reinterpret_cast<const uint2*>(X + t * st + 4 * p);
+            const uint2 v1 = *reinterpret_cast<const uint2*>(X + (t + NG) * st + 4 * p);
+            const float w0 = w[t], w1 = w[t + NG];
+            fma4(a, w0, v0);
+            fma4(b, w1, v1);
+        }
+        if (t < T) fma4(a, w[t], *reinterpret_cast<const uint2*>(X + t * st + 4 * p));
+        a += b;
+    }
+    // a += sum_t wa[t] Xa[t], b += sum_t wb[t] Xb[t] in one pass (the key side's dK and dV)
+    __device__ __forceinline__ void acc2(f32x4_t& a, const float* wa, const bf16_t* Xa, f32x4_t& b,
+                                         const float* wb, const bf16_t* Xb, int T) const {
+        if (!on) return;
+        constexpr int st = stride(HS);
         for (int t = g; t < T; t += NG) {
-            const uint2 v = *reinterpret_cast<const uint2*>(X + t * st + 4 * p);
-            const float wt = w[t];
-            a[0] += wt * __uint_as_float(v.x << 16);
-            a[1] += wt * __uint_as_float(v.x & 0xffff0000u);
-            a[2] += wt * __uint_as_float(v.y << 16);
-            a[3] += wt * __uint_as_float(v.y & 0xffff0000u);
+            const uint2 va = *reinterpret_cast<const uint2*>(Xa + t * st + 4 * p);
+            const uint2 vb = *reinterpret_cast<const uint2*>(Xb + t * st + 4 * p);
+            fma4(a, wa[t], va);
+            fma4(b, wb[t], vb);
         }
     }
     // after reduce, lanes with g == 0 hold the full sums
@@ -1181,8 +1203,7 @@ __global__ __launch_bounds__(NW * 64) void bwd_kv_k(bf16_t* __restrict__ dqkv, c
         }
         wave_lds_sync();
         f32x4_t ka = {0.f, 0.f, 0.f, 0.f}, va = {0.f, 0.f, 0.f, 0.f};
-        pr.acc(ka, ds, Qs, T);
-        pr.acc(va, ps, Gs, T);
+        pr.acc2(ka, ds, Qs, va, ps, Gs, T);
         pr.reduce(ka, lane);
         pr.reduce(va, lane);
         if (pr.writer()) {
