@@ -18,6 +18,9 @@
  *                 materialised attention) — the parity path (<= 1e-4 rel vs the CPU oracle).
  *   VIT_BF16 (1): the fast path — bf16 MFMA GEMMs with fused epilogues, fused attention,
  *                 fp32 master weights / gradients / residual stream / LN statistics.
+ *                 Head size 64 with T <= 256 uses the MFMA attention; head sizes 32/80/96/128
+ *                 or T > 256 (ViT-H/14) use generic VALU attention kernels, and a patch whose
+ *                 3*P*P is not a multiple of 8 runs the patch embedding on the fp32 GEMM.
  * All calls are asynchronous on the trainer's stream unless noted; functions returning int
  * return 0 on success (details via vit_last_error()).
  */
