@@ -56,7 +56,8 @@ void residual_forward(float* out, const float* inp1, const float* inp2, int N);
 /* train_vit.rs:384 — out[BT,OC] = inp[BT,C] . weight[OC,C]^T + bias */
 void matmul_forward(float* out, const float* inp, const float* weight, const float* bias,
                     int B, int T, int C, int OC);
-/* train_vit.rs:400 (+ attention.rs:1) — preatt/att [B,T,NH,T] are required (drop-in mode) */
+/* train_vit.rs:400 (+ attention.rs:1) — preatt/att [B,T,NH,T] are materialised like the
+ * reference; either may be NULL (fused use: the scores are then not stored) */
 void attention_forward(float* out, float* preatt, float* att, const float* inp,
                        int B, int T, int C, int NH);
 /* train_vit.rs:453 */
@@ -109,9 +110,11 @@ void matmul_backward_bf16(float* dinp, float* dweight, float* dbias, const uint1
                           const uint16_t* inp, const uint16_t* weight, int B, int T, int C,
                           int OC);
 /* fused attention: out_bf16 [B,T,C], lse [B,NH,T] (log2 domain), no T x T HBM traffic.
- * Head size 64 with T <= 256 runs the MFMA kernels; head sizes 32/80/96/128 or T > 256 (e.g.
- * ViT-H/14: hs 80, T 257) run generic VALU kernels with the same outputs; other shapes set
- * vit_last_error. */
+ * Head sizes 32/64/80/96/128 run the MFMA kernels while the head's operands fit the LDS
+ * (T <= 320; <= 288 at head size 128), e.g. ViT-B/16 (hs 64, T 197) and ViT-H/14 (hs 80,
+ * T 257); longer sequences run generic VALU kernels with the same outputs; other shapes set
+ * vit_last_error.  vit_attention_kernel_kind: 1 = MFMA, 2 = generic, 0 = unsupported. */
+int vit_attention_kernel_kind(int T, int C, int NH);
 void attention_forward_fused_bf16(uint16_t* out, float* lse, const uint16_t* inp,
                                   int B, int T, int C, int NH);
 /* dinp_bf16 [B,T,3C] is OVERWRITTEN (it is produced whole); recomputes P from lse */

@@ -239,16 +239,26 @@ def test_matmul_bf16(gpu, oracle64, M, N, K):
 
 
 # ------------------------------------------------------------------ fused bf16 attention
-@pytest.mark.parametrize("B,T,NH,HS", [(2, 197, 3, 64), (1, 1, 1, 64), (2, 17, 2, 64), (1, 64, 2, 64),
-                                        (1, 256, 1, 64), (3, 33, 4, 64),
-                                        # generic VALU kernels: ViT-H/14 (hs 80, T 257), T > 256, hs 32 / 128
-                                        (2, 257, 2, 80), (1, 300, 1, 64), (2, 50, 3, 32), (1, 70, 1, 128),
-                                        (1, 1, 1, 80)])
-def test_attention_fused_bf16(gpu, oracle64, B, T, NH, HS):
-    """bf16 attention (fused MFMA kernels for head size 64 and T <= 256, generic kernels
-    otherwise) vs the fp64 oracle of the reference loops on the same bf16-rounded inputs."""
+@pytest.mark.parametrize("B,T,NH,HS,path", [
+    (2, 197, 3, 64, "mfma"), (1, 1, 1, 64, "mfma"), (2, 17, 2, 64, "mfma"), (1, 64, 2, 64, "mfma"),
+    (1, 256, 1, 64, "mfma"), (3, 33, 4, 64, "mfma"), (1, 300, 1, 64, "mfma"),
+    # the other head sizes on the MFMA kernels: ViT-H/14 (hs 80, T 257), hs 32 / 96 / 128
+    (2, 257, 2, 80, "mfma"), (1, 1, 1, 80, "mfma"), (2, 50, 3, 32, "mfma"), (1, 70, 2, 96, "mfma"),
+    (1, 70, 1, 128, "mfma"), (1, 288, 1, 128, "mfma"),
+    # past the LDS range (T > 320): the generic VALU kernels
+    (1, 330, 1, 64, "auto"), (1, 400, 2, 32, "auto"),
+    # the generic kernels forced on shapes the MFMA kernels also take (same outputs)
+    (2, 257, 2, 80, "generic"), (1, 70, 2, 96, "generic")])
+def test_attention_fused_bf16(gpu, oracle64, monkeypatch, B, T, NH, HS, path):
+    """bf16 attention (fused MFMA kernels for head sizes 32/64/80/96/128 while the head's images fit
+    the LDS, generic VALU kernels past that) vs the fp64 oracle of the reference loops on the same
+    bf16-rounded inputs."""
+    if path == "generic":
+        monkeypatch.setenv("VIT_ATTN_GENERIC", "1")
     v, o = gpu, oracle64
     C = HS * NH
+    kind = v.lib().vit_attention_kernel_kind(T, C, NH)
+    assert kind == {"mfma": 1, "generic": 2}.get(path, 2), (path, kind)
     rng = np.random.default_rng(T * 7 + NH)
     qkv = rng.normal(size=B * T * 3 * C).astype(np.float32)
     qb = v.bf16_bits(qkv)

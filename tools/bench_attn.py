@@ -1,5 +1,6 @@
-"""Microbenchmark of the fused bf16 attention kernels at ViT-B/16 B=256 (HIP events).
-    python tools/bench_attn.py [--iters 10] [--batch 256]"""
+"""Microbenchmark of the fused bf16 attention kernels (HIP events); default ViT-B/16 B=256.
+    python tools/bench_attn.py [--iters 10] [--batch 256] [--T 197] [--NH 12] [--hs 64] [--generic]
+    ViT-H/14 B=128: --batch 128 --T 257 --NH 16 --hs 80"""
 import argparse
 import os
 import sys
@@ -16,11 +17,16 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--T", type=int, default=197)
     ap.add_argument("--NH", type=int, default=12)
+    ap.add_argument("--hs", type=int, default=64)
+    ap.add_argument("--generic", action="store_true", help="force the generic VALU kernels")
     args = ap.parse_args()
+    if args.generic:
+        os.environ["VIT_ATTN_GENERIC"] = "1"
     L = vit.lib()
     assert L.vit_init(0) == 0
     B, T, NH = args.batch, args.T, args.NH
-    C = 64 * NH
+    C = args.hs * NH
+    kind = {1: "mfma", 2: "generic"}.get(L.vit_attention_kernel_kind(T, C, NH), "unsupported")
     rng = np.random.default_rng(0)
     qkv = vit.DeviceArray.from_numpy(vit.bf16_bits(rng.normal(size=B * T * 3 * C).astype(np.float32)), np.uint16)
     dout = vit.DeviceArray.from_numpy(vit.bf16_bits(rng.normal(size=B * T * C).astype(np.float32)), np.uint16)
@@ -42,7 +48,7 @@ def main():
         L.vit_event_record(e1)
         ms = L.vit_event_elapsed_ms(e0, e1) / args.iters
         vit.check(name)
-        print(f"attention {name}: {ms * 1e3:8.1f} us  {fl / ms / 1e9:7.1f} TFLOP/s", flush=True)
+        print(f"attention {name} [{kind} B={B} T={T} NH={NH} hs={args.hs}]: {ms * 1e3:8.1f} us  {fl / ms / 1e9:7.1f} TFLOP/s", flush=True)
 
 
 if __name__ == "__main__":

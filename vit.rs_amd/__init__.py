@@ -92,6 +92,7 @@ _SIGS = {
     "matmul_forward_bf16": (None, [P, P, P, P, I, I, I, I]),
     "matmul_backward_bf16": (None, [P, P, P, P, P, P, I, I, I, I]),
     "attention_forward_fused_bf16": (None, [P, P, P, I, I, I, I]),
+    "vit_attention_kernel_kind": (I, [I, I, I]),
     "attention_backward_fused_bf16": (None, [P, P, P, P, P, I, I, I, I]),
     "layernorm_forward_bf16": (None, [P, P, P, P, P, P, I, I, I]),
     "gemm_bf16_ex": (None, [P, LL, P, LL, I, P, LL, I, P, P, I, I, I, I, I]),

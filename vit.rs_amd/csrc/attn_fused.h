@@ -1,0 +1,636 @@
+// attn_fused.h — fused bf16 MFMA attention (attention_forward / attention_backward,
+// /root/reference/train_vit.rs:400-451, 559-601; attention.rs:1-57) for any head size HS in
+// {32, 64, 80, 96, 128} and T up to what the LDS holds.  Fixes D1 (offsets by T), D2 (full
+// normalisation), D3 (non-causal).  Instantiated per head size by attn_h*.hip (parallel builds).
+//
+// One workgroup per (b,h) holds the head's operands in LDS; scores never touch HBM.
+//   forward : per 16-query tile, S^T = K.Q^T with v_mfma_f32_16x16x32_bf16 so each lane owns one
+//             query column (lane&15) -> row max/sum need only two cross-lane shuffles; the fp32
+//             score accumulators convert in place into the B operand of O^T = V^T.P^T (k = 4g+j |
+//             16+4g+j on both operands), V read with ds_read_b64_tr_b16.  Writes O (bf16) and lse
+//             (log2 domain) per query.
+//   backward: two roles of one launch (kv: 32 keys per wave, dK^T, dV^T; q: 32 queries per wave,
+//             dQ^T), P recomputed from lse, dS = P (dP - delta) with delta = rowsum(dO*O), the
+//             O(T^2) form of the reference's O(T^3) softmax Jacobian loop (train_vit.rs:583-589).
+// Head dims: the score products run k-steps of 32 over the head dim; when HS % 32 == 16 (HS 80,
+// 96 is a multiple of 32) the last k-step's upper half (d = HS .. HS+15) is zero IN REGISTERS on
+// both operands, so the images need no padding columns and nothing past column HS is read.  The
+// output products tile the head dim by 16 (HS/16 tiles).  Rows >= T of every image are zero;
+// the padded length TP is a multiple of 32.
+#pragma once
+#include "ops_internal.h"
+
+namespace vit {
+namespace fa {
+
+constexpr float LOG2E = 1.4426950408889634f;
+
+template <int HS>
+struct Geo {
+    static_assert(HS % 16 == 0 && HS >= 32 && HS <= 128, "head size");
+    static constexpr int KS = (HS + 31) / 32;      // 32-deep k-steps over the head dim
+    static constexpr bool HALF = (HS % 32) != 0;   // last k-step: upper 16 are zero padding
+    static constexpr int DT = HS / 16;             // 16-wide output tiles of the head dim
+    static constexpr int CH = HS / 8;              // 16-B chunks per image row
+    // row-read image stride: (SK/2) = 4*odd (mod 64) dwords -> 16 rows x 2 lane groups of b64
+    // reads cover 64 distinct banks (HS + 8 satisfies it for every supported HS)
+    static constexpr int SK = HS + 8;
+    // transposed-read-only image stride: (SV/2) = 8*odd (mod 64) dwords -> the 8 rows x 32 B of a
+    // ds_read_b64_tr_b16 lane group hit distinct banks
+    static constexpr int SV = HS == 32 ? 48 : HS == 64 ? 80 : HS == 80 ? 80 : HS == 96 ? 112 : 144;
+};
+
+// 8 bf16 of rows r0+i for k-step s (k = 32s + 4g + j | 32s + 16 + 4g + j - 4)
+template <int HS>
+__device__ __forceinline__ bf16x8_t frag_row(const bf16_t* img, int stride, int r0, int s, int lane) {
+    const int i = lane & 15, g = lane >> 4;
+    const bf16_t* p = img + (r0 + i) * stride + 32 * s + 4 * g;
+    const bf16x4_t lo = *reinterpret_cast<const bf16x4_t*>(p);
+    bf16x4_t hi = {};
+    if (!(Geo<HS>::HALF && s == Geo<HS>::KS - 1)) hi = *reinterpret_cast<const bf16x4_t*>(p + 16);
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+// the same fragment straight from a [T][ld] global operand (rows >= T -> 0)
+template <int HS>
+__device__ __forceinline__ bf16x8_t frag_glb(const bf16_t* base, long long ld, int row, int T, int s, int lane) {
+    const int g = lane >> 4;
+    bf16x4_t lo = {}, hi = {};
+    if (row < T) {
+        const bf16_t* p = base + (long long)row * ld + 32 * s + 4 * g;
+        lo = *reinterpret_cast<const bf16x4_t*>(p);
+        if (!(Geo<HS>::HALF && s == Geo<HS>::KS - 1)) hi = *reinterpret_cast<const bf16x4_t*>(p + 16);
+    }
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+// transposed: k = rows kb + (4g+j | 16+4g+j-4), column c0 + i
+__device__ __forceinline__ bf16x8_t frag_tr(const bf16_t* img, int stride, int kb, int c0, int lane) {
+    const int i = lane & 15, g = lane >> 4;
+    const bf16_t* p = img + (kb + 4 * g + (i >> 2)) * stride + c0 + 4 * (i & 3);
+    const bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4_t, p));
+    const bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4_t, p + 16 * stride));
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+// two 16-row accumulator tiles (rows 4g+r) -> one 32-deep operand with the shared permutation
+__device__ __forceinline__ bf16x8_t pack_acc(f32x4_t a, f32x4_t b) {
+    bf16x8_t r;
+    r[0] = (__bf16)a[0]; r[1] = (__bf16)a[1]; r[2] = (__bf16)a[2]; r[3] = (__bf16)a[3];
+    r[4] = (__bf16)b[0]; r[5] = (__bf16)b[1]; r[6] = (__bf16)b[2]; r[7] = (__bf16)b[3];
+    return r;
+}
+// v_exp_f32 (2^x, ~1 ulp; results below 2^-126 flush to 0, irrelevant for probabilities that
+// are rounded to bf16); exp2f adds a denormal range-reduction sequence around it
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ f32x4_t mfma(bf16x8_t a, bf16x8_t b, f32x4_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// rows of HS bf16 (HS/8 x 16 B each, rows >= T zero-filled) of NOP operands into their LDS images.
+// Every global load of the thread is issued before its first LDS store, so the whole staging is
+// one memory round trip.
+template <int HS, int TP, int NTHR, int NOP>
+__device__ __forceinline__ void load_images(bf16_t* const (&img)[NOP], const int (&stride)[NOP],
+                                            const bf16_t* const (&src)[NOP],
+                                            const long long (&ld)[NOP], int T) {
+    constexpr int CH = Geo<HS>::CH;
+    constexpr int PER = (TP * CH + NTHR - 1) / NTHR;
+    uint4 v[NOP][PER];
+#pragma unroll
+    for (int o = 0; o < NOP; o++)
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            const int idx = j * NTHR + (int)threadIdx.x, t = idx / CH, c = idx - t * CH;
+            v[o][j] = make_uint4(0, 0, 0, 0);
+            if (idx < TP * CH && t < T) v[o][j] = *reinterpret_cast<const uint4*>(src[o] + (long long)t * ld[o] + c * 8);
+        }
+#pragma unroll
+    for (int o = 0; o < NOP; o++)
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            const int idx = j * NTHR + (int)threadIdx.x, t = idx / CH, c = idx - t * CH;
+            if (idx < TP * CH) *reinterpret_cast<uint4*>(img[o] + t * stride[o] + c * 8) = v[o][j];
+        }
+}
+__device__ __forceinline__ void store4(bf16_t* dst, f32x4_t v, float mul) {
+    *reinterpret_cast<uint2*>(dst) =
+        make_uint2(pack_bf16x2(v[0] * mul, v[1] * mul), pack_bf16x2(v[2] * mul, v[3] * mul));
+}
+
+// ---------------------------------------------------------------------------------- forward
+template <int HS, int NKT>  // key tiles of 16 covering TP = 16*NKT (a multiple of 32)
+constexpr int fwd_lds_bytes() { return NKT * 16 * (Geo<HS>::SK + Geo<HS>::SV) * 2; }
+// workgroups per CU the forward's LDS allows (launch bound)
+template <int HS, int NKT>
+constexpr int fwd_occ() { return fwd_lds_bytes<HS, NKT>() <= 80 * 1024 ? 2 : 1; }
+
+template <int HS, int NKT>
+__global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* __restrict__ out,
+                                                                        float* __restrict__ lse,
+                                                                        const bf16_t* __restrict__ qkv,
+                                                                        int T, int C, int NH) {
+    using G = Geo<HS>;
+    constexpr int TP = NKT * 16;
+    __shared__ __attribute__((aligned(16))) bf16_t Ks[TP * G::SK];
+    __shared__ __attribute__((aligned(16))) bf16_t Vs[TP * G::SV];
+    const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
+    const long long C3 = 3LL * C;
+    const bf16_t* base = qkv + (long long)b * T * C3 + h * HS;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, g = lane >> 4;
+    // Q fragments of a 16-query tile straight from HBM (rows >= T -> 0); the next tile's are
+    // requested while the current one computes, the first ones before the K/V staging
+    auto load_q = [&](int qt, bf16x8_t (&qf)[G::KS]) {
+#pragma unroll
+        for (int s = 0; s < G::KS; s++) qf[s] = frag_glb<HS>(base, C3, qt * 16 + i, T, s, lane);
+    };
+    const int nqt = (T + 15) / 16;
+    bf16x8_t qn[G::KS];
+    load_q(w, qn);
+    {
+        bf16_t* const img[2] = {Ks, Vs};
+        const int st[2] = {G::SK, G::SV};
+        const bf16_t* const src[2] = {base + C, base + 2 * C};
+        const long long ld[2] = {C3, C3};
+        load_images<HS, TP, 256, 2>(img, st, src, ld, T);
+    }
+    __syncthreads();
+    const float c = LOG2E / sqrtf((float)HS);
+    for (int qt = w; qt < nqt; qt += 4) {
+        const int q = qt * 16 + i;
+        bf16x8_t qf[G::KS];
+#pragma unroll
+        for (int s = 0; s < G::KS; s++) qf[s] = qn[s];
+        if (qt + 4 < nqt) load_q(qt + 4, qn);
+        f32x4_t sacc[NKT];
+#pragma unroll
+        for (int kt = 0; kt < NKT; kt++) {
+            f32x4_t a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < G::KS; s++) a = mfma(frag_row<HS>(Ks, G::SK, kt * 16, s, lane), qf[s], a);
+            sacc[kt] = a;
+        }
+        // lane (i,g) holds S^T[key = 16kt+4g+r][q]
+        float mx = -INFINITY;
+#pragma unroll
+        for (int kt = 0; kt < NKT; kt++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int key = kt * 16 + 4 * g + r;
+                const float x = key < T ? sacc[kt][r] * c : -INFINITY;
+                sacc[kt][r] = x;
+                mx = fmaxf(mx, x);
+            }
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        float l = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < NKT; kt++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const float p = fexp2(sacc[kt][r] - mx);
+                sacc[kt][r] = p;
+                l += p;
+            }
+        l += __shfl_xor(l, 16, 64);
+        l += __shfl_xor(l, 32, 64);
+        f32x4_t o[G::DT];
+#pragma unroll
+        for (int dt = 0; dt < G::DT; dt++) o[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < NKT / 2; ks++) {
+            const bf16x8_t pb = pack_acc(sacc[2 * ks], sacc[2 * ks + 1]);
+#pragma unroll
+            for (int dt = 0; dt < G::DT; dt++) o[dt] = mfma(frag_tr(Vs, G::SV, 32 * ks, 16 * dt, lane), pb, o[dt]);
+        }
+        if (q < T) {
+            const float inv = 1.0f / l;
+            bf16_t* dst = out + ((long long)b * T + q) * C + h * HS + 4 * g;
+#pragma unroll
+            for (int dt = 0; dt < G::DT; dt++) store4(dst + 16 * dt, o[dt], inv);
+            if (g == 0) lse[(long long)bh * T + q] = mx + log2f(l);
+        }
+    }
+}
+
+// --------------------------------------------------------------------------------- backward
+// Two roles of one launch with 32-row register tiles (bwd_kv_body and bwd_q_body), a 256-thread
+// workgroup per (b,h) and role.  Each fragment read from LDS feeds two 16-row MFMA tiles:
+//   kv: wave owns 32 keys (K, V fragments in registers, dK^T / dV^T accumulators); per 32-query
+//       chunk: S, dP (Q / dO rows from LDS), P = exp2(S c - lse), dS = P (dP - delta),
+//       dV^T += dO^T P, dK^T += Q^T dS (transposed reads).
+//   q:  wave owns 32 queries (Q, dO fragments in registers, dQ^T accumulators); per 32-key chunk:
+//       S^T, dP^T (K / V rows from LDS), dQ^T += K^T dS^T.
+// Rows >= T are zero-filled, so padded keys contribute nothing to dQ; padded queries have
+// lse = +inf (P = 0).  P of padded keys is zeroed for the fused bias column sums.
+template <int HS, int NKT>
+constexpr int bwd_lds_bytes() {
+    return 2 * NKT * 16 * Geo<HS>::SK * 2 + 2 * NKT * 16 * 4 + 4 * 2 * HS * 4;
+}
+template <int HS, int NKT>
+constexpr int bwd_occ() { return bwd_lds_bytes<HS, NKT>() <= 80 * 1024 ? 2 : 1; }
+
+template <int HS, int NKT>
+__device__ __forceinline__ void bwd_kv_body(char* lds, int bh, bf16_t* __restrict__ dqkv,
+                                            const bf16_t* __restrict__ dout,
+                                            const bf16_t* __restrict__ qkv,
+                                            const bf16_t* __restrict__ out,
+                                            const float* __restrict__ lse, int T, int C, int NH,
+                                            float* __restrict__ dsum) {
+    using G = Geo<HS>;
+    constexpr int TP = NKT * 16;  // padded length, multiple of 32
+    constexpr int SK = G::SK, KS = G::KS, DT = G::DT;
+    bf16_t* Qs = reinterpret_cast<bf16_t*>(lds);
+    bf16_t* Ds = Qs + TP * SK;
+    float* lse_s = reinterpret_cast<float*>(Ds + TP * SK);
+    float* del_s = lse_s + TP;
+    float (*csum_s)[2 * HS] = reinterpret_cast<float (*)[2 * HS]>(del_s + TP);
+    const int b = bh / NH, h = bh % NH;
+    const long long C3 = 3LL * C;
+    const bf16_t* base = qkv + (long long)b * T * C3 + h * HS;
+    const bf16_t* dbase = dout + (long long)b * T * C + h * HS;
+    const bf16_t* obase = out + (long long)b * T * C + h * HS;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, i = lane & 15, g = lane >> 4;
+    // K, V fragments of a 2 x 16-key tile straight from HBM (rows >= T -> 0); the wave's first
+    // tile is requested before the Q/dO staging so its latency hides behind it
+    auto load_kv = [&](int kt, bf16x8_t (&kf)[2][KS], bf16x8_t (&vf)[2][KS]) {
+#pragma unroll
+        for (int kk = 0; kk < 2; kk++) {
+            const int key = kt * 32 + kk * 16 + i;
+#pragma unroll
+            for (int s = 0; s < KS; s++) {
+                kf[kk][s] = frag_glb<HS>(base + C, C3, key, T, s, lane);
+                vf[kk][s] = frag_glb<HS>(base + 2 * C, C3, key, T, s, lane);
+            }
+        }
+    };
+    bf16x8_t kf[2][KS], vf[2][KS];
+    if (w < TP / 32) load_kv(w, kf, vf);
+    {
+        bf16_t* const img[2] = {Qs, Ds};
+        const int st[2] = {SK, SK};
+        const bf16_t* const src[2] = {base, dbase};
+        const long long ld[2] = {C3, C};
+        load_images<HS, TP, 256, 2>(img, st, src, ld, T);
+    }
+    __syncthreads();
+    // delta = rowsum(dO * O) per query (O from HBM, dO from the image), lse staged
+    for (int t = tid; t < TP; t += 256) {
+        float dl = 0.f, ls = INFINITY;
+        if (t < T) {
+            ls = lse[(long long)bh * T + t];
+            uint4 ov[G::CH];
+#pragma unroll
+            for (int cc = 0; cc < G::CH; cc++) ov[cc] = *reinterpret_cast<const uint4*>(obase + (long long)t * C + cc * 8);
+#pragma unroll
+            for (int cc = 0; cc < G::CH; cc++) {
+                const uint4 dv = *reinterpret_cast<const uint4*>(Ds + t * SK + cc * 8);
+                const uint32_t* o32 = reinterpret_cast<const uint32_t*>(&ov[cc]);
+                const uint32_t* d32 = reinterpret_cast<const uint32_t*>(&dv);
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    dl += __uint_as_float(o32[e] << 16) * __uint_as_float(d32[e] << 16);
+                    dl += __uint_as_float(o32[e] & 0xffff0000u) * __uint_as_float(d32[e] & 0xffff0000u);
+                }
+            }
+        }
+        lse_s[t] = ls;
+        del_s[t] = dl;
+    }
+    __syncthreads();
+    const float scale = 1.0f / sqrtf((float)HS);
+    const float c = LOG2E * scale;
+    f32x4_t ck[DT] = {}, cv[DT] = {};  // this lane's share of the dK / dV column sums
+    for (int kt = w; kt < TP / 32; kt += 4) {
+        const int key0 = kt * 32;
+        if (kt != w) load_kv(kt, kf, vf);
+        const bool kok[2] = {key0 + i < T, key0 + 16 + i < T};
+        f32x4_t dv[2][DT], dk[2][DT];
+#pragma unroll
+        for (int kk = 0; kk < 2; kk++)
+#pragma unroll
+            for (int dt = 0; dt < DT; dt++) dv[kk][dt] = dk[kk][dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+        for (int qs = 0; qs < TP / 32; qs++) {
+            f32x4_t P[2][2], dS[2][2];  // [kk][u]: lane (i,g) -> [q = 32qs+16u+4g+r][key = 16kk+i]
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const int qt0 = qs * 32 + u * 16;
+                bf16x8_t qr[KS], dr[KS];
+#pragma unroll
+                for (int s = 0; s < KS; s++) {
+                    qr[s] = frag_row<HS>(Qs, SK, qt0, s, lane);
+                    dr[s] = frag_row<HS>(Ds, SK, qt0, s, lane);
+                }
+                float lq[4], dq[4];
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    lq[r] = lse_s[qt0 + 4 * g + r];
+                    dq[r] = del_s[qt0 + 4 * g + r];
+                }
+#pragma unroll
+                for (int kk = 0; kk < 2; kk++) {
+                    f32x4_t s_ = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int s = 0; s < KS; s++) {
+                        s_ = mfma(qr[s], kf[kk][s], s_);
+                        dp = mfma(dr[s], vf[kk][s], dp);
+                    }
+                    // padded keys (K, V rows zero) get P != 0 here; they only reach dK / dV rows
+                    // that are neither stored nor summed
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const float pv = fexp2(s_[r] * c - lq[r]);
+                        P[kk][u][r] = pv;
+                        dS[kk][u][r] = pv * (dp[r] - dq[r]);
+                    }
+                }
+            }
+            bf16x8_t pb[2], db[2];
+#pragma unroll
+            for (int kk = 0; kk < 2; kk++) {
+                pb[kk] = pack_acc(P[kk][0], P[kk][1]);
+                db[kk] = pack_acc(dS[kk][0], dS[kk][1]);
+            }
+#pragma unroll
+            for (int dt = 0; dt < DT; dt++) {
+                const bf16x8_t td = frag_tr(Ds, SK, 32 * qs, 16 * dt, lane);
+                const bf16x8_t tq = frag_tr(Qs, SK, 32 * qs, 16 * dt, lane);
+#pragma unroll
+                for (int kk = 0; kk < 2; kk++) {
+                    dv[kk][dt] = mfma(td, pb[kk], dv[kk][dt]);
+                    dk[kk][dt] = mfma(tq, db[kk], dk[kk][dt]);
+                }
+            }
+        }
+        // lane (i,g) of tile (kk,dt): key = key0 + 16kk + i, d = 16dt + 4g + r
+#pragma unroll
+        for (int kk = 0; kk < 2; kk++) {
+            if (!kok[kk]) continue;
+            bf16_t* dst = dqkv + ((long long)b * T + key0 + kk * 16 + i) * C3 + h * HS + 4 * g;
+#pragma unroll
+            for (int dt = 0; dt < DT; dt++) {
+                store4(dst + C + 16 * dt, dk[kk][dt], scale);
+                store4(dst + 2 * C + 16 * dt, dv[kk][dt], 1.0f);
+            }
+        }
+        if (dsum) {
+#pragma unroll
+            for (int kk = 0; kk < 2; kk++) {
+                if (!kok[kk]) continue;
+#pragma unroll
+                for (int dt = 0; dt < DT; dt++) {
+                    ck[dt] += dk[kk][dt] * scale;
+                    cv[dt] += dv[kk][dt];
+                }
+            }
+        }
+    }
+    if (dsum) {  // per-(b,h) column sums of dK, dV -> dsum[bh][HS .. 3HS)
+#pragma unroll
+        for (int dt = 0; dt < DT; dt++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                float tk = ck[dt][r], tv = cv[dt][r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    tk += __shfl_xor(tk, o, 64);
+                    tv += __shfl_xor(tv, o, 64);
+                }
+                if (i == 0) {
+                    csum_s[w][16 * dt + 4 * g + r] = tk;
+                    csum_s[w][HS + 16 * dt + 4 * g + r] = tv;
+                }
+            }
+        __syncthreads();
+        if (tid < 2 * HS)
+            dsum[(long long)bh * 3 * HS + HS + tid] = csum_s[0][tid] + csum_s[1][tid] + csum_s[2][tid] + csum_s[3][tid];
+    }
+}
+
+template <int HS, int NKT>
+__device__ __forceinline__ void bwd_q_body(char* lds, int bh, bf16_t* __restrict__ dqkv,
+                                           const bf16_t* __restrict__ dout,
+                                           const bf16_t* __restrict__ qkv,
+                                           const bf16_t* __restrict__ out,
+                                           const float* __restrict__ lse, int T, int C, int NH,
+                                           float* __restrict__ dsum) {
+    using G = Geo<HS>;
+    constexpr int TP = NKT * 16;
+    constexpr int SK = G::SK, KS = G::KS, DT = G::DT;
+    bf16_t* Ks = reinterpret_cast<bf16_t*>(lds);
+    bf16_t* Vs = Ks + TP * SK;
+    float (*csum_s)[HS] = reinterpret_cast<float (*)[HS]>(Vs + TP * SK);
+    const int b = bh / NH, h = bh % NH;
+    const bf16_t* obase = out + (long long)b * T * C + h * HS;
+    const long long C3 = 3LL * C;
+    const bf16_t* base = qkv + (long long)b * T * C3 + h * HS;
+    const bf16_t* dbase = dout + (long long)b * T * C + h * HS;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, i = lane & 15, g = lane >> 4;
+    // own 32-query tile: Q / dO fragments, lse, delta straight from HBM; the next tile's are
+    // requested while the current one computes, the first ones before the K/V staging
+    auto load_tile = [&](int qt, bf16x8_t (&qf)[2][KS], bf16x8_t (&df)[2][KS], float (&lq)[2], float (&dl)[2]) {
+        const int q0 = qt * 32;
+        float part[2] = {0.f, 0.f};
+#pragma unroll
+        for (int qq = 0; qq < 2; qq++) {
+            const int q = q0 + qq * 16 + i;
+#pragma unroll
+            for (int s = 0; s < KS; s++) {
+                qf[qq][s] = frag_glb<HS>(base, C3, q, T, s, lane);
+                df[qq][s] = frag_glb<HS>(dbase, C, q, T, s, lane);
+                const bf16x8_t of = frag_glb<HS>(obase, C, q, T, s, lane);
+                // delta = rowsum(dO * O): this lane's share of the query's HS columns (the
+                // zero padding of a half k-step adds nothing)
+#pragma unroll
+                for (int e = 0; e < 8; e++) part[qq] += (float)df[qq][s][e] * (float)of[e];
+            }
+            lq[qq] = q < T ? lse[(long long)bh * T + q] : INFINITY;
+        }
+#pragma unroll
+        for (int qq = 0; qq < 2; qq++) {  // the 4 lanes of a query are lane, lane ^ 16, ^ 32
+            float t = part[qq];
+            t += __shfl_xor(t, 16, 64);
+            t += __shfl_xor(t, 32, 64);
+            dl[qq] = t;
+        }
+    };
+    bf16x8_t qn[2][KS], dn[2][KS];
+    float lqn[2], dln[2];
+    if (w < TP / 32) load_tile(w, qn, dn, lqn, dln);
+    {
+        bf16_t* const img[2] = {Ks, Vs};
+        const int st[2] = {SK, SK};
+        const bf16_t* const src[2] = {base + C, base + 2 * C};
+        const long long ld[2] = {C3, C3};
+        load_images<HS, TP, 256, 2>(img, st, src, ld, T);
+    }
+    __syncthreads();
+    const float scale = 1.0f / sqrtf((float)HS);
+    const float c = LOG2E * scale;
+    f32x4_t cq[DT] = {};
+    for (int qt = w; qt < TP / 32; qt += 4) {
+        const int q0 = qt * 32;
+        bf16x8_t qf[2][KS], df[2][KS];
+        float lq[2], dl[2];
+#pragma unroll
+        for (int qq = 0; qq < 2; qq++) {
+            lq[qq] = lqn[qq];
+            dl[qq] = dln[qq];
+#pragma unroll
+            for (int s = 0; s < KS; s++) {
+                qf[qq][s] = qn[qq][s];
+                df[qq][s] = dn[qq][s];
+            }
+        }
+        if (qt + 4 < TP / 32) load_tile(qt + 4, qn, dn, lqn, dln);
+        f32x4_t dq[2][DT];
+#pragma unroll
+        for (int qq = 0; qq < 2; qq++)
+#pragma unroll
+            for (int dt = 0; dt < DT; dt++) dq[qq][dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+        for (int ks = 0; ks < TP / 32; ks++) {
+            f32x4_t dS[2][2];  // [qq][u]: lane (i,g) -> [key = 32ks+16u+4g+r][q = 16qq+i]
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const int kt0 = ks * 32 + u * 16;
+                bf16x8_t kr[KS], vr[KS];
+#pragma unroll
+                for (int s = 0; s < KS; s++) {
+                    kr[s] = frag_row<HS>(Ks, SK, kt0, s, lane);
+                    vr[s] = frag_row<HS>(Vs, SK, kt0, s, lane);
+                }
+#pragma unroll
+                for (int qq = 0; qq < 2; qq++) {
+                    f32x4_t s_ = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int s = 0; s < KS; s++) {
+                        s_ = mfma(kr[s], qf[qq][s], s_);
+                        dp = mfma(vr[s], df[qq][s], dp);
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; r++) dS[qq][u][r] = fexp2(s_[r] * c - lq[qq]) * (dp[r] - dl[qq]);
+                }
+            }
+            bf16x8_t db[2];
+#pragma unroll
+            for (int qq = 0; qq < 2; qq++) db[qq] = pack_acc(dS[qq][0], dS[qq][1]);
+#pragma unroll
+            for (int dt = 0; dt < DT; dt++) {
+                const bf16x8_t tk = frag_tr(Ks, SK, 32 * ks, 16 * dt, lane);
+#pragma unroll
+                for (int qq = 0; qq < 2; qq++) dq[qq][dt] = mfma(tk, db[qq], dq[qq][dt]);
+            }
+        }
+#pragma unroll
+        for (int qq = 0; qq < 2; qq++) {
+            const int q = q0 + qq * 16 + i;
+            if (q >= T) continue;
+            bf16_t* dst = dqkv + ((long long)b * T + q) * C3 + h * HS + 4 * g;
+#pragma unroll
+            for (int dt = 0; dt < DT; dt++) store4(dst + 16 * dt, dq[qq][dt], scale);
+        }
+        if (dsum) {  // padded queries: dS = exp2(-inf) * ... = 0
+#pragma unroll
+            for (int qq = 0; qq < 2; qq++)
+#pragma unroll
+                for (int dt = 0; dt < DT; dt++) cq[dt] += dq[qq][dt] * scale;
+        }
+    }
+    if (dsum) {
+#pragma unroll
+        for (int dt = 0; dt < DT; dt++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                float tq = cq[dt][r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) tq += __shfl_xor(tq, o, 64);
+                if (i == 0) csum_s[w][16 * dt + 4 * g + r] = tq;
+            }
+        __syncthreads();
+        if (tid < HS) dsum[(long long)bh * 3 * HS + tid] = csum_s[0][tid] + csum_s[1][tid] + csum_s[2][tid] + csum_s[3][tid];
+    }
+}
+
+// kv and q roles of one (b,h) in ONE launch: the two workgroups of a pair are dealt to the same
+// XCD back to back (block ids 16k + x and 16k + 8 + x), so the second reads of Q, K, V, dO, O
+// are served from that XCD's L2 instead of HBM.  Both roles compute delta themselves.
+template <int HS, int NKT>
+__global__ __launch_bounds__(256, (bwd_occ<HS, NKT>())) void attn_bwd_pair_k(
+    bf16_t* __restrict__ dqkv, const bf16_t* __restrict__ dout, const bf16_t* __restrict__ qkv,
+    const bf16_t* __restrict__ out, const float* __restrict__ lse, int T, int C, int NH, int BH,
+    float* __restrict__ dsum) {
+    __shared__ __attribute__((aligned(16))) char lds[bwd_lds_bytes<HS, NKT>()];
+    const int x = blockIdx.x & 7, grp = blockIdx.x >> 3;
+    const int role = grp & 1, bh = (grp >> 1) * 8 + x;
+    if (bh >= BH) return;
+    if (role == 0) bwd_kv_body<HS, NKT>(lds, bh, dqkv, dout, qkv, out, lse, T, C, NH, dsum);
+    else bwd_q_body<HS, NKT>(lds, bh, dqkv, dout, qkv, out, lse, T, C, NH, dsum);
+}
+
+// largest padded length (multiple of 32) whose forward AND backward images fit the 160 KiB LDS
+template <int HS>
+constexpr int max_tp() {
+    int tp = 32;
+    while (tp + 32 <= 320 && (tp + 32) * (Geo<HS>::SK + Geo<HS>::SV) * 2 <= 160 * 1024 &&
+           2 * (tp + 32) * Geo<HS>::SK * 2 + 2 * (tp + 32) * 4 + 8 * HS * 4 <= 160 * 1024)
+        tp += 32;
+    return tp;
+}
+
+// launchers over the key-tile count (NKT = 2, 4, ..., 2*max_tp/32)
+template <int HS, int NKT>
+void launch_fwd(bf16_t* out, float* lse, const bf16_t* qkv, int B, int T, int C, int NH, hipStream_t s) {
+    attn_fwd_k<HS, NKT><<<B * NH, 256, 0, s>>>(out, lse, qkv, T, C, NH);
+}
+template <int HS, int NKT>
+void launch_bwd(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t* out,
+                const float* lse, int B, int T, int C, int NH, float* part, hipStream_t s) {
+    attn_bwd_pair_k<HS, NKT><<<2 * cdiv(B * NH, 8) * 8, 256, 0, s>>>(dqkv, dout, qkv, out, lse, T, C, NH,
+                                                                     B * NH, part);
+}
+template <int HS, int NKT = 2>
+bool dispatch_fwd(int nkt, bf16_t* out, float* lse, const bf16_t* qkv, int B, int T, int C, int NH,
+                  hipStream_t s) {
+    if constexpr (NKT * 16 > max_tp<HS>()) {
+        return false;
+    } else {
+        if (nkt == NKT) { launch_fwd<HS, NKT>(out, lse, qkv, B, T, C, NH, s); return true; }
+        return dispatch_fwd<HS, NKT + 2>(nkt, out, lse, qkv, B, T, C, NH, s);
+    }
+}
+template <int HS, int NKT = 2>
+bool dispatch_bwd(int nkt, bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t* out,
+                  const float* lse, int B, int T, int C, int NH, float* part, hipStream_t s) {
+    if constexpr (NKT * 16 > max_tp<HS>()) {
+        return false;
+    } else {
+        if (nkt == NKT) { launch_bwd<HS, NKT>(dqkv, dout, qkv, out, lse, B, T, C, NH, part, s); return true; }
+        return dispatch_bwd<HS, NKT + 2>(nkt, dqkv, dout, qkv, out, lse, B, T, C, NH, part, s);
+    }
+}
+
+}  // namespace fa
+
+// per-head-size entry points (attn_h*.hip); false = shape outside the instantiated range
+#define VIT_FA_DECLARE(HS)                                                                         \
+    bool fa_forward_h##HS(bf16_t* out, float* lse, const bf16_t* qkv, int B, int T, int C, int NH, \
+                          hipStream_t s);                                                          \
+    bool fa_backward_h##HS(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t* out, \
+                           const float* lse, int B, int T, int C, int NH, float* part, hipStream_t s); \
+    int fa_max_t_h##HS();
+VIT_FA_DECLARE(32)
+VIT_FA_DECLARE(64)
+VIT_FA_DECLARE(80)
+VIT_FA_DECLARE(96)
+VIT_FA_DECLARE(128)
+
+#define VIT_FA_DEFINE(HS)                                                                           \
+    bool fa_forward_h##HS(bf16_t* out, float* lse, const bf16_t* qkv, int B, int T, int C, int NH,  \
+                          hipStream_t s) {                                                          \
+        return fa::dispatch_fwd<HS>(cdiv(T, 32) * 2, out, lse, qkv, B, T, C, NH, s);                \
+    }                                                                                               \
+    bool fa_backward_h##HS(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t* out,  \
+                           const float* lse, int B, int T, int C, int NH, float* part, hipStream_t s) { \
+        return fa::dispatch_bwd<HS>(cdiv(T, 32) * 2, dqkv, dout, qkv, out, lse, B, T, C, NH, part, s); \
+    }                                                                                               \
+    int fa_max_t_h##HS() { return fa::max_tp<HS>(); }
+
+}  // namespace vit
