@@ -1,9 +1,13 @@
 #!/usr/bin/env python3
 """Benchmark: ViT-B/16 224x224 bf16 training step (forward + backward + SGD) on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--model vit_b16] [--batch 256]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--model vit_b16] [--batch 256] [--dtype bf16]
     torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
         bench.py --gpus N --steps K --warmup W
+Run directly with --gpus N > 1 (no WORLD_SIZE in the environment) it launches the N ranks itself:
+N child processes with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, started
+before this process touches the GPU (it never does); it prints rank 0's JSON line and exits
+non-zero if any rank fails.
 
 One process per GPU.  Each rank trains on its own 256-image shard of one seeded synthetic stream
 (weak scaling); gradients are summed by RCCL inside libvit_hip.so (per-layer chunks on a side
@@ -23,16 +27,24 @@ import os
 import sys
 import time
 
-import torch  # noqa: F401  (first: owns the HIP runtime of the process)
+import socket
+import subprocess
+
+import torch  # noqa: F401  (first: owns the HIP runtime of the process; importing it starts no GPU work)
 import torch.distributed as dist
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-from vitpkg import vit  # noqa: E402
+vit = None  # vitpkg.vit, imported in the rank processes only (launch_ranks never loads the library)
 
 METRIC = "images/sec (train step) ViT-B/16 224² bf16 at 1/2/4/8 MI355X; % MFMA roofline"
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
+PEAK_FP8_TFLOPS = 5000.0    # dense fp8 (block-scaled f8f6f4 MFMA), same table
+MODEL_NAMES = {"vit_tiny16": "ViT-Tiny/16", "vit_b16": "ViT-B/16", "vit_l16": "ViT-L/16", "vit_h14": "ViT-H/14"}
+# GEMM classes that run on MXFP8 operands in --dtype fp8 (forward and input-gradient GEMMs)
+FP8_CLASSES = {"gemm_qkv_fwd", "gemm_proj_fwd", "gemm_fc_fwd", "gemm_fcproj_fwd",
+               "gemm_qkv_dgrad", "gemm_proj_dgrad", "gemm_fc_dgrad", "gemm_fcproj_dgrad"}
 PEAK_HBM_GBS = 8000.0
 
 
@@ -62,6 +74,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="vit_b16")
     ap.add_argument("--batch", type=int, default=256, help="images per GPU")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
+                    help="fp8: MXFP8 forward / input-gradient GEMMs (BASELINE config 5)")
     ap.add_argument("--lr", type=float, default=1e-4)
     ap.add_argument("--no-overlap", action="store_true", help="one all-reduce after backward")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -107,13 +121,60 @@ def _block_once(o, t):
     return time.perf_counter() - t0
 
 
+def _cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def config1_step(oc, o):
+    """BASELINE config 1 on the CPU: one full ViT-Tiny/16 224x224 B=8 training step (forward +
+    backward + SGD) of the C oracle (train_vit.rs:188-373, 737-743 restated), seeded inputs."""
+    cfg = vit.data.CONFIGS["vit_tiny16"]
+    B = 8
+    params = o.arr(vit.data.init_params(cfg, "ref", seed=1337))
+    px, lab = vit.data.synthetic_batch(cfg, B, seed=1337)
+    m = oc.RefViT(o, oc.VitConfig(cfg.img, cfg.patch, cfg.in_ch, cfg.channels, cfg.num_layers,
+                                  cfg.num_heads, cfg.num_classes), B)
+    g = np.zeros_like(params)
+    t0 = time.perf_counter()
+    loss = m.forward(params, px, lab)
+    m.backward(params, g)
+    params -= np.float32(1e-4) * g   # optimizer_step (SGD)
+    dt = time.perf_counter() - t0
+    return {"model": "vit_tiny16", "batch": B, "s_per_step": round(dt, 3),
+            "images_per_s": round(B / dt, 4), "loss": round(loss, 4),
+            "gflop_per_step": round(B * cfg.train_gflop_per_image()[1], 2)}
+
+
 def cpu_baseline(cfg, reps=3):
-    """Time the CPU oracle (reference loops, C, 1 thread) on a bounded sample: one image through
-    one transformer block forward + backward (all layer ops in train_vit.rs order, mean of `reps`)
-    plus the patch embedding and head; images/s = 1 / (L * t_block + t_embed_head)."""
+    """Time the CPU oracle (reference loops restated in C, 1 thread pinned to one core) on the
+    GPU box's host:
+      value: the bench's workload (cfg, one image) on a bounded sample — one transformer block
+             forward + backward (all layer ops in train_vit.rs order, mean of `reps`) x L plus the
+             patch embedding and head; images/s = 1 / (L * t_block + t_embed_head);
+      config1_vit_tiny16_b8: one full ViT-Tiny/16 B=8 training step (BASELINE config 1)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_ctypes as oc
     o = oc.Oracle("f32")
+    allowed = os.sched_getaffinity(0)
+    core = min(allowed)
+    os.sched_setaffinity(0, {core})
+    try:
+        res = _cpu_baseline_pinned(oc, o, cfg, reps)
+        res["config1_vit_tiny16_b8"] = config1_step(oc, o)
+    finally:
+        os.sched_setaffinity(0, allowed)
+    res.update({"pinned_core": core, "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
+                "affinity_cpus": len(allowed)})
+    return res
+
+
+def _cpu_baseline_pinned(oc, o, cfg, reps):
     rng = np.random.default_rng(0)
     C, T, NH, NC, P, IMG = cfg.channels, cfg.T, cfg.num_heads, cfg.num_classes, cfg.patch, cfg.img
     B = 1
@@ -197,8 +258,41 @@ def pipeline_rate(m, cfg, B, args):
         os.rmdir(d)
 
 
+def _free_port():
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n):
+    """Single-node launcher for `python bench.py --gpus N`: one child per GPU (the torchrun
+    environment contract), this process stays off the GPU; rank 0's stdout is the result."""
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out0 = procs[0].communicate()[0]
+    rcs = [procs[0].returncode] + [p.wait() for p in procs[1:]]
+    if out0:
+        sys.stdout.write(out0.decode())
+        sys.stdout.flush()
+    bad = [(r, rc) for r, rc in enumerate(rcs) if rc != 0]
+    if bad:
+        print(f"[bench] ranks failed (rank, exit code): {bad}", file=sys.stderr)
+        return 1
+    return 0
+
+
 def main():
+    global vit
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    from vitpkg import vit as _vit
+    vit = _vit
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -212,7 +306,7 @@ def main():
         vit.check("vit_init")
     cfg = vit.data.CONFIGS[args.model]
     B = args.batch
-    m = vit.ViT(cfg, B, vit.VIT_BF16, device=local)
+    m = vit.ViT(cfg, B, vit.VIT_FP8 if args.dtype == "fp8" else vit.VIT_BF16, device=local)
     m.set_params(vit.data.init_params(cfg, "ref", seed=1337))
     px, lab = vit.data.synthetic_batch(cfg, B, seed=1337, offset_images=rank * B)
     m.set_batch(px, lab)
@@ -221,6 +315,7 @@ def main():
         uid = [vit.ViT.dp_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         m.dp_init(rank, world, uid[0], overlap=not args.no_overlap)
+    rccl_ranks = m.dp_ranks()  # ncclCommCount of the trainer's communicator (0 = no DP)
     b_global = B * world
     if args.serial:
         m.set_concurrency(False)
@@ -233,13 +328,13 @@ def main():
     def timed(steps):
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
+        torch.cuda.synchronize(local)
         m.sync()
         t0 = time.perf_counter()
         for _ in range(steps):
             m.train_step(args.lr, b_global)
         m.sync()
-        torch.cuda.synchronize()
+        torch.cuda.synchronize(local)
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
@@ -275,34 +370,48 @@ def main():
 
     out = None
     if rank == 0:
-        gemms = {k: v for k, v in kern.items() if k.startswith("gemm_")}
-        roof = None
-        if gemms:
+        def roofline(classes, peak):
+            gemms = {k: v for k, v in kern.items() if k in classes}
+            if not gemms:
+                return None
             dom = max(gemms, key=lambda k: gemms[k]["ms"])
             d = gemms[dom]
             avg_ms = d["ms"] / d["calls"]
             ach = d["flops"] / d["calls"] / (avg_ms * 1e-3) / 1e12
             traffic, tsrc = pmc_traffic(dom)
-            roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS,
-                    "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
+            return {"kernel": dom, "bound": "mfma", "achieved": round(ach, 1), "peak": peak,
+                    "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                     "traffic": round(traffic) if traffic else None, "traffic_unit": "bytes/launch",
                     "traffic_source": tsrc,
                     "avg_launch_ms": round(avg_ms, 4), "flops_per_launch": d["flops"] / d["calls"]}
+        all_gemms = {k for k in kern if k.startswith("gemm_")}
+        if args.dtype == "fp8":
+            roof = roofline(all_gemms & FP8_CLASSES, PEAK_FP8_TFLOPS)
+            roof_bf16 = roofline(all_gemms - FP8_CLASSES, PEAK_BF16_TFLOPS)
+        else:
+            roof, roof_bf16 = roofline(all_gemms, PEAK_BF16_TFLOPS), None
         ksum = {k: {"ms_per_step": round(v["ms"] / args.steps, 3), "calls_per_step": v["calls"] // args.steps,
                     "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1) if v["flops"] and v["ms"] else None}
                 for k, v in sorted(kern.items(), key=lambda kv: -kv[1]["ms"])}
+        metric = METRIC
+        if args.model != "vit_b16" or args.dtype != "bf16":
+            metric = (f"images/sec (train step) {MODEL_NAMES.get(cfg.name, cfg.name)} {cfg.img}² {args.dtype} "
+                      f"on MI355X; % MFMA roofline")
         out = {
-            "metric": METRIC, "value": round(ips, 2), "unit": "images/s", "n_gpus": world,
+            "metric": metric, "value": round(ips, 2), "unit": "images/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (seeded splitmix64: N(0,1) pixels, uniform labels; reference init U[0,1)*0.02)",
-            "config": {"workload": f"{cfg.name} 224x224 train step (fwd+bwd+SGD), batch {B}/GPU",
+            "rccl_ranks": rccl_ranks,
+            "config": {"workload": f"{cfg.name} {cfg.img}x{cfg.img} train step (fwd+bwd+SGD), batch {B}/GPU, {args.dtype}",
                        "model": cfg.name, "global_batch": b_global, "seq_len": cfg.T,
                        "parallelism": f"dp{world}"},
             "mfma_roofline_frac_step": round(ips * gflop_img / world / (PEAK_BF16_TFLOPS * 1e3), 4),
+            "mfma_roofline_frac_step_peak_tflops": PEAK_BF16_TFLOPS,
             "train_gflop_per_image": round(gflop_img, 3),
             "loss_after_warmup": round(loss_w, 4),
-            "roofline": roof, "kernels": ksum, "input_pipeline": pipe,
+            "roofline": roof, "kernels": ksum,
+            **({"roofline_bf16_gemms": roof_bf16, "fp8_gemm_classes": sorted(FP8_CLASSES)} if args.dtype == "fp8" else {}), "input_pipeline": pipe,
             "kernels_note": "per-kernel ms from HIP events over a second pass of the same steps run "
                             "with stream concurrency off (kernels one at a time)",
         }

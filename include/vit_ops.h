@@ -138,6 +138,25 @@ void gemm_bf16_fused(void* C, void* C2, long long ldc, const void* aux, long lon
                      const uint16_t* A, long long lda, int a_kcontig, const uint16_t* B,
                      long long ldb, int b_kcontig, const float* bias, float* colsum_out, int M,
                      int N, int K, int epi);
+/* ------------------------------------------------------------------ fp8 (MXFP8) GEMM path
+ * OCP fp8 e4m3 operands with one E8M0 scale per 32 consecutive k-elements of a row (OCP MX block
+ * scaling) on v_mfma_scale_f32_32x32x64_f8f6f4, fp32 accumulate: the fp8 mode's forward and
+ * input-gradient GEMMs (matmul_forward, train_vit.rs:384; dinp of matmul_backward, :530-541).
+ * Scales use the lane-native layout [K/64][Rpad/32][64] bytes (Rpad = rows rounded up to 256;
+ * byte h*32 + r of row group g at step s scales row 32g + r, k-block 2s + h): mx_scale_size
+ * bytes per operand.  quantize_mx_*: x [R][K] (row stride ldx elements, K % 64 == 0) -> q [R][K]
+ * e4m3 (row stride ldq bytes) + scales; scale 2^X with X = ceil(log2(amax / 448)) per block,
+ * x * 2^-X rounded to nearest even.  gemm_fp8_fused: C = A . B^T with A [M][K], B [N][K]
+ * (K-contiguous bytes) and the epilogues of gemm_bf16_fused (epi 0, 1, 3, 4, 5, 6). */
+long long mx_scale_size(long long rows, int K);
+void quantize_mx_bf16_ex(uint8_t* q, uint8_t* scales, const uint16_t* x, long long R, int K,
+                         long long ldx, long long ldq);
+void quantize_mx_f32_ex(uint8_t* q, uint8_t* scales, const float* x, long long R, int K,
+                        long long ldx, long long ldq);
+void gemm_fp8_fused(void* C, void* C2, long long ldc, const void* aux, long long ldaux,
+                    const uint8_t* A, const uint8_t* a_scale, long long lda, const uint8_t* B,
+                    const uint8_t* b_scale, long long ldb, const float* bias, float* colsum_out,
+                    int M, int N, int K, int epi);
 /* tools: GEMM engine selection (1 = 128x128, 2 = 256x256 one workgroup per CU, the default,
  * 4 = 256x128 two per CU) and diagnostics (flag 2: skip epilogues, main-loop timing only) */
 void gemm_bf16_set_variant(int variant);

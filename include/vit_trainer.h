@@ -18,9 +18,16 @@
  *                 materialised attention) — the parity path (<= 1e-4 rel vs the CPU oracle).
  *   VIT_BF16 (1): the fast path — bf16 MFMA GEMMs with fused epilogues, fused attention,
  *                 fp32 master weights / gradients / residual stream / LN statistics.
- *                 Head size 64 with T <= 256 uses the MFMA attention; head sizes 32/80/96/128
- *                 or T > 256 (ViT-H/14) use generic VALU attention kernels, and a patch whose
- *                 3*P*P is not a multiple of 8 runs the patch embedding on the fp32 GEMM.
+ *                 Head sizes 32/64/80/96/128 use the MFMA attention while T <= 320 (generic
+ *                 VALU kernels beyond), and a patch whose 3*P*P is not a multiple of 8 runs the
+ *                 patch embedding on the fp32 GEMM.
+ *   VIT_FP8 (2):  BASELINE config 5 ("fp8 weights/activations"): VIT_BF16 with the forward and
+ *                 input-gradient GEMMs of every layer (qkv, proj, fc, fcproj) on MXFP8 operands
+ *                 (OCP e4m3 + one E8M0 scale per 32 k-elements, v_mfma_scale_f32_32x32x64_f8f6f4);
+ *                 weights quantized from the fp32 master after every optimizer step, activations /
+ *                 output gradients quantized as each GEMM consumes them.  Weight gradients,
+ *                 attention, LayerNorm, the residual stream and the optimizer stay bf16 / fp32.
+ *                 Needs C % 64 == 0.
  * All calls are asynchronous on the trainer's stream unless noted; functions returning int
  * return 0 on success (details via vit_last_error()).
  */
@@ -35,7 +42,7 @@ typedef struct {
     int img, patch, in_ch, channels, num_layers, num_heads, num_classes;
 } vit_config_t;
 
-enum { VIT_FP32 = 0, VIT_BF16 = 1 };
+enum { VIT_FP32 = 0, VIT_BF16 = 1, VIT_FP8 = 2 };
 enum { VIT_NUM_PARAM_TENSORS = 20 };
 
 typedef struct vit_trainer vit_trainer_t;
@@ -88,6 +95,8 @@ int vit_dp_get_unique_id(char* out);   /* rank 0 creates; broadcast the bytes ou
 /* chunks: 0 = one all-reduce of the whole gradient arena after backward;
  *         1 = per-layer chunks on a side stream overlapped with backward (default) */
 int vit_trainer_dp_init(vit_trainer_t* t, int rank, int world, const char* unique_id, int overlap);
+/* ranks of the trainer's RCCL communicator (ncclCommCount); 0 before vit_trainer_dp_init */
+int vit_trainer_dp_ranks(vit_trainer_t* t);
 
 /* ---- stream concurrency (bf16 mode): on (default) = the batch runs as two micro-batch row halves
  *      on two streams and the weight-gradient GEMMs on a third; off = one stream, kernels one at a
@@ -95,9 +104,14 @@ int vit_trainer_dp_init(vit_trainer_t* t, int rank, int world, const char* uniqu
 int vit_trainer_set_concurrency(vit_trainer_t* t, int on);
 /* ---- tuning options for A/B measurements in one process (call between steps):
  *      "microbatch" = number of micro-batch streams wanted (1 .. 4; the largest divisor of B),
- *      "dgrad_transposed" = 1 (default): dgrad GEMMs read the transposed weight copy.
+ *      "dgrad_transposed" = 1 (default): dgrad GEMMs read the transposed weight copy,
+ *      "dp_probe" = 1: every gradient chunk is also copied, on the all-reduce stream right after
+ *      its all-reduce, into a snapshot arena (read with vit_trainer_get_dp_snapshot) — a check
+ *      that each overlapped chunk was final when it was reduced.
  *      Returns non-zero (and sets the error) for an unknown name. ---- */
 int vit_trainer_set_option(vit_trainer_t* t, const char* name, int value);
+/* canonical host copy of the dp_probe snapshot arena; synchronous */
+int vit_trainer_get_dp_snapshot(vit_trainer_t* t, float* host);
 
 /* ---- per-kernel-class timing with HIP events on the stream each kernel runs on ---- */
 int vit_trainer_set_timing(vit_trainer_t* t, int on);

@@ -2,8 +2,9 @@
 
 fp32 mode runs the reference op sequence on the GPU: logits, loss and every per-parameter
 gradient within 1e-4 relative (max-normalised per tensor) of the fp32 CPU oracle — the
-north-star parity bar.  bf16 mode (the benchmarked fast path) is reported against the same
-oracle with a bf16 tolerance (loss 1e-2, logits/grads 5e-2 per tensor).
+north-star parity bar.  bf16 mode (the benchmarked fast path) is gated against the same
+oracle at the SURVEY.md §8d bf16 target: loss 1e-2, logits / every gradient tensor 2e-2
+(max-normalised; measured <= 1.2e-2 at full ViT-B/16 depth, profiles/r02_parity.json).
 """
 import os
 
@@ -57,9 +58,9 @@ def test_fp32_trainer_matches_golden(gpu, name):
     m.close()
 
 
-@pytest.mark.parametrize("name,B", [("vit_tiny16", 2), ("test", 5)])
+@pytest.mark.parametrize("name,B", [("vit_tiny16", 8), ("test", 5)])
 def test_fp32_trainer_matches_oracle(gpu, oracle32, name, B):
-    """ViT-Tiny/16 224x224 (BASELINE config 1 shapes, T=197) through the reference op sequence."""
+    """ViT-Tiny/16 224x224 at B=8 (BASELINE config 1, T=197) through the reference op sequence."""
     import oracle_ctypes as oc
     v = gpu
     cfg = v.data.CONFIGS[name]
@@ -84,7 +85,7 @@ def test_fp32_trainer_matches_oracle(gpu, oracle32, name, B):
     m.close()
 
 
-@pytest.mark.parametrize("name,B", [("test_h64", 4), ("vit_tiny16", 2)])
+@pytest.mark.parametrize("name,B", [("test_h64", 4), ("vit_tiny16", 8)])
 def test_bf16_trainer_vs_oracle(gpu, oracle32, name, B):
     import oracle_ctypes as oc
     v = gpu
@@ -98,9 +99,9 @@ def test_bf16_trainer_vs_oracle(gpu, oracle32, name, B):
     m.backward()
     g = m.grads()
     assert abs(loss - loss_r) <= 1e-2 * abs(loss_r)
-    assert rel_err(m.logits(), logits_r) <= 5e-2
+    assert rel_err(m.logits(), logits_r) <= 2e-2
     errs = per_tensor_errs(cfg, g, g_r)
-    assert max(errs.values()) <= 5e-2, errs
+    assert max(errs.values()) <= 2e-2, errs
     m.close()
 
 
@@ -156,7 +157,7 @@ def test_vit_b16_full_size_step(gpu):
 def test_vit_b16_fp32_and_bf16_vs_oracle_one_image(gpu, oracle32):
     """ViT-B/16 224x224 at full width/depth (C=768, L=12, T=197), one image: the fp32 trainer
     within 1e-4 of the CPU oracle on logits, loss and all 20 gradient tensors; the bf16 fast
-    path reported against the same oracle (bf16 tolerance)."""
+    path within 1e-2 (loss) / 2e-2 (logits, every gradient tensor) of the same oracle."""
     import oracle_ctypes as oc
     v = gpu
     cfg = v.data.CONFIGS["vit_b16"]
@@ -164,7 +165,7 @@ def test_vit_b16_fp32_and_bf16_vs_oracle_one_image(gpu, oracle32):
     px, lab = v.data.synthetic_batch(cfg, 1, seed=5)
     loss_r, logits_r, g_r = oracle_step(oc, oracle32, cfg, params, px, lab)
     res = {}
-    for prec, tol in ((v.VIT_FP32, 1e-4), (v.VIT_BF16, 5e-2)):
+    for prec, tol, tol_loss in ((v.VIT_FP32, 1e-4, 1e-4), (v.VIT_BF16, 2e-2, 1e-2)):
         m = v.ViT.build(cfg, 1, prec, params=params)
         m.zero_grad()
         loss = m.forward(px, lab)
@@ -172,7 +173,7 @@ def test_vit_b16_fp32_and_bf16_vs_oracle_one_image(gpu, oracle32):
         g = m.grads()
         errs = per_tensor_errs(cfg, g, g_r)
         res[prec] = (abs(loss - loss_r) / abs(loss_r), rel_err(m.logits(), logits_r), max(errs.values()))
-        assert res[prec][0] <= tol and res[prec][1] <= tol and res[prec][2] <= tol, (prec, res[prec], errs)
+        assert res[prec][0] <= tol_loss and res[prec][1] <= tol and res[prec][2] <= tol, (prec, res[prec], errs)
         if prec == v.VIT_FP32:
             ok, frac = elementwise_ok(g, g_r)
             assert ok, frac
@@ -185,9 +186,10 @@ def test_vit_b16_fp32_and_bf16_vs_oracle_one_image(gpu, oracle32):
 def test_dp_single_rank_rccl_is_identity(gpu, prec_name, overlap):
     """The RCCL path on one GPU: world_size 1 all-reduce (per-layer chunks on the
     side stream, or one whole-arena call) must leave the gradients equal to no DP and the SGD step
-    that waits on it must produce the same parameters.  A chunk all-reduced before its layer's
-    gradients are final would lose updates (an O(1) error); the tolerance only absorbs the
-    float-atomic summation order of the split-K / column-sum kernels between two runs."""
+    that waits on it must produce the same parameters (the tolerance only absorbs the float-atomic
+    summation order of the split-K / column-sum kernels between two runs).  At world 1 the sum is
+    an identity, so this does not see a chunk reduced too early: test_dp_overlap_chunks_are_final
+    does."""
     v = gpu
     prec = getattr(v, prec_name)
     cfg = v.data.CONFIGS["test_h64"]
@@ -207,6 +209,40 @@ def test_dp_single_rank_rccl_is_identity(gpu, prec_name, overlap):
         m.close()
     assert rel_err(out[1][0], out[0][0]) <= 1e-6
     assert rel_err(out[1][1], out[0][1]) <= 1e-6
+
+
+@pytest.mark.parametrize("prec_name", ["VIT_FP32", "VIT_BF16", "VIT_FP8"])
+@pytest.mark.parametrize("nmb", [1, 2, 4])
+def test_dp_overlap_chunks_are_final(gpu, prec_name, nmb):
+    """Ordering of the overlapped per-layer all-reduce (trainer chunk_done: events on the compute,
+    weight-gradient and micro-batch streams before each chunk's ncclAllReduce on the comm stream;
+    train_vit.rs:271-373 produces the chunks, :737-743 consumes them).  With option dp_probe the
+    comm stream copies every chunk right after its all-reduce; the copy must equal the final
+    gradients BIT FOR BIT for every chunk, with stream concurrency on and 1, 2 and 4 micro-batch
+    streams (a chunk reduced before its last writer finished would be caught here even at
+    world 1).  Three steps, so the zero_grad / previous-step ordering is exercised too."""
+    v = gpu
+    prec = getattr(v, prec_name)
+    cfg = v.data.CONFIGS["test_h64"]
+    params = v.data.init_params(cfg, "parity", seed=17)
+    px, lab = v.data.synthetic_batch(cfg, 4, seed=18)
+    m = v.ViT.build(cfg, 4, prec, params=params)
+    m.set_concurrency(True)
+    m.set_option("microbatch", nmb)
+    m.dp_init(0, 1, v.ViT.dp_unique_id(), overlap=True)
+    assert m.dp_ranks() == 1
+    m.set_option("dp_probe", 1)
+    m.set_batch(px, lab)
+    for _ in range(3):
+        m.train_step(0.01)
+        m.sync()
+        g = m.grads()
+        snap = m.dp_snapshot()
+        assert np.abs(g).max() > 0
+        bad = [n for n, a, b in zip(cfg.split(g).keys(), cfg.split(g).values(), cfg.split(snap).values())
+               if not np.array_equal(a, b)]
+        assert not bad, bad
+    m.close()
 
 
 def test_vit_l16_full_size_step(gpu):
@@ -240,7 +276,7 @@ def test_vit_l16_full_size_step(gpu):
 def test_vit_l16_bf16_vs_fp32_trainer_two_layers(gpu):
     """ViT-L/16 width (C=1024, NH=16, MLP 4096, T=197) at reduced depth and B=2: the bf16 fast
     path against the fp32 path of the same trainer (itself pinned to the oracle at 1e-4 above),
-    bf16 tolerance 5e-2 on loss, logits and every gradient tensor."""
+    loss 1e-2, logits and every gradient tensor 2e-2."""
     v = gpu
     base = v.data.CONFIGS["vit_l16"]
     cfg = v.data.VitCfg("vit_l16_l2", img=224, patch=16, channels=1024, num_layers=2,
@@ -258,17 +294,17 @@ def test_vit_l16_bf16_vs_fp32_trainer_two_layers(gpu):
     lf, zf, gf = out[v.VIT_FP32]
     lb, zb, gb = out[v.VIT_BF16]
     assert abs(lb - lf) <= 1e-2 * abs(lf)
-    assert rel_err(zb, zf) <= 5e-2
+    assert rel_err(zb, zf) <= 2e-2
     errs = per_tensor_errs(cfg, gb, gf)
-    assert max(errs.values()) <= 5e-2, errs
+    assert max(errs.values()) <= 2e-2, errs
     assert base.channels == cfg.channels
 
 
 def test_vit_h14_geometry_fp32_vs_oracle(gpu, oracle32):
     """BASELINE config 5 geometry (ViT-H/14: patch 14 -> im2col K=588, T=257, C=1280, NH=16,
     head size 80) at reduced depth, one image: fp32 parity mode within 1e-4 of the CPU oracle on
-    logits, loss and all gradient tensors; bf16 mode (generic attention kernels, fp32 patch
-    embedding since 588 % 8 != 0) reported against the same oracle at the bf16 tolerance."""
+    logits, loss and all gradient tensors; bf16 mode (MFMA attention at head size 80, fp32 patch
+    embedding since 588 % 8 != 0) within the bf16 gate (loss 1e-2, logits / grads 2e-2)."""
     import oracle_ctypes as oc
     v = gpu
     cfg = v.data.VitCfg("vit_h14_l1", img=224, patch=14, channels=1280, num_layers=1,
@@ -293,9 +329,9 @@ def test_vit_h14_geometry_fp32_vs_oracle(gpu, oracle32):
     m.backward()
     g = m.grads()
     assert abs(loss - loss_r) <= 1e-2 * abs(loss_r)
-    assert rel_err(m.logits(), logits_r) <= 5e-2
+    assert rel_err(m.logits(), logits_r) <= 2e-2
     errs = per_tensor_errs(cfg, g, g_r)
-    assert max(errs.values()) <= 5e-2, errs
+    assert max(errs.values()) <= 2e-2, errs
     m.close()
 
 
@@ -319,6 +355,92 @@ def test_vit_h14_full_width_bf16_step(gpu):
     assert np.all(np.isfinite(g))
     gs = cfg.split(g)
     for n in ("patch_w", "qkvw", "qkvb", "fcw", "head_w", "wpe"):
+        assert np.abs(gs[n]).max() > 0, n
+    m.optimizer_step(0.05)
+    m.zero_grad()
+    loss1 = m.forward()
+    assert loss1 < loss0
+    m.close()
+
+
+def _fp8_vs_oracle(v, oracle32, cfg, B, seed):
+    import oracle_ctypes as oc
+    params = v.data.init_params(cfg, "parity", seed=seed)
+    px, lab = v.data.synthetic_batch(cfg, B, seed=seed + 1)
+    loss_r, logits_r, g_r = oracle_step(oc, oracle32, cfg, params, px, lab)
+    out = {}
+    for prec in (v.VIT_BF16, v.VIT_FP8):
+        m = v.ViT.build(cfg, B, prec, params=params)
+        m.zero_grad()
+        loss = m.forward(px, lab)
+        m.backward()
+        g = m.grads()
+        errs = per_tensor_errs(cfg, g, g_r)
+        out[prec] = (abs(loss - loss_r) / abs(loss_r), rel_err(m.logits(), logits_r), errs)
+        m.close()
+    return out
+
+
+@pytest.mark.parametrize("name,B", [("test_h64", 4), ("vit_h14_l1", 1)])
+def test_fp8_trainer_vs_oracle(gpu, oracle32, name, B):
+    """BASELINE config 5's fp8 mode (MXFP8 forward and input-gradient GEMMs) against the fp32 CPU
+    oracle: loss within 2e-2, logits within 1e-1 and every gradient tensor within 1.5e-1
+    (max-normalised) — the e4m3 element rounding (2^-4 relative) through two GEMMs per gradient
+    path; the bf16 mode on the same inputs is reported beside it (its own gate is 2e-2)."""
+    v = gpu
+    cfg = (v.data.VitCfg("vit_h14_l1", img=224, patch=14, channels=1280, num_layers=1, num_heads=16,
+                         num_classes=1000) if name == "vit_h14_l1" else v.data.CONFIGS[name])
+    out = _fp8_vs_oracle(v, oracle32, cfg, B, seed=41)
+    lf, zf, ef = out[v.VIT_FP8]
+    print(f"{name} fp8 vs oracle: loss {lf:.2e} logits {zf:.2e} max grad {max(ef.values()):.2e}",
+          {k: round(e, 4) for k, e in ef.items()})
+    lb, zb, eb = out[v.VIT_BF16]
+    print(f"{name} bf16 vs oracle: loss {lb:.2e} logits {zb:.2e} max grad {max(eb.values()):.2e}")
+    assert lf <= 2e-2 and zf <= 1e-1, (lf, zf)
+    assert max(ef.values()) <= 1.5e-1, ef
+
+
+def test_fp8_training_reduces_loss(gpu):
+    """fp8 mode fits one batch like the bf16 mode (40 SGD steps, loss / 10) and its first steps
+    track the bf16 trajectory."""
+    v = gpu
+    cfg = v.data.CONFIGS["test_h64"]
+    params = v.data.init_params(cfg, "parity", seed=1)
+    px, lab = v.data.synthetic_batch(cfg, 8, seed=2)
+    traj = {}
+    for prec in (v.VIT_BF16, v.VIT_FP8):
+        m = v.ViT.build(cfg, 8, prec, params=params)
+        m.set_batch(px, lab)
+        losses = []
+        for _ in range(40):
+            m.train_step(0.1)
+            losses.append(float(v.lib().vit_trainer_mean_loss(m.h)))
+        assert losses[-1] < 0.1 * losses[0], (prec, [round(x, 3) for x in losses])
+        traj[prec] = np.array(losses)
+        m.close()
+    early = np.abs(traj[v.VIT_FP8][:8] / traj[v.VIT_BF16][:8] - 1).max()
+    assert early < 5e-2, (early, traj)
+
+
+def test_vit_h14_fp8_full_width_step(gpu):
+    """Config 5 at full width (C=1280, hs 80, T=257), 4 layers, B=32, fp8 mode: finite loss near
+    ln(1000), finite non-zero grads in every tensor family, loss drops after one SGD step."""
+    v = gpu
+    cfg = v.data.VitCfg("vit_h14_l4", img=224, patch=14, channels=1280, num_layers=4, num_heads=16,
+                        num_classes=1000)
+    B = 32
+    params = v.data.init_params(cfg, "parity", seed=31)
+    px, lab = v.data.synthetic_batch(cfg, B, seed=32)
+    m = v.ViT.build(cfg, B, v.VIT_FP8, params=params)
+    m.set_batch(px, lab)
+    m.zero_grad()
+    loss0 = m.forward()
+    assert np.isfinite(loss0) and abs(loss0 - np.log(1000)) < 1.5
+    m.backward()
+    g = m.grads()
+    assert np.all(np.isfinite(g))
+    gs = cfg.split(g)
+    for n in ("patch_w", "qkvw", "qkvb", "fcw", "fcprojw", "attprojw", "head_w", "wpe"):
         assert np.abs(gs[n]).max() > 0, n
     m.optimizer_step(0.05)
     m.zero_grad()

@@ -21,7 +21,7 @@ LIB_PATH = os.environ.get("VIT_LIB") or os.path.join(HERE, "libvit_hip.so")  # V
 
 from . import data  # noqa: E402  (configs, canonical layout, seeded synthetic inputs)
 
-VIT_FP32, VIT_BF16 = 0, 1
+VIT_FP32, VIT_BF16, VIT_FP8 = 0, 1, 2
 _lib = None
 
 
@@ -97,6 +97,10 @@ _SIGS = {
     "layernorm_forward_bf16": (None, [P, P, P, P, P, P, I, I, I]),
     "gemm_bf16_ex": (None, [P, LL, P, LL, I, P, LL, I, P, P, I, I, I, I, I]),
     "gemm_bf16_fused": (None, [P, P, LL, P, LL, P, LL, I, P, LL, I, P, P, I, I, I, I]),
+    "mx_scale_size": (LL, [LL, I]),
+    "quantize_mx_bf16_ex": (None, [P, P, P, LL, I, LL, LL]),
+    "quantize_mx_f32_ex": (None, [P, P, P, LL, I, LL, LL]),
+    "gemm_fp8_fused": (None, [P, P, LL, P, LL, P, P, LL, P, P, LL, P, P, I, I, I, I]),
     "gemm_bf16_set_variant": (None, [I]), "gemm_bf16_set_debug": (None, [I]),
     "convert_f32_to_bf16": (None, [P, P, LL]),
     "convert_bf16_to_f32": (None, [P, P, LL]),
@@ -113,6 +117,8 @@ _SIGS = {
     "vit_trainer_stream": (P, [P]),
     "vit_dp_unique_id_size": (I, []), "vit_dp_get_unique_id": (I, [ctypes.c_char_p]),
     "vit_trainer_dp_init": (I, [P, I, I, ctypes.c_char_p, I]),
+    "vit_trainer_dp_ranks": (I, [P]),
+    "vit_trainer_get_dp_snapshot": (I, [P, P]),
     "vit_trainer_set_timing": (I, [P, I]), "vit_trainer_set_concurrency": (I, [P, I]),
     "vit_trainer_set_option": (I, [P, ctypes.c_char_p, I]),
     "vit_trainer_timing": (I, [P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
@@ -515,6 +521,19 @@ class ViT:
 
     def dp_init(self, rank, world, unique_id, overlap=True):
         self._ok(lib().vit_trainer_dp_init(self.h, rank, world, unique_id, int(overlap)), "dp_init")
+
+    def dp_snapshot(self):
+        """the dp_probe snapshot arena (canonical order): each chunk as it stood when reduced."""
+        out = np.empty(self.num_parameters, dtype=np.float32)
+        self._ok(lib().vit_trainer_get_dp_snapshot(self.h, out.ctypes.data_as(P)), "dp_snapshot")
+        return out
+
+    def dp_ranks(self):
+        """ranks RCCL reports for the trainer's communicator (0 without DP)."""
+        n = lib().vit_trainer_dp_ranks(self.h)
+        if n < 0:
+            check("dp_ranks")
+        return n
 
     # ---- stream concurrency (micro-batch streams + weight-gradient stream), on by default
     def set_concurrency(self, on=True):

@@ -50,6 +50,9 @@ struct GemmArgs {
     // use and left zeroed by every launch; nullptr = the calling thread's.  Launches sharing one
     // scratch must be ordered (same stream).
     char* sk_ws = nullptr;
+    // fp8 operands (gemm_fp8): MX scales of A and B in the lane-native layout of gemm_fp8.hip
+    const void* a_scale = nullptr;
+    const void* b_scale = nullptr;
 };
 size_t gemm_sk_bytes();
 
@@ -64,6 +67,26 @@ bool gemm_bf16_supported(const GemmArgs& a);
 // loop only), 4 = 256x256 engine with LDS-DMA prefetch depth 3 instead of 2
 void gemm_set_variant(int v);
 void gemm_set_debug(int flags);
+
+// fp8 (OCP e4m3) operands with MX block scales (one E8M0 per 32 k-elements), fp32 accumulate
+// (v_mfma_scale_f32_32x32x64_f8f6f4): A [M][K], B [N][K] K-contiguous byte rows (lda/ldb in
+// bytes, % 16 == 0), K % 64 == 0, scales from quantize_mx_* (a_scale / b_scale); every epilogue
+// except the split-K ones.
+void gemm_fp8(const GemmArgs& a, hipStream_t s);
+bool gemm_fp8_supported(const GemmArgs& a);
+// MX quantizer: x [R][K] (row stride ldx elements) -> q [R][K] e4m3 (row stride ldq bytes) +
+// scales sl (mx_scale_bytes(R, K) bytes, layout of gemm_fp8.hip)
+void quantize_mx_bf16(uint8_t* q, uint8_t* sl, const bf16_t* x, long long R, int K, long long ldx,
+                      long long ldq, hipStream_t s);
+void quantize_mx_f32(uint8_t* q, uint8_t* sl, const float* x, long long R, int K, long long ldx,
+                     long long ldq, hipStream_t s);
+// `count` dense [R][K] matrices xs elements apart -> q matrices qs bytes apart, scales ss apart
+void quantize_mx_batched_bf16(uint8_t* q, uint8_t* sl, const bf16_t* x, long long R, int K, int count,
+                              long long xs, long long qs, long long ss, hipStream_t s);
+void quantize_mx_batched_f32(uint8_t* q, uint8_t* sl, const float* x, long long R, int K, int count,
+                             long long xs, long long qs, long long ss, hipStream_t s);
+long long mx_rows_padded(long long rows);
+size_t mx_scale_bytes(long long rows, int K);
 
 // column sums: dbias[n] += sum_m X[m*ld + n]   (X fp32 or bf16)
 void colsum_f32(float* dbias, const float* X, int M, int N, long long ld, hipStream_t s);

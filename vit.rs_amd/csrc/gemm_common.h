@@ -1,0 +1,351 @@
+// gemm_common.h — launch parameters, XCD / split-K tile mapping and the fused epilogues shared
+// by the bf16 GEMM engines (gemm.hip) and the fp8 engine (gemm_fp8.hip).
+#pragma once
+#include "gemm.h"
+
+namespace vit {
+
+struct GemmParams {
+    const void* A;
+    const void* B;
+    void* C;
+    void* C2;
+    const void* aux;
+    const float* bias;
+    float* dbias;
+    float* colsum_out;
+    long long lda, ldb, ldc, ldaux;
+    int M, N, K;
+    int kchunk;  // K range per split (multiple of the K tile)
+    int debug_same_tile;
+    int no_epi;  // diagnostic (gemm_bf16_set_debug): skip the epilogue, keep the accumulators live
+    int epi_generic;  // A/B (debug flag 32): the generic (bounds-checked) staged epilogue everywhere
+    int tiles;   // output tiles of the launch (the grid is tiles x K-splits)
+    int stagger;  // first-round start delay of every other workgroup, in s_sleep(127) units
+};
+
+// (tile, K-split) of this workgroup.  Workgroups are dealt round-robin over the 8 XCDs in
+// linear-id order (x fastest), so the XCD-aware remap runs over the whole (split, tile) grid: the
+// ~1/8 of the grid on one XCD is a contiguous range of the same K-split's tiles, which share
+// their A and B K-slices in that XCD's L2 (split-K wgrad launches have tiles x splits blocks).
+__device__ __forceinline__ void split_remap(int tiles, int& tile, int& split) {
+    const int nwg = gridDim.x * gridDim.y;
+    const int l = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, nwg);
+    split = l / tiles;
+    tile = l - split * tiles;
+}
+__device__ __forceinline__ int split_index(int tiles) {
+    int t, s;
+    split_remap(tiles, t, s);
+    return s;
+}
+
+// diagnostic: time the main loop alone (the accumulators stay live so nothing is eliminated)
+template <int NA, int NB>
+__device__ __forceinline__ bool skip_epilogue(const GemmParams& p, f32x4_t (&acc)[NA][NB]) {
+    if (!p.no_epi) return false;
+#pragma unroll
+    for (int a = 0; a < NA; a++)
+#pragma unroll
+        for (int b = 0; b < NB; b++) asm volatile("" ::"v"(acc[a][b]));
+    return true;
+}
+
+// epilogue for one lane's C[m][n..n+3] (n % 4 == 0, m < M, n < N)
+template <int EPI>
+__device__ __forceinline__ void epilogue(const GemmParams& p, int m, int n, f32x4_t& v) {
+    if constexpr (EPI != EPI_F32_ATOMIC && EPI != EPI_BF16_DGELU && EPI != EPI_F32_SLAB) {
+        if (p.bias) {
+            const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
+            v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+        }
+    }
+    const long long off = (long long)m * p.ldc + n;
+    if constexpr (EPI == EPI_F32_STORE) {
+        *reinterpret_cast<float4*>((float*)p.C + off) = make_float4(v[0], v[1], v[2], v[3]);
+    } else if constexpr (EPI == EPI_F32_ACC) {
+        float4* q = reinterpret_cast<float4*>((float*)p.C + off);
+        float4 o = *q;
+        o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
+        *q = o;
+    } else if constexpr (EPI == EPI_F32_ATOMIC) {
+        float* q = (float*)p.C + off;
+        atomicAdd(q + 0, v[0]);
+        atomicAdd(q + 1, v[1]);
+        atomicAdd(q + 2, v[2]);
+        atomicAdd(q + 3, v[3]);
+    } else if constexpr (EPI == EPI_BF16_STORE) {
+        *reinterpret_cast<uint2*>((bf16_t*)p.C + off) =
+            make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+    } else if constexpr (EPI == EPI_BF16_GELU) {
+        *reinterpret_cast<uint2*>((bf16_t*)p.C + off) =
+            make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        *reinterpret_cast<uint2*>((bf16_t*)p.C2 + off) =
+            make_uint2(pack_bf16x2(gelu_fast_f(v[0]), gelu_fast_f(v[1])),
+                       pack_bf16x2(gelu_fast_f(v[2]), gelu_fast_f(v[3])));
+    } else if constexpr (EPI == EPI_F32_RESID) {
+        const float4 r = *reinterpret_cast<const float4*>((const float*)p.aux +
+                                                          (long long)m * p.ldaux + n);
+        *reinterpret_cast<float4*>((float*)p.C + off) =
+            make_float4(v[0] + r.x, v[1] + r.y, v[2] + r.z, v[3] + r.w);
+    } else if constexpr (EPI == EPI_F32_SLAB) {
+        float* slab = (float*)p.C + (long long)split_index(p.tiles) * p.M * p.ldc;
+        *reinterpret_cast<float4*>(slab + off) = make_float4(v[0], v[1], v[2], v[3]);
+    } else if constexpr (EPI == EPI_BF16_DGELU) {
+        const uint2 h = *reinterpret_cast<const uint2*>((const bf16_t*)p.aux +
+                                                        (long long)m * p.ldaux + n);
+        const float x0 = __uint_as_float(h.x << 16), x1 = __uint_as_float(h.x & 0xffff0000u);
+        const float x2 = __uint_as_float(h.y << 16), x3 = __uint_as_float(h.y & 0xffff0000u);
+        v[0] *= gelu_grad_fast_f(x0); v[1] *= gelu_grad_fast_f(x1);
+        v[2] *= gelu_grad_fast_f(x2); v[3] *= gelu_grad_fast_f(x3);
+        *reinterpret_cast<uint2*>((bf16_t*)p.C + off) =
+            make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+    }
+}
+
+// ------------------------------------------------------------- row-contiguous (staged) epilogue
+// Columns n..n+7 of row m (n % 8 == 0), v = raw accumulators: one 16-B (bf16) or 2 x 16-B (fp32)
+// access per lane and operand, so a wave instruction covers whole 128-B lines.  cs accumulates
+// the column sums of the DGELU output (fused bias gradient).
+template <int EPI>
+__device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, float (&v)[8],
+                                          float (&cs)[8]) {
+    if constexpr (EPI != EPI_F32_ATOMIC && EPI != EPI_BF16_DGELU && EPI != EPI_F32_SLAB) {
+        if (p.bias) {
+            const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
+            const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
+            v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+            v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+        }
+    }
+    const long long off = (long long)m * p.ldc + n;
+    auto st_f32 = [&](float* q) {
+        reinterpret_cast<float4*>(q)[0] = make_float4(v[0], v[1], v[2], v[3]);
+        reinterpret_cast<float4*>(q)[1] = make_float4(v[4], v[5], v[6], v[7]);
+    };
+    auto pack8 = [&](const float (&w)[8]) {
+        return make_uint4(pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3]), pack_bf16x2(w[4], w[5]),
+                          pack_bf16x2(w[6], w[7]));
+    };
+    if constexpr (EPI == EPI_F32_STORE) {
+        st_f32((float*)p.C + off);
+    } else if constexpr (EPI == EPI_F32_ACC) {
+        float* q = (float*)p.C + off;
+        const float4 o0 = reinterpret_cast<const float4*>(q)[0];
+        const float4 o1 = reinterpret_cast<const float4*>(q)[1];
+        v[0] += o0.x; v[1] += o0.y; v[2] += o0.z; v[3] += o0.w;
+        v[4] += o1.x; v[5] += o1.y; v[6] += o1.z; v[7] += o1.w;
+        st_f32(q);
+    } else if constexpr (EPI == EPI_F32_ATOMIC) {
+        float* q = (float*)p.C + off;
+#pragma unroll
+        for (int j = 0; j < 8; j++) atomicAdd(q + j, v[j]);
+    } else if constexpr (EPI == EPI_F32_SLAB) {
+        st_f32((float*)p.C + (long long)split_index(p.tiles) * p.M * p.ldc + off);
+    } else if constexpr (EPI == EPI_BF16_STORE) {
+        *reinterpret_cast<uint4*>((bf16_t*)p.C + off) = pack8(v);
+    } else if constexpr (EPI == EPI_BF16_GELU) {
+        float gv[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) gv[j] = gelu_fast_f(v[j]);
+        *reinterpret_cast<uint4*>((bf16_t*)p.C + off) = pack8(v);
+        *reinterpret_cast<uint4*>((bf16_t*)p.C2 + off) = pack8(gv);
+    } else if constexpr (EPI == EPI_F32_RESID) {
+        const float* r = (const float*)p.aux + (long long)m * p.ldaux + n;
+        const float4 r0 = reinterpret_cast<const float4*>(r)[0];
+        const float4 r1 = reinterpret_cast<const float4*>(r)[1];
+        v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
+        v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
+        st_f32((float*)p.C + off);
+    } else if constexpr (EPI == EPI_BF16_DGELU) {
+        const uint4 h = *reinterpret_cast<const uint4*>((const bf16_t*)p.aux + (long long)m * p.ldaux + n);
+        const uint32_t hw[4] = {h.x, h.y, h.z, h.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            v[2 * j] *= gelu_grad_fast_f(__uint_as_float(hw[j] << 16));
+            v[2 * j + 1] *= gelu_grad_fast_f(__uint_as_float(hw[j] & 0xffff0000u));
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) cs[j] += v[j];
+        *reinterpret_cast<uint4*>((bf16_t*)p.C + off) = pack8(v);
+    }
+}
+
+// Epilogue of one wave's 128x64 accumulator tile (8x4 16x16 tiles; lane (i,g) of tile (a,b) holds
+// row 16a+i, columns 16b+4g..+3) through a wave-private LDS area of 64 x 68 fp32 (17 KiB, two
+// passes of 64 rows): each lane then owns 8 consecutive columns of a row, so every global load
+// and store of the epilogue is a 16-B access and a wave instruction covers 8 rows x 128 B (bf16)
+// or 8 rows x 256 B (fp32) instead of 16 rows x 32 B.  Callers guarantee the area is free
+// (every wave past the main loop and its LDS-DMA retired).
+constexpr int STG_LD = 68;                       // padded row (floats): conflict-free b128 access
+constexpr int STG_WAVE_BYTES = 64 * STG_LD * 4;  // 17,408 B per wave
+// Interior wave tiles (all 128 rows < M, all 64 columns < N): one pass of 64 rows with every
+// global load of the pass (aux rows, bias) issued before the first computation, and no branch
+// between loads and stores.  The generic loop below serialised load -> s_waitcnt vmcnt(0) ->
+// compute -> store per 8-row step (the wait also drained the previous step's stores), so the
+// DGELU / RESID epilogues ran one HBM round trip per step.
+template <int EPI>
+__device__ __forceinline__ void staged_pass_interior(const GemmParams& p, const float* st, int rr,
+                                                     int cc, int mrow, int n, float (&cs)[8]) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if constexpr (EPI != EPI_F32_ATOMIC && EPI != EPI_BF16_DGELU && EPI != EPI_F32_SLAB) {
+        if (p.bias) {
+            const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
+            const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
+            bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w;
+            bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+        }
+    }
+    constexpr bool AUX16 = EPI == EPI_BF16_DGELU;
+    constexpr bool AUX32 = EPI == EPI_F32_RESID || EPI == EPI_F32_ACC;
+    u32x4 ax[AUX16 ? 8 : (AUX32 ? 16 : 1)];
+    if constexpr (AUX16) {
+#pragma unroll
+        for (int it = 0; it < 8; it++)
+            ax[it] = *reinterpret_cast<const u32x4*>((const bf16_t*)p.aux + (long long)(mrow + it * 8 + rr) * p.ldaux + n);
+    } else if constexpr (AUX32) {
+        const float* src = EPI == EPI_F32_RESID ? (const float*)p.aux : (const float*)p.C;
+        const long long ld = EPI == EPI_F32_RESID ? p.ldaux : p.ldc;
+#pragma unroll
+        for (int it = 0; it < 8; it++) {
+            const u32x4* q = reinterpret_cast<const u32x4*>(src + (long long)(mrow + it * 8 + rr) * ld + n);
+            ax[2 * it] = q[0];
+            ax[2 * it + 1] = q[1];
+        }
+    }
+    float* slab = nullptr;
+    if constexpr (EPI == EPI_F32_SLAB) slab = (float*)p.C + (long long)split_index(p.tiles) * p.M * p.ldc;
+#pragma unroll
+    for (int it = 0; it < 8; it++) {
+        const int r = it * 8 + rr;
+        const f32x4_t lo = *reinterpret_cast<const f32x4_t*>(st + r * STG_LD + cc);
+        const f32x4_t hi = *reinterpret_cast<const f32x4_t*>(st + r * STG_LD + cc + 4);
+        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const long long off = (long long)(mrow + r) * p.ldc + n;
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] += bv[j];
+        auto pack8 = [](const float (&w)[8]) {
+            return u32x4{pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3]), pack_bf16x2(w[4], w[5]),
+                         pack_bf16x2(w[6], w[7])};
+        };
+        auto st_f32 = [&](float* q) {
+            reinterpret_cast<float4*>(q)[0] = make_float4(v[0], v[1], v[2], v[3]);
+            reinterpret_cast<float4*>(q)[1] = make_float4(v[4], v[5], v[6], v[7]);
+        };
+        if constexpr (EPI == EPI_F32_STORE) {
+            st_f32((float*)p.C + off);
+        } else if constexpr (EPI == EPI_F32_SLAB) {
+            st_f32(slab + off);
+        } else if constexpr (AUX32) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                v[j] += __uint_as_float(ax[2 * it][j]);
+                v[4 + j] += __uint_as_float(ax[2 * it + 1][j]);
+            }
+            st_f32((float*)p.C + off);
+        } else if constexpr (EPI == EPI_BF16_STORE) {
+            *reinterpret_cast<u32x4*>((bf16_t*)p.C + off) = pack8(v);
+        } else if constexpr (EPI == EPI_BF16_GELU) {
+            float gv[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) gv[j] = gelu_fast_f(v[j]);
+            *reinterpret_cast<u32x4*>((bf16_t*)p.C + off) = pack8(v);
+            *reinterpret_cast<u32x4*>((bf16_t*)p.C2 + off) = pack8(gv);
+        } else if constexpr (EPI == EPI_BF16_DGELU) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                v[2 * j] *= gelu_grad_fast_f(__uint_as_float(ax[it][j] << 16));
+                v[2 * j + 1] *= gelu_grad_fast_f(__uint_as_float(ax[it][j] & 0xffff0000u));
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++) cs[j] += v[j];
+            *reinterpret_cast<u32x4*>((bf16_t*)p.C + off) = pack8(v);
+        }
+    }
+}
+
+GemmParams make_gemm_params(const GemmArgs& a, int kchunk);  // gemm.hip
+
+// one 64-row pass of a wave's 128x64 tile, staged in `st` (64 x STG_LD fp32, row r = tile row
+// 64*pass + r): every lane owns 8 consecutive columns of a row per access
+template <int EPI>
+__device__ __forceinline__ void staged_pass(const GemmParams& p, const float* st, int lane, int m0,
+                                            int n0, int pass, bool interior, float (&cs)[8]) {
+    const int rr = lane >> 3, cc = (lane & 7) * 8;
+    if (interior) {
+        staged_pass_interior<EPI>(p, st, rr, cc, m0 + pass * 64, n0 + cc, cs);
+        return;
+    }
+#pragma unroll
+    for (int it = 0; it < 8; it++) {
+        const int r = it * 8 + rr;
+        float v[8];
+        const f32x4_t lo = *reinterpret_cast<const f32x4_t*>(st + r * STG_LD + cc);
+        const f32x4_t hi = *reinterpret_cast<const f32x4_t*>(st + r * STG_LD + cc + 4);
+        v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+        v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+        const int m = m0 + pass * 64 + r, n = n0 + cc;
+        if (m >= p.M) continue;
+        if (n + 8 <= p.N) {
+            epilogue8<EPI>(p, m, n, v, cs);
+        } else if (n + 4 <= p.N) {  // ragged N (N % 8 == 4): the 4-wide form
+            f32x4_t t = lo;
+            epilogue<EPI>(p, m, n, t);
+            if constexpr (EPI == EPI_BF16_DGELU) {
+                const uint2 h = *reinterpret_cast<const uint2*>((const bf16_t*)p.aux + (long long)m * p.ldaux + n);
+                cs[0] += lo[0] * gelu_grad_fast_f(__uint_as_float(h.x << 16));
+                cs[1] += lo[1] * gelu_grad_fast_f(__uint_as_float(h.x & 0xffff0000u));
+                cs[2] += lo[2] * gelu_grad_fast_f(__uint_as_float(h.y << 16));
+                cs[3] += lo[3] * gelu_grad_fast_f(__uint_as_float(h.y & 0xffff0000u));
+            }
+        }
+    }
+}
+template <int EPI>
+__device__ __forceinline__ bool staged_interior(const GemmParams& p, int m0, int n0) {
+    return EPI != EPI_F32_ATOMIC && !p.epi_generic && m0 + 128 <= p.M && n0 + 64 <= p.N;
+}
+// fused bias gradient of the next GEMM: column sums of the DGELU output
+template <int EPI>
+__device__ __forceinline__ void staged_colsum(const GemmParams& p, int lane, int n0, float (&cs)[8]) {
+    if constexpr (EPI == EPI_BF16_DGELU) {
+        if (p.colsum_out) {
+            const int rr = lane >> 3, cc = (lane & 7) * 8;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                float t = cs[j];
+                t += __shfl_xor(t, 8, 64);
+                t += __shfl_xor(t, 16, 64);
+                t += __shfl_xor(t, 32, 64);
+                cs[j] = t;
+            }
+            if (rr == 0) {
+#pragma unroll
+                for (int j = 0; j < 8; j++)
+                    if (n0 + cc + j < p.N) atomicAdd(p.colsum_out + n0 + cc + j, cs[j]);
+            }
+        }
+    }
+}
+
+template <int EPI>
+__device__ __forceinline__ void staged_epilogue(const GemmParams& p, f32x4_t (&acc)[8][4],
+                                                char* stage, int lane, int m0, int n0) {
+    float* st = reinterpret_cast<float*>(stage);
+    const int i = lane & 15, g = lane >> 4;
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const bool interior = staged_interior<EPI>(p, m0, n0);
+#pragma unroll
+    for (int pass = 0; pass < 2; pass++) {
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+                *reinterpret_cast<f32x4_t*>(st + (a * 16 + i) * STG_LD + b * 16 + 4 * g) = acc[pass * 4 + a][b];
+        staged_pass<EPI>(p, st, lane, m0, n0, pass, interior, cs);
+    }
+    staged_colsum<EPI>(p, lane, n0, cs);
+}
+
+}  // namespace vit

@@ -1,0 +1,407 @@
+// gemm_fp8.hip — MXFP8 GEMM for the fp8 mode of matmul_forward / matmul_backward's input gradient
+// (train_vit.rs:384-398, 530-541) and the MX block quantizer that feeds it.
+//
+// Operands are OCP fp8 e4m3 with one E8M0 scale per 32 consecutive k-elements of a row (the OCP
+// MX block scaling), multiplied on v_mfma_scale_f32_32x32x64_f8f6f4 (twice the bf16 MFMA rate,
+// fp32 accumulate, the block scales applied in hardware).  Both operands are K-contiguous byte
+// rows: A [M][K] (activations or output gradients) and B [N][K] (W[n][k] for the forward; the
+// transposed weight copy WT[n][k] for the input gradient).
+//
+// Engine: the bf16 256x256 pipeline of gemm.hip (g2) with bytes in place of bf16.  One LDS slot
+// holds a 64-deep k-step of both 256-row operands (16 KiB each, 64-B rows) = exactly one
+// 32x32x64 MFMA k-step, so the slot cadence, the ring of 4 slots (LDS-DMA 2 steps ahead), the
+// counted vmcnt waits and the staggered wave halves carry over unchanged: per slot and wave,
+// 2 phases x 4 MFMAs of 64 cycles (= g2's 2 x 16 x 16).  8 waves (2 M x 4 N), 128 x 64 per wave =
+// 4 x 2 tiles of 32x32.  MFMA lane layout (tools/probe_mx.hip, measured): lane (r = l&31,
+// h = l>>5) carries k [16h, 16h+16) in bytes 0..15 and k [32+16h, 48+16h) in bytes 16..31 of the
+// step, i.e. 16-B chunks h and 2+h of the 64-B row; its scale byte scales row r, k-block h.
+// LDS images are lane-linear (LDS-DMA); chunk' = chunk ^ ((row >> 2) & 3) on the global source
+// address makes the 32-row fragment reads conflict free.
+//
+// Scales, "lane-native" layout: S[K/64][Rpad/32][64] bytes, Rpad = rows rounded up to 256; byte
+// h*32 + r of row group g at step s is the scale of row 32g + r, k-block 2s + h.  Per slot the
+// tile's scales are 512 contiguous bytes per operand, staged by one 4-byte LDS-DMA per wave;
+// each MFMA reads its lane's byte with one ds_read_u8.  Padding rows carry scale 0 (2^-127).
+#include "gemm_common.h"
+
+namespace vit {
+namespace f8 {
+constexpr int BM = 256, BN = 256, NT = 512;
+constexpr int KB = 64;                           // k bytes (= fp8 elements) per slot
+constexpr int IMG_BYTES = 256 * KB;              // 16 KiB per operand image
+constexpr int SC_BYTES = 1024;                   // scales of one slot: A 512 B | B 512 B
+constexpr int SLOT_BYTES = 2 * IMG_BYTES + SC_BYTES;
+constexpr int DEPTH = 2, NS = DEPTH + 2;
+constexpr int SMEM = NS * SLOT_BYTES > 8 * STG_WAVE_BYTES ? NS * SLOT_BYTES : 8 * STG_WAVE_BYTES;
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int swz(int row) { return (row >> 2) & 3; }
+
+// this wave's 2 data pieces of one operand image (piece blk = 8j + wave: rows 16blk .. 16blk+15)
+__device__ __forceinline__ void stage(const uint8_t* __restrict__ base, long long ld, int row0,
+                                      int rows_lim, int k0, char* img, int wave, int lane) {
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const int blk = j * 8 + wave;
+        const int row = blk * 16 + (lane >> 2);
+        const int c = (lane & 3) ^ swz(row);
+        const int gr = min(row0 + row, rows_lim - 1);
+        const uint8_t* src = base + (long long)gr * ld + k0 + c * 16;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(img + blk * 1024),
+                                         16, 0, 0);
+    }
+}
+// this wave's 128 B of the slot's scales: waves 0-3 the A tile's 8 row groups, 4-7 the B tile's;
+// 4-byte LDS-DMA on lanes 0-31 (every wave issues the same one instruction, so the counted vmcnt
+// waits stay uniform; sub-dword LDS-DMA does not pack lanes at their byte size)
+__device__ __forceinline__ void stage_scales(const uint8_t* __restrict__ sa, const uint8_t* __restrict__ sb,
+                                             int rga, int rgb, int ks, int rga_tot, int rgb_tot,
+                                             char* sc, int wave, int lane) {
+    const bool isb = wave >= 4;
+    const int w4 = wave & 3;
+    const uint8_t* src = isb ? sb + ((long long)ks * rgb_tot + rgb + 2 * w4) * 64
+                             : sa + ((long long)ks * rga_tot + rga + 2 * w4) * 64;
+    if (lane < 32)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 4 * lane),
+                                         (__attribute__((address_space(3))) void*)(sc + (isb ? 512 : 0) + w4 * 128),
+                                         4, 0, 0);
+}
+// rows [r0, r0+32) of an image: chunks h and 2+h of the lane's row
+__device__ __forceinline__ v8i frag(const char* img, int r0, int lane) {
+    const int r = r0 + (lane & 31), h = lane >> 5, sw = swz(r);
+    const u32x4 lo = *reinterpret_cast<const u32x4*>(img + r * KB + ((h ^ sw) << 4));
+    const u32x4 hi = *reinterpret_cast<const u32x4*>(img + r * KB + (((2 + h) ^ sw) << 4));
+    return v8i{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+}
+__device__ __forceinline__ int scale_of(const char* sc, int grp, int lane) {
+    return *reinterpret_cast<const uint8_t*>(sc + grp * 64 + lane);
+}
+__device__ __forceinline__ void wait_vm(int n) {
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+}
+
+struct F8Params {
+    GemmParams p;
+    const uint8_t* sa;
+    const uint8_t* sb;
+    int rga_tot, rgb_tot;  // scale row groups (Rpad / 32) of A and B
+};
+
+// Pipeline (as g2): every 64-deep k-step is two phases of 4 MFMAs per wave; each phase is
+// [LDS fragment reads + LDS-DMA] barrier [MFMAs] barrier; waves 4-7 run one barrier behind.
+// Per step and wave 5 DMA instructions: A half (2 data + 1 scale) in phase 0, B half (2) in
+// phase 1, for step kt + DEPTH into the slot read at step kt - 2.
+template <int EPI>
+__global__ __launch_bounds__(NT, 1) void gemm_kernel(F8Params fp) {
+    const GemmParams& p = fp.p;
+    __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int ntn = cdiv(p.N, BN);
+    int wg, split;
+    split_remap(p.tiles, wg, split);
+    const int tm0 = (wg / ntn) * BM, tn0 = (wg % ntn) * BN;
+    const int nk = p.K / KB;
+    const uint8_t* A = (const uint8_t*)p.A;
+    const uint8_t* B = (const uint8_t*)p.B;
+
+    v16f acc[4][2];
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++) acc[a][b] = v16f{};
+
+    auto slot_of = [&](int st) { return smem + (st % NS) * SLOT_BYTES; };
+    auto issue_a = [&](int st) {  // A image pieces + this wave's scale piece of step st
+        if (st < nk) {
+            stage(A, p.lda, tm0, p.M, st * KB, slot_of(st), wave, lane);
+            stage_scales(fp.sa, fp.sb, tm0 / 32, tn0 / 32, st, fp.rga_tot, fp.rgb_tot,
+                         slot_of(st) + 2 * IMG_BYTES, wave, lane);
+        }
+    };
+    auto issue_b = [&](int st) {
+        if (st < nk) stage(B, p.ldb, tn0, p.N, st * KB, slot_of(st) + IMG_BYTES, wave, lane);
+    };
+    auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // instruction A = the B fragment (rows = output columns), instruction B = the A fragment, so a
+    // lane's accumulator registers run along output columns of one output row (as g2)
+    auto mfma_half = [&](int half, const v8i (&fa)[2], const int (&sa)[2], const v8i (&fb)[2], const int (&sb)[2]) {
+#pragma unroll
+        for (int a = 0; a < 2; a++)
+#pragma unroll
+            for (int b = 0; b < 2; b++)
+                acc[half * 2 + a][b] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+                    fb[b], fa[a], acc[half * 2 + a][b], 0, 0, 0, sb[b], 0, sa[a]);
+    };
+
+    const bool lagging = wave >= 4;
+    if (nk > 0) {
+#pragma unroll
+        for (int st = 0; st < DEPTH; st++) { issue_a(st); issue_b(st); }
+        wait_vm(5 * (min(DEPTH, nk) - 1));  // own pieces of step 0
+        bar();
+        if (lagging) {
+            __builtin_amdgcn_s_setprio(1);  // static priority for the younger half
+            bar();                          // stagger: one barrier behind waves 0-3
+        }
+    }
+    v8i fb[2], fa0[2], fa1[2];
+    int sb_[2], sa0[2], sa1[2];
+    for (int kt = 0; kt < nk; kt++) {
+        const char* img = slot_of(kt);
+        const char* sc = img + 2 * IMG_BYTES;
+        // ---- phase 0: B fragments, A tiles 0-1 (rows 0-63 of the wave tile)
+#pragma unroll
+        for (int b = 0; b < 2; b++) {
+            fb[b] = frag(img + IMG_BYTES, wn * 64 + b * 32, lane);
+            sb_[b] = scale_of(sc + 512, wn * 2 + b, lane);
+        }
+#pragma unroll
+        for (int a = 0; a < 2; a++) {
+            fa0[a] = frag(img, wm * 128 + a * 32, lane);
+            sa0[a] = scale_of(sc, wm * 4 + a, lane);
+        }
+        issue_a(kt + DEPTH);
+        bar();
+        mfma_half(0, fa0, sa0, fb, sb_);
+        bar();
+        // ---- phase 1: A tiles 2-3
+#pragma unroll
+        for (int a = 0; a < 2; a++) {
+            fa1[a] = frag(img, wm * 128 + (2 + a) * 32, lane);
+            sa1[a] = scale_of(sc, wm * 4 + 2 + a, lane);
+        }
+        // own pieces of step kt+1 landed: the younger ones are the A half of step kt+DEPTH (3)
+        wait_vm(kt + DEPTH < nk ? 3 : 0);
+        issue_b(kt + DEPTH);
+        bar();
+        mfma_half(1, fa1, sa1, fb, sb_);
+        bar();
+    }
+    if (nk > 0 && !lagging) bar();  // balance the stagger barrier
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(0);
+
+    if (p.no_epi) {  // diagnostic: main loop only; keep the accumulators live (in 16-B pieces: a
+                     // 64-B "v" asm operand makes hipcc drop the host stubs of the other instances)
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+#pragma unroll
+            for (int b = 0; b < 2; b++)
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    asm volatile("" ::"v"(f32x4_t{acc[a][b][4 * q], acc[a][b][4 * q + 1], acc[a][b][4 * q + 2],
+                                                   acc[a][b][4 * q + 3]}));
+        return;
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // 32x32 accumulators -> the row-staged epilogue: lane l of tile (a,b) holds output row
+    // 32a + (l&31), columns 32b + 8q + 4(l>>5) + 0..3 in registers 4q..4q+3
+    float* st = reinterpret_cast<float*>(smem + wave * STG_WAVE_BYTES);
+    const int m0 = tm0 + wm * 128, n0 = tn0 + wn * 64;
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const bool interior = staged_interior<EPI>(p, m0, n0);
+    const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int pass = 0; pass < 2; pass++) {
+#pragma unroll
+        for (int a = 0; a < 2; a++)
+#pragma unroll
+            for (int b = 0; b < 2; b++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const v16f& v = acc[pass * 2 + a][b];
+                    *reinterpret_cast<f32x4_t*>(st + (a * 32 + r) * STG_LD + b * 32 + 8 * q + 4 * h) =
+                        f32x4_t{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+                }
+        staged_pass<EPI>(p, st, lane, m0, n0, pass, interior, cs);
+    }
+    staged_colsum<EPI>(p, lane, n0, cs);
+}
+
+// ------------------------------------------------------------------------------- quantizer
+// MX block quantization of a [R][K] fp32 / bf16 matrix (row stride ldx elements) into fp8 e4m3
+// rows (stride ldq bytes) + lane-native scales.  One wave per (32-row group, 64-deep k-step):
+// lane (r, h) owns row 32g + r, k-block 2s + h (32 elements): amax -> the smallest power of two
+// 2^X with amax / 2^X <= 448 (the e4m3 maximum; v_cvt_pk_fp8_f32 does not saturate) -> E8M0 byte
+// X + 127 -> x * 2^-X (exact) rounded to nearest even by v_cvt_pk_fp8_f32.  Rows >= R get scale 0.
+__device__ __forceinline__ int mx_scale_byte(float amax) {
+    if (!(amax > 0.f)) return 127;
+    const uint32_t u = __float_as_uint(amax);
+    const int e = (int)((u >> 23) & 0xff), mant = (int)(u & 0x7fffff);
+    int s = e - 8 + (mant > 0x600000 ? 1 : 0);  // X + 127 with X = ceil(log2(amax / 448))
+    return s < 0 ? 0 : (s > 254 ? 254 : s);
+}
+// blockIdx.y: matrix of a batch (x, q, sl advance by xs elements, qs bytes, ss bytes)
+template <typename TX>
+__global__ __launch_bounds__(256) void quantize_mx_k(uint8_t* __restrict__ q, uint8_t* __restrict__ sl,
+                                                     const TX* __restrict__ x, int R, int K, long long ldx,
+                                                     long long ldq, int rg_tot, long long xs, long long qs,
+                                                     long long ss) {
+    x += blockIdx.y * xs;
+    q += blockIdx.y * qs;
+    sl += blockIdx.y * ss;
+    const int lane = threadIdx.x & 63;
+    const long long wv = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int nks = K / 64;
+    if (wv >= (long long)rg_tot * nks) return;
+    const int ks = (int)(wv / rg_tot), rg = (int)(wv - (long long)ks * rg_tot);
+    const int r = lane & 31, h = lane >> 5;
+    const int row = rg * 32 + r;
+    const int k0 = ks * 64 + h * 32;
+    float v[32];
+    if (row < R) {
+        const TX* src = x + (long long)row * ldx + k0;
+        if constexpr (sizeof(TX) == 2) {
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const u32x4 w = reinterpret_cast<const u32x4*>(src)[c];
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    v[8 * c + 2 * e] = __uint_as_float(w[e] << 16);
+                    v[8 * c + 2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < 8; c++) {
+                const float4 w = reinterpret_cast<const float4*>(src)[c];
+                v[4 * c] = w.x; v[4 * c + 1] = w.y; v[4 * c + 2] = w.z; v[4 * c + 3] = w.w;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 32; j++) v[j] = 0.f;
+    }
+    float amax = 0.f;
+#pragma unroll
+    for (int j = 0; j < 32; j++) amax = fmaxf(amax, fabsf(v[j]));
+    const int sb = row < R ? mx_scale_byte(amax) : 0;
+    sl[((long long)ks * rg_tot + rg) * 64 + lane] = (uint8_t)sb;
+    if (row >= R) return;
+    const float inv = __uint_as_float((uint32_t)(254 - sb) << 23);  // 2^(127 - sb), exact
+    uint32_t w[8];
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+        int t = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * c] * inv, v[4 * c + 1] * inv, 0, false);
+        t = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * c + 2] * inv, v[4 * c + 3] * inv, t, true);
+        w[c] = (uint32_t)t;
+    }
+    u32x4* dst = reinterpret_cast<u32x4*>(q + (long long)row * ldq + k0);
+    dst[0] = u32x4{w[0], w[1], w[2], w[3]};
+    dst[1] = u32x4{w[4], w[5], w[6], w[7]};
+}
+}  // namespace f8
+
+long long mx_rows_padded(long long rows) { return (rows + 255) / 256 * 256; }
+size_t mx_scale_bytes(long long rows, int K) { return (size_t)mx_rows_padded(rows) / 32 * (K / 64) * 64; }
+
+bool gemm_fp8_supported(const GemmArgs& a) {
+    auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+    return a.a_kcontig && a.b_kcontig && a.K % 64 == 0 && a.lda % 16 == 0 && a.ldb % 16 == 0 &&
+           a.N % 4 == 0 && a.ldc % 4 == 0 && al16(a.A) && al16(a.B) && a.a_scale && a.b_scale &&
+           a.epi != EPI_F32_ATOMIC && a.epi != EPI_F32_SLAB;
+}
+
+void gemm_fp8(const GemmArgs& a, hipStream_t s) {
+    if (a.M <= 0 || a.N <= 0) return;
+    if (!gemm_fp8_supported(a)) {
+        set_error("gemm_fp8: unsupported shape/layout M=%d N=%d K=%d lda=%lld ldb=%lld epi=%d", a.M, a.N,
+                  a.K, a.lda, a.ldb, a.epi);
+        return;
+    }
+    f8::F8Params fp;
+    fp.p = make_gemm_params(a, a.K);
+    const int tiles = cdiv(a.M, f8::BM) * cdiv(a.N, f8::BN);
+    fp.p.tiles = tiles;
+    fp.sa = (const uint8_t*)a.a_scale;
+    fp.sb = (const uint8_t*)a.b_scale;
+    fp.rga_tot = (int)(mx_rows_padded(a.M) / 32);
+    fp.rgb_tot = (int)(mx_rows_padded(a.N) / 32);
+    switch (a.epi) {
+#define VIT_CASE(E) \
+    case E: f8::gemm_kernel<E><<<tiles, f8::NT, 0, s>>>(fp); break;
+        VIT_CASE(EPI_F32_STORE)
+        VIT_CASE(EPI_F32_ACC)
+        VIT_CASE(EPI_BF16_STORE)
+        VIT_CASE(EPI_BF16_GELU)
+        VIT_CASE(EPI_F32_RESID)
+        VIT_CASE(EPI_BF16_DGELU)
+#undef VIT_CASE
+        default: set_error("gemm_fp8: unsupported epilogue %d", a.epi); return;
+    }
+    after_launch("gemm_fp8");
+}
+
+template <typename TX>
+static void quantize_mx(uint8_t* q, uint8_t* sl, const TX* x, long long R, int K, long long ldx,
+                        long long ldq, int count, long long xs, long long qs, long long ss, hipStream_t s) {
+    if (R <= 0 || count <= 0) return;
+    if (K % 64 || ldx % (16 / sizeof(TX)) || ldq % 16 || xs % (16 / sizeof(TX)) || qs % 16 ||
+        ((uintptr_t)x & 15) || ((uintptr_t)q & 15) || R >= (1LL << 31)) {
+        set_error("quantize_mx: K %% 64 and 16-B aligned rows required (K=%d)", K);
+        return;
+    }
+    const int rg = (int)(mx_rows_padded(R) / 32);
+    const long long waves = (long long)rg * (K / 64);
+    f8::quantize_mx_k<TX><<<dim3(cdiv(waves, 4), count), 256, 0, s>>>(q, sl, x, (int)R, K, ldx, ldq, rg, xs, qs, ss);
+    after_launch("quantize_mx");
+}
+void quantize_mx_bf16(uint8_t* q, uint8_t* sl, const bf16_t* x, long long R, int K, long long ldx,
+                      long long ldq, hipStream_t s) {
+    quantize_mx<bf16_t>(q, sl, x, R, K, ldx, ldq, 1, 0, 0, 0, s);
+}
+void quantize_mx_f32(uint8_t* q, uint8_t* sl, const float* x, long long R, int K, long long ldx,
+                     long long ldq, hipStream_t s) {
+    quantize_mx<float>(q, sl, x, R, K, ldx, ldq, 1, 0, 0, 0, s);
+}
+void quantize_mx_batched_bf16(uint8_t* q, uint8_t* sl, const bf16_t* x, long long R, int K, int count,
+                              long long xs, long long qs, long long ss, hipStream_t s) {
+    quantize_mx<bf16_t>(q, sl, x, R, K, K, K, count, xs, qs, ss, s);
+}
+void quantize_mx_batched_f32(uint8_t* q, uint8_t* sl, const float* x, long long R, int K, int count,
+                             long long xs, long long qs, long long ss, hipStream_t s) {
+    quantize_mx<float>(q, sl, x, R, K, K, K, count, xs, qs, ss, s);
+}
+
+}  // namespace vit
+
+// ============================================================================ C ABI (vit_ops.h)
+using namespace vit;
+extern "C" {
+long long mx_scale_size(long long rows, int K) { return (long long)mx_scale_bytes(rows, K); }
+void quantize_mx_bf16_ex(uint8_t* q, uint8_t* scales, const uint16_t* x, long long R, int K, long long ldx,
+                         long long ldq) {
+    quantize_mx_bf16(q, scales, x, R, K, ldx, ldq, stream());
+}
+void quantize_mx_f32_ex(uint8_t* q, uint8_t* scales, const float* x, long long R, int K, long long ldx,
+                        long long ldq) {
+    quantize_mx_f32(q, scales, x, R, K, ldx, ldq, stream());
+}
+void gemm_fp8_fused(void* C, void* C2, long long ldc, const void* aux, long long ldaux, const uint8_t* A,
+                    const uint8_t* a_scale, long long lda, const uint8_t* B, const uint8_t* b_scale,
+                    long long ldb, const float* bias, float* colsum_out, int M, int N, int K, int epi) {
+    GemmArgs a;
+    a.C = C; a.C2 = C2; a.ldc = ldc; a.aux = aux; a.ldaux = ldaux;
+    a.A = A; a.a_scale = a_scale; a.lda = lda; a.B = B; a.b_scale = b_scale; a.ldb = ldb;
+    a.bias = bias; a.colsum_out = colsum_out; a.M = M; a.N = N; a.K = K; a.epi = epi;
+    gemm_fp8(a, stream());
+}
+}

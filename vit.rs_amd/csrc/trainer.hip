@@ -34,14 +34,14 @@ enum TimerClass {
     TC_PATCH, TC_LN_FWD, TC_QKV_FWD, TC_ATTN_FWD, TC_PROJ_FWD, TC_FC_FWD, TC_FCPROJ_FWD, TC_HEAD,
     TC_FCPROJ_DGRAD, TC_FCPROJ_WGRAD, TC_FC_DGRAD, TC_FC_WGRAD, TC_PROJ_DGRAD, TC_PROJ_WGRAD,
     TC_ATTN_BWD, TC_QKV_DGRAD, TC_QKV_WGRAD, TC_LN_BWD, TC_COLSUM, TC_PATCH_BWD, TC_SGD, TC_MISC,
-    TC_COUNT
+    TC_QUANT, TC_COUNT
 };
 const char* kTimerNames[TC_COUNT] = {
     "patch_embed_fwd", "layernorm_fwd", "gemm_qkv_fwd", "attention_fwd", "gemm_proj_fwd",
     "gemm_fc_fwd", "gemm_fcproj_fwd", "head", "gemm_fcproj_dgrad", "gemm_fcproj_wgrad",
     "gemm_fc_dgrad", "gemm_fc_wgrad", "gemm_proj_dgrad", "gemm_proj_wgrad", "attention_bwd",
     "gemm_qkv_dgrad", "gemm_qkv_wgrad", "layernorm_bwd", "bias_colsum", "patch_embed_bwd", "sgd",
-    "misc"};
+    "misc", "quantize_mx"};
 
 // out[r][n] = vec[n] for r < rows (the bias start value of a split-K head GEMM)
 __global__ void bcast_rows_k(float* __restrict__ out, const float* __restrict__ vec, int rows, int n) {
@@ -247,6 +247,10 @@ struct Trainer {
     // ---- DP
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1, overlap = 1;
+    // option "dp_probe": each chunk is also copied, on s_comm right after its all-reduce, into this
+    // snapshot arena (same layout as grads): snapshot == final grads bitwise proves every chunk
+    // was final when the comm stream reduced it (at world 1 the sum itself is an identity)
+    float* dp_snap = nullptr;
 
     // ---- timing
     bool timing = false;
@@ -274,6 +278,26 @@ struct Trainer {
     }
 
     bool layered(int ti) const { return ti >= P_LN1W && ti <= P_FCPROJB; }
+    bool lowp() const { return prec != VIT_FP32; }  // bf16 or fp8 mode (the fast path)
+    bool fp8() const { return prec == VIT_FP8; }
+    // ---- fp8 mode: MXFP8 copies of the four layer weights (forward B operand, [N][K]) and of their
+    // transposes (input-gradient B operand, [Cin][OC]), refreshed after every optimizer step, and
+    // per-micro-batch scratch for the quantized A operand of each fp8 GEMM
+    static constexpr int NWK = 4;
+    const int wkinds[NWK] = {P_QKVW, P_ATTPROJW, P_FCW, P_FCPROJW};
+    struct QMat { uint8_t* q = nullptr; uint8_t* s = nullptr; };
+    QMat wq[NWK], wtq[NWK];            // [L] matrices each, in the source's memory order
+    long long wq_n[NWK]{}, wq_k[NWK]{};  // forward view: N x K per layer
+    uint8_t* act_q[4]{};
+    uint8_t* act_s[4]{};
+    int wslot(int k, int l) const {    // memory-order index of layer l's copy of weight kind k
+        const long long stride = L > 1 ? off[wkinds[k] * L + 1] - off[wkinds[k] * L] : 0;
+        return stride < 0 ? L - 1 - l : l;
+    }
+    int wkind_of(int ti) const {
+        for (int k = 0; k < NWK; k++) if (wkinds[k] == ti) return k;
+        return -1;
+    }
     long long per_layer(int ti) const { return canon_size[ti] / L; }
     float* P(int ti, int l = 0) const { return params + off[ti * L + l]; }
     float* G(int ti, int l = 0) const { return grads + off[ti * L + l]; }
@@ -419,8 +443,12 @@ struct Trainer {
         BT = (long long)B * T;
         prec = precision;
         device = dev;
-        if (c->in_ch != 3 || C % NH || L < 1 || L > 64 || B < 1) {
+        if (c->in_ch != 3 || C % NH || L < 1 || L > 64 || B < 1 || prec < VIT_FP32 || prec > VIT_FP8) {
             set_error("trainer: unsupported config");
+            return false;
+        }
+        if (prec == VIT_FP8 && C % 64) {
+            set_error("trainer: fp8 mode needs C %% 64 == 0 (MX k-steps of 64), C=%d", C);
             return false;
         }
         if (hipSetDevice(dev) != hipSuccess) { set_error("trainer: hipSetDevice(%d)", dev); return false; }
@@ -472,7 +500,7 @@ struct Trainer {
         dres_b = alloc<float>(BT * C);
         emb_tmp = alloc<float>((long long)B * NP * C);
         la.resize(L);
-        if (prec == VIT_BF16) {
+        if (lowp()) {
             if (!(attn_fused_supported(T, C, NH) || attn_generic_supported(T, C, NH)) || C % 8) {
                 set_error("trainer: bf16 path needs an even head size <= 128 and C%%8==0 (T=%d C=%d NH=%d)", T, C, NH);
                 return false;
@@ -515,7 +543,23 @@ struct Trainer {
             // slabs: <= 32 splits of the largest weight gradient (4C x C)
             gemm_ws_bytes = (size_t)32 * 4 * C * (size_t)std::max(C, KP) * sizeof(float);
             gemm_ws = alloc<float>((long long)(gemm_ws_bytes / sizeof(float)));
-            attn_part = alloc<float>((long long)B * NH * (3 * 64 + T));  // bias partials | delta
+            attn_part = alloc<float>((long long)B * NH * (3 * (C / NH) + T));  // bias partials | delta
+            if (fp8()) {
+                const long long ns[NWK] = {3LL * C, C, 4LL * C, C}, ks[NWK] = {C, C, C, 4LL * C};
+                for (int k = 0; k < NWK; k++) {
+                    wq_n[k] = ns[k];
+                    wq_k[k] = ks[k];
+                    wq[k].q = alloc<uint8_t>(L * ns[k] * ks[k]);
+                    wq[k].s = alloc<uint8_t>((long long)L * mx_scale_bytes(ns[k], (int)ks[k]));
+                    wtq[k].q = alloc<uint8_t>(L * ns[k] * ks[k]);
+                    wtq[k].s = alloc<uint8_t>((long long)L * mx_scale_bytes(ks[k], (int)ns[k]));
+                }
+                // A-operand scratch per micro-batch stream: rows x (widest K = 4C) bytes + scales
+                for (int k = 0; k < MAXMB; k++) {
+                    act_q[k] = alloc<uint8_t>(BT * 4 * C);
+                    act_s[k] = alloc<uint8_t>((long long)mx_scale_bytes(BT, 4 * C));
+                }
+            }
         } else {
             patches_f = alloc<float>((long long)B * NP * KP);
             dpatch_f = alloc<float>((long long)B * NP * C);
@@ -588,7 +632,7 @@ struct Trainer {
     }
 
     void refresh_bf16() {
-        if (prec != VIT_BF16) return;
+        if (!lowp()) return;
         to_bf16_k<<<grid_for(arena_elems, 256), 256, 0, s>>>(pbf, params, arena_elems);
         after_launch("params_to_bf16");
         refresh_transposed();
@@ -604,6 +648,46 @@ struct Trainer {
             const int l0 = stride < 0 ? L - 1 : 0;
             transpose_bf16(WT(kinds[k], l0), W(kinds[k], l0), rows[k], cols[k], L, stride < 0 ? -stride : stride, s);
         }
+        if (fp8()) refresh_fp8();
+    }
+    // MXFP8 weight copies: W [N][K] from the fp32 master, WT [Cin][OC] from the bf16 transpose;
+    // one batched launch per kind over the L layers (a constant stride apart in the arena)
+    void refresh_fp8() {
+        tbeg(TC_QUANT, 0);
+        for (int k = 0; k < NWK; k++) {
+            const long long stride = L > 1 ? off[wkinds[k] * L + 1] - off[wkinds[k] * L] : 0;
+            const int l0 = stride < 0 ? L - 1 : 0;
+            const long long as = stride < 0 ? -stride : stride;
+            const long long N = wq_n[k], K = wq_k[k];
+            quantize_mx_batched_f32(wq[k].q, wq[k].s, P(wkinds[k], l0), N, (int)K, L, as, N * K,
+                                    (long long)mx_scale_bytes(N, (int)K), s);
+            quantize_mx_batched_bf16(wtq[k].q, wtq[k].s, WT(wkinds[k], l0), K, (int)N, L, as, N * K,
+                                     (long long)mx_scale_bytes(K, (int)N), s);
+        }
+        tend();
+    }
+    QMat wq_of(int ti, int l) const {
+        const int k = wkind_of(ti), j = wslot(k, l);
+        return {wq[k].q + (long long)j * wq_n[k] * wq_k[k], wq[k].s + (long long)j * mx_scale_bytes(wq_n[k], (int)wq_k[k])};
+    }
+    QMat wtq_of(int ti, int l) const {
+        const int k = wkind_of(ti), j = wslot(k, l);
+        return {wtq[k].q + (long long)j * wq_n[k] * wq_k[k], wtq[k].s + (long long)j * mx_scale_bytes(wq_k[k], (int)wq_n[k])};
+    }
+    // a forward (transposed = false) or input-gradient (true) GEMM of weight ti, layer l: bf16
+    // mode as given; fp8 mode quantizes the bf16 A operand into the stream's scratch and runs the
+    // MXFP8 engine against the weight's fp8 copy
+    void gemm_w(int cls, GemmArgs a, int ti, int l, bool transposed, int mb, hipStream_t st) {
+        if (!fp8()) { gemm(cls, a, true, st); return; }
+        tbeg(TC_QUANT, 0, st);
+        quantize_mx_bf16(act_q[mb], act_s[mb], (const bf16_t*)a.A, a.M, a.K, a.lda, a.K, st);
+        tend();
+        const QMat w = transposed ? wtq_of(ti, l) : wq_of(ti, l);
+        a.A = act_q[mb]; a.lda = a.K; a.a_scale = act_s[mb];
+        a.B = w.q; a.ldb = a.K; a.b_scale = w.s; a.b_kcontig = true;
+        tbeg(cls, 2.0 * a.M * (double)a.N * a.K, st);
+        gemm_fp8(a, st);
+        tend();
     }
 
     // ------------------------------------------------------------------ head (both modes)
@@ -616,7 +700,7 @@ struct Trainer {
         GemmArgs a;
         a.A = lnf; a.lda = C; a.B = P(P_HEADW); a.ldb = C; a.C = logits; a.ldc = NC;
         a.bias = P(P_HEADB); a.M = B; a.N = NC; a.K = C; a.epi = EPI_F32_STORE;
-        if (prec == VIT_BF16) {
+        if (lowp()) {
             // fast path: the M = B head GEMMs have 64 output tiles for 256 CUs, so they run
             // split-K with float atomics onto the bias (fp32 mode keeps the ordered sums)
             bcast_rows_k<<<cdiv((long long)B * NC, 256), 256, 0, s>>>(logits, P(P_HEADB), B, NC);
@@ -638,12 +722,12 @@ struct Trainer {
         GemmArgs a;  // dlnf += dlogits . head_w
         a.A = dlogits; a.lda = NC; a.a_kcontig = true;
         a.B = P(P_HEADW); a.ldb = C; a.b_kcontig = false;
-        a.C = dlnf; a.ldc = C; a.M = B; a.N = C; a.K = NC; a.epi = prec == VIT_BF16 ? EPI_F32_ATOMIC : EPI_F32_ACC;
+        a.C = dlnf; a.ldc = C; a.M = B; a.N = C; a.K = NC; a.epi = lowp() ? EPI_F32_ATOMIC : EPI_F32_ACC;
         gemm_f32(a, s);
         GemmArgs w;  // dhead_w += dlogits^T . lnf
         w.A = dlogits; w.lda = NC; w.a_kcontig = false;
         w.B = lnf; w.ldb = C; w.b_kcontig = false;
-        w.C = G(P_HEADW); w.ldc = C; w.M = NC; w.N = C; w.K = B; w.epi = prec == VIT_BF16 ? EPI_F32_ATOMIC : EPI_F32_ACC;
+        w.C = G(P_HEADW); w.ldc = C; w.M = NC; w.N = C; w.K = B; w.epi = lowp() ? EPI_F32_ATOMIC : EPI_F32_ACC;
         gemm_f32(w, s);
         colsum_f32(G(P_HEADB), dlogits, B, NC, NC, s);
         VIT_HIP(hipMemsetAsync(dcls_x, 0, (size_t)B * C * 4, s));
@@ -693,7 +777,7 @@ struct Trainer {
                 GemmArgs q;
                 q.A = a.ln1 + r0 * C; q.lda = C; q.B = W(P_QKVW, l); q.ldb = C; q.C = a.qkv + r0 * 3 * C;
                 q.ldc = 3 * C; q.bias = P(P_QKVB, l); q.M = (int)R; q.N = 3 * C; q.K = C; q.epi = EPI_BF16_STORE;
-                gemm(TC_QKV_FWD, q, true, st);
+                gemm_w(TC_QKV_FWD, q, P_QKVW, l, false, mb, st);
                 tbeg(TC_ATTN_FWD, 4.0 * Bm * (double)T * T * C, st);
                 attn_forward_fused(a.atty + r0 * C, a.lse + (long long)mb * Bm * NH * T, a.qkv + r0 * 3 * C, Bm, T, C, NH, st);
                 tend();
@@ -701,7 +785,7 @@ struct Trainer {
                 pr.A = a.atty + r0 * C; pr.lda = C; pr.B = W(P_ATTPROJW, l); pr.ldb = C; pr.C = a.res2 + r0 * C;
                 pr.ldc = C; pr.bias = P(P_ATTPROJB, l); pr.aux = x; pr.ldaux = C;
                 pr.M = (int)R; pr.N = C; pr.K = C; pr.epi = EPI_F32_RESID;
-                gemm(TC_PROJ_FWD, pr, true, st);
+                gemm_w(TC_PROJ_FWD, pr, P_ATTPROJW, l, false, mb, st);
                 tbeg(TC_LN_FWD, 0, st);
                 ln_forward_bf16(a.ln2 + r0 * C, a.ln2_mean + r0, a.ln2_rstd + r0, a.res2 + r0 * C, P(P_LN2W, l),
                                 P(P_LN2B, l), R, C, st);
@@ -710,12 +794,12 @@ struct Trainer {
                 f.A = a.ln2 + r0 * C; f.lda = C; f.B = W(P_FCW, l); f.ldb = C; f.C = a.fch + r0 * 4 * C;
                 f.C2 = a.fchg + r0 * 4 * C; f.ldc = 4 * C; f.bias = P(P_FCB, l); f.M = (int)R; f.N = 4 * C;
                 f.K = C; f.epi = EPI_BF16_GELU;
-                gemm(TC_FC_FWD, f, true, st);
+                gemm_w(TC_FC_FWD, f, P_FCW, l, false, mb, st);
                 GemmArgs fp;
                 fp.A = a.fchg + r0 * 4 * C; fp.lda = 4 * C; fp.B = W(P_FCPROJW, l); fp.ldb = 4 * C;
                 fp.C = a.res3 + r0 * C; fp.ldc = C; fp.bias = P(P_FCPROJB, l); fp.aux = a.res2 + r0 * C;
                 fp.ldaux = C; fp.M = (int)R; fp.N = C; fp.K = 4 * C; fp.epi = EPI_F32_RESID;
-                gemm(TC_FCPROJ_FWD, fp, true, st);
+                gemm_w(TC_FCPROJ_FWD, fp, P_FCPROJW, l, false, mb, st);
             }
         }
         mb_join();
@@ -779,7 +863,7 @@ struct Trainer {
                 d1.C = dfch + r0 * 4 * C; d1.ldc = 4 * C; d1.aux = a.fch + r0 * 4 * C; d1.ldaux = 4 * C;
                 d1.M = (int)R; d1.N = 4 * C; d1.K = C; d1.epi = EPI_BF16_DGELU;
                 d1.colsum_out = G(P_FCB, l);
-                gemm(TC_FCPROJ_DGRAD, d1, true, ms[mb]);
+                gemm_w(TC_FCPROJ_DGRAD, d1, P_FCPROJW, l, true, mb, ms[mb]);
             }
             // fc: dln2 = dfch . fcw;  fcw += dfch^T . ln2
             wgrad(TC_FC_WGRAD, dfch, 4 * C, a.ln2, C, G(P_FCW, l), EV_DFCH, EV_W2);
@@ -788,7 +872,7 @@ struct Trainer {
                 GemmArgs d2;
                 d2.A = dfch + r0 * 4 * C; d2.lda = 4 * C; dgrad_b(d2, P_FCW, l, 4 * C, C);
                 d2.C = dln_bf + r0 * C; d2.ldc = C; d2.M = (int)R; d2.N = C; d2.K = 4 * C; d2.epi = EPI_BF16_STORE;
-                gemm(TC_FC_DGRAD, d2, true, ms[mb]);
+                gemm_w(TC_FC_DGRAD, d2, P_FCW, l, true, mb, ms[mb]);
                 // ln2 backward + residual: dres2 = dres3 + LN2'(dln2); attproj_b += colsum(dres2)
                 after_wgrad(EV_W3, ms[mb]);  // the previous layer's attproj wgrad has read rbB
                 tbeg(TC_LN_BWD, 0, ms[mb]);
@@ -805,13 +889,13 @@ struct Trainer {
                 GemmArgs d3;
                 d3.A = rbB + r0 * C; d3.lda = C; dgrad_b(d3, P_ATTPROJW, l, C, C);
                 d3.C = datty + r0 * C; d3.ldc = C; d3.M = (int)R; d3.N = C; d3.K = C; d3.epi = EPI_BF16_STORE;
-                gemm(TC_PROJ_DGRAD, d3, true, ms[mb]);
+                gemm_w(TC_PROJ_DGRAD, d3, P_ATTPROJW, l, true, mb, ms[mb]);
                 // attention (+ qkv_b)
                 after_wgrad(EV_W4, ms[mb]);  // the previous layer's qkv wgrad has read dqkv
                 tbeg(TC_ATTN_BWD, 8.0 * Bm * (double)T * T * C, ms[mb]);
                 attn_backward_fused(dqkv + r0 * 3 * C, datty + r0 * C, a.qkv + r0 * 3 * C, a.atty + r0 * C,
                                     a.lse + (long long)mb * Bm * NH * T, Bm, T, C, NH, ms[mb], G(P_QKVB, l),
-                                    attn_part + (long long)mb * Bm * NH * (3 * 64 + T));
+                                    attn_part + (long long)mb * Bm * NH * (3 * (C / NH) + T));
                 tend();
             }
             // qkv
@@ -821,7 +905,7 @@ struct Trainer {
                 GemmArgs d4;
                 d4.A = dqkv + r0 * 3 * C; d4.lda = 3 * C; dgrad_b(d4, P_QKVW, l, 3 * C, C);
                 d4.C = dln_bf + r0 * C; d4.ldc = C; d4.M = (int)R; d4.N = C; d4.K = 3 * C; d4.epi = EPI_BF16_STORE;
-                gemm(TC_QKV_DGRAD, d4, true, ms[mb]);
+                gemm_w(TC_QKV_DGRAD, d4, P_QKVW, l, true, mb, ms[mb]);
                 // ln1 backward: dres = dres2 + LN1'(dln1); fcproj_b of layer l-1 += colsum(dres)
                 after_wgrad(EV_W1, ms[mb]);  // this layer's fcproj wgrad has read rbA
                 tbeg(TC_LN_BWD, 0, ms[mb]);
@@ -950,7 +1034,7 @@ struct Trainer {
         if (!comm || !overlap) return;
         VIT_HIP(hipEventRecord(chunk_ev[c], s));
         VIT_HIP(hipStreamWaitEvent(s_comm, chunk_ev[c], 0));
-        if (two_streams && prec == VIT_BF16) {  // the chunk's gradients also come from s2 / ms[]
+        if (two_streams && lowp()) {  // the chunk's gradients also come from s2 / ms[]
             VIT_HIP(hipEventRecord(chunk_ev2[c], s2));
             VIT_HIP(hipStreamWaitEvent(s_comm, chunk_ev2[c], 0));
             for (int k = 1; k < nmb; k++) {
@@ -962,6 +1046,8 @@ struct Trainer {
         const long long o = chunk_off[c], n = chunk_off[c + 1] - chunk_off[c];
         ncclResult_t r = ncclAllReduce(grads + o, grads + o, (size_t)n, ncclFloat32, ncclSum, comm, s_comm);
         if (r != ncclSuccess) set_error("ncclAllReduce(chunk %d): %s", c, ncclGetErrorString(r));
+        if (dp_snap)
+            VIT_HIP(hipMemcpyAsync(dp_snap + o, grads + o, (size_t)n * 4, hipMemcpyDeviceToDevice, s_comm));
     }
     void finish_allreduce() {
         if (!comm) return;  // (world 1 with a communicator still runs RCCL: the tested path)
@@ -1029,24 +1115,24 @@ struct Trainer {
         const float bc2 = 1.0f - (float)pow((double)hp.beta2, (double)adam_t);
         tbeg(TC_SGD, 0);
         adamw_k<<<grid_for(arena_elems / 4, 256), 256, 0, s>>>(
-            params, prec == VIT_BF16 ? pbf : nullptr, grads, adam_m, adam_v, arena_elems, lr,
+            params, lowp() ? pbf : nullptr, grads, adam_m, adam_v, arena_elems, lr,
             hp.beta1, hp.beta2, 1.0f - hp.beta1, 1.0f - hp.beta2, bc1, bc2, hp.eps, hp.weight_decay);
         after_launch("adamw");
-        if (prec == VIT_BF16) refresh_transposed();
         tend();
+        if (lowp()) refresh_transposed();
     }
 
     void step(float lr) {
         finish_allreduce();
         tbeg(TC_SGD, 0);
-        if (prec == VIT_BF16) {
+        if (lowp()) {
             sgd_bf16_k<<<grid_for(arena_elems / 4, 256), 256, 0, s>>>(params, pbf, grads, arena_elems, lr);
             after_launch("sgd_bf16");
-            refresh_transposed();
         } else {
             sgd(params, grads, arena_elems, lr, s);
         }
         tend();
+        if (lowp()) refresh_transposed();
     }
 };
 
@@ -1143,7 +1229,7 @@ int vit_trainer_set_batch_device(vit_trainer_t* h, const float* px, const int* l
 int vit_trainer_forward(vit_trainer_t* h, int b_global) {
     auto& t = h->t;
     t.b_global = b_global > 0 ? b_global : t.B;
-    if (t.prec == VIT_BF16) t.forward_bf16(); else t.forward_f32();
+    if (t.lowp()) t.forward_bf16(); else t.forward_f32();
     return vit::has_error();
 }
 int vit_trainer_zero_grad(vit_trainer_t* h) {
@@ -1162,7 +1248,7 @@ int vit_trainer_backward(vit_trainer_t* h) {
         set_error("vit_trainer_backward: the batch has no targets (forward-only batch)");
         return 1;
     }
-    if (t.prec == VIT_BF16) t.backward_bf16(); else t.backward_f32();
+    if (t.lowp()) t.backward_bf16(); else t.backward_f32();
     return vit::has_error();
 }
 int vit_trainer_step(vit_trainer_t* h, float lr) {
@@ -1205,7 +1291,7 @@ int vit_trainer_eval(vit_trainer_t* h, int* host_pred, int* host_correct) {
     auto& t = h->t;
     if (host_correct) *host_correct = -1;
     t.b_global = t.B;
-    if (t.prec == VIT_BF16) t.forward_bf16(); else t.forward_f32();
+    if (t.lowp()) t.forward_bf16(); else t.forward_f32();
     VIT_HIP(hipMemsetAsync(t.preds + t.B, 0, 4, t.s));
     vit::argmax_rows_k<<<cdiv(t.B, 4), 256, 0, t.s>>>(t.preds, t.preds + t.B, t.logits,
                                                  t.has_targets ? t.labels : nullptr, t.B, t.NC);
@@ -1317,6 +1403,26 @@ int vit_trainer_dp_init(vit_trainer_t* h, int rank, int world, const char* uid, 
     }
     return 0;
 }
+int vit_trainer_get_dp_snapshot(vit_trainer_t* h, float* host) {
+    auto& t = h->t;
+    if (!t.dp_snap) {
+        set_error("vit_trainer_get_dp_snapshot: option dp_probe is off");
+        return 1;
+    }
+    VIT_HIP(hipStreamSynchronize(t.s_comm));
+    t.device_to_canon(t.dp_snap, host);
+    return vit::has_error();
+}
+int vit_trainer_dp_ranks(vit_trainer_t* h) {
+    if (!h->t.comm) return 0;
+    int n = 0;
+    ncclResult_t r = ncclCommCount(h->t.comm, &n);
+    if (r != ncclSuccess) {
+        set_error("ncclCommCount: %s", ncclGetErrorString(r));
+        return -1;
+    }
+    return n;
+}
 int vit_trainer_set_concurrency(vit_trainer_t* h, int on) {
     auto& t = h->t;
     VIT_HIP(hipStreamSynchronize(t.s2));
@@ -1334,6 +1440,13 @@ int vit_trainer_set_option(vit_trainer_t* h, const char* name, int value) {
         t.nmb = t.pick_nmb(value);
     } else if (n == "dgrad_transposed") {
         t.dgrad_wt = value != 0;
+    } else if (n == "dp_probe") {
+        if (value && !t.dp_snap) {
+            t.dp_snap = t.alloc<float>(t.arena_elems);
+            if (t.dp_snap) VIT_HIP(hipMemset(t.dp_snap, 0, t.arena_elems * 4));
+        } else if (!value) {
+            t.dp_snap = nullptr;  // the arena stays allocated until destroy
+        }
     } else {
         set_error("vit_trainer_set_option: unknown option '%s'", n.c_str());
         return 1;
