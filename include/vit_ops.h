@@ -123,6 +123,15 @@ void attention_backward_fused_bf16(uint16_t* dinp, const uint16_t* dout, const u
                                    int NH);
 void layernorm_forward_bf16(uint16_t* out, float* mean, float* rstd, const float* inp,
                             const float* weight, const float* bias, int B, int T, int C);
+/* train_vit.rs:603 with the LN-output gradient in bf16 (as the trainer's dgrad GEMMs write it):
+ * dinp, dweight, dbias (fp32) += */
+void layernorm_backward_bf16(float* dinp, float* dweight, float* dbias, const uint16_t* dout,
+                             const float* inp, const float* weight, const float* mean,
+                             const float* rstd, int B, int T, int C);
+/* train_vit.rs:482 / :639 (D4) in the form the fused GEMM epilogues use (logistic tanh, raw
+ * v_exp / v_rcp): out_bf16 = gelu(inp_bf16); dinp_f32 += gelu'(inp_bf16) * dout_bf16 */
+void gelu_forward_bf16(uint16_t* out, const uint16_t* inp, int N);
+void gelu_backward_bf16(float* dinp, const uint16_t* inp, const uint16_t* dout, int N);
 /* generic bf16 GEMM (the engine under matmul_*_bf16), for tests and tools:
  * C[M,N] (epilogue)= A . B with A(m,k) = a_kcontig ? A[m*lda+k] : A[k*lda+m],
  * B(k,n) = b_kcontig ? B[n*ldb+k] : B[k*ldb+n].  epi: 0 f32 store, 1 f32 +=, 2 f32 atomic +=

@@ -387,3 +387,75 @@ def test_gemm_bf16_fused_epilogues(gpu, engine, M, N, K):
     want = (ar @ wkr) * _gelu_grad64(xr)
     assert rel_err(v.bf16_to_f32(c4.numpy()).reshape(M, N), want) < 1e-2
     assert rel_err(cs.numpy(), 1.0 + want.sum(0)) < 1e-2
+
+
+# ------------------------------------------------------------------ bf16 op-level family
+@pytest.mark.parametrize("rows,C", [(394, 192), (100, 768), (7, 1000)])
+def test_layernorm_backward_bf16(gpu, oracle64, rows, C):
+    """layernorm_backward_bf16 (train_vit.rs:603, bf16 LN-output gradient as the dgrad GEMMs write
+    it) vs the fp64 oracle on the same bf16-rounded dout: += semantics on all three outputs."""
+    v, o = gpu, oracle64
+    rng = np.random.default_rng(C + 1)
+    x, w, b = rng.normal(size=rows * C) * 3 + 1, rng.normal(size=C), rng.normal(size=C)
+    out, m, r = np.zeros(rows * C), np.zeros(rows), np.zeros(rows)
+    o.call("layernorm_forward", out, m, r, x, w, b, rows, 1, C)
+    dyb = v.bf16_bits(rng.normal(size=rows * C).astype(np.float32))
+    dyr = v.bf16_to_f32(dyb).astype(np.float64)
+    p0 = rng.normal(size=rows * C)
+    di, dw, db = p0.copy(), np.ones(C), np.zeros(C)
+    o.call("layernorm_backward", di, dw, db, dyr, x, w, m, r, rows, 1, C)
+    gdi, gdw, gdb = D(v, p0), D(v, np.ones(C)), Z(v, C)
+    v.call("layernorm_backward_bf16", gdi, gdw, gdb, D(v, dyb, np.uint16), D(v, x), D(v, w), D(v, m), D(v, r),
+           rows, 1, C)
+    assert rel_err(gdi.numpy(), di) < 1e-4 and rel_err(gdw.numpy(), dw) < 1e-5 and rel_err(gdb.numpy(), db) < 1e-5
+
+
+def test_gelu_bf16_pair(gpu, oracle64):
+    """gelu_forward_bf16 / gelu_backward_bf16 (train_vit.rs:482, :639 with D4) vs the fp64 oracle
+    on bf16-rounded inputs: forward within bf16 output rounding, backward (+= fp32) 1e-5."""
+    v, o = gpu, oracle64
+    rng = np.random.default_rng(12)
+    n = 100003
+    xb = v.bf16_bits((rng.normal(size=n) * 3).astype(np.float32))
+    gb = v.bf16_bits(rng.normal(size=n).astype(np.float32))
+    xr, gr = v.bf16_to_f32(xb).astype(np.float64), v.bf16_to_f32(gb).astype(np.float64)
+    ref = np.zeros(n)
+    o.call("gelu_forward", ref, xr, n)
+    out = Z(v, n, np.uint16)
+    v.call("gelu_forward_bf16", out, D(v, xb, np.uint16), n)
+    assert rel_err(v.bf16_to_f32(out.numpy()), ref) < 4e-3
+    p0 = rng.normal(size=n)
+    dref = p0.copy()
+    o.call("gelu_backward", dref, xr, gr, n)
+    dout = D(v, p0)
+    v.call("gelu_backward_bf16", dout, D(v, xb, np.uint16), D(v, gb, np.uint16), n)
+    assert rel_err(dout.numpy(), dref) < 1e-5
+
+
+def test_attention_forward_null_scores(gpu, oracle32):
+    """attention_forward with preatt / att NULL (nullable in fused use): same output,
+    nothing else written."""
+    v, o = gpu, oracle32
+    B, T, C, NH = 2, 17, 32, 2
+    rng = np.random.default_rng(3)
+    x = o.arr(rng.normal(size=B * T * 3 * C))
+    n = B * T * NH * T
+    ref, pre, att = o.arr(np.zeros(B * T * C)), o.arr(np.zeros(n)), o.arr(np.zeros(n))
+    o.call("attention_forward", ref, pre, att, x, B, T, C, NH)
+    out = Z(v, B * T * C)
+    v.call("attention_forward", out, None, None, D(v, x), B, T, C, NH)
+    assert rel_err(out.numpy(), ref) < 1e-5
+    gatt = Z(v, n)
+    v.call("attention_forward", out, None, gatt, D(v, x), B, T, C, NH)
+    assert rel_err(gatt.numpy(), att) < 1e-5
+
+
+def test_trainer_rejects_out_of_range_labels(gpu):
+    v = gpu
+    cfg = v.data.CONFIGS["test"]
+    m = v.ViT.build(cfg, 2, v.VIT_FP32, params=v.data.init_params(cfg, "parity", seed=1))
+    px, lab = v.data.synthetic_batch(cfg, 2, seed=2)
+    lab[1] = cfg.num_classes
+    with pytest.raises(v.VitError, match="outside"):
+        m.set_batch(px, lab)
+    m.close()

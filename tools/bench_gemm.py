@@ -30,6 +30,8 @@ def main():
                     help="comma-separated gemm_bf16_set_debug flag sets to A/B (2 = no epilogue, "
                          "4 = g2 prefetch depth 3); default 0 (and 2 with --no-epi)")
     ap.add_argument("--only", default=None, help="comma-separated GEMM names")
+    ap.add_argument("--fp8", action="store_true",
+                    help="also time the MXFP8 engine (variant 8) on the forward / dgrad GEMMs")
     args = ap.parse_args()
     L = vit.lib()
     assert L.vit_init(0) == 0
@@ -50,6 +52,11 @@ def main():
     bias = vit.DeviceArray.from_numpy(rng.uniform(-1, 1, size=4 * C).astype(np.float32))
     csum = vit.DeviceArray.zeros(4 * C, np.float32)
     e0, e1 = L.vit_event_create(), L.vit_event_create()
+    if args.fp8:  # MXFP8 copies of the A and weight operands (quantized once)
+        q_act = vit.DeviceArray.zeros(big, np.uint8)
+        s_act = vit.DeviceArray.zeros(int(L.mx_scale_size(BT, 4 * C)) * 4, np.uint8)
+        q_w = vit.DeviceArray.zeros(4 * C * C, np.uint8)
+        s_w = vit.DeviceArray.zeros(int(L.mx_scale_size(4 * C, 4 * C)) * 4, np.uint8)
 
     # name, M, N, K, a_kcontig, lda, b_kcontig, ldb, epi
     g = [
@@ -57,10 +64,11 @@ def main():
         ("fwd_proj", BT, C, C, 1, C, 1, C, 5),
         ("fwd_fc", BT, 4 * C, C, 1, C, 1, C, 4),
         ("fwd_fcproj", BT, C, 4 * C, 1, 4 * C, 1, 4 * C, 5),
-        ("dgrad_fcproj", BT, 4 * C, C, 1, C, 0, 4 * C, 6),
-        ("dgrad_fc", BT, C, 4 * C, 1, 4 * C, 0, C, 0),
-        ("dgrad_proj", BT, C, C, 1, C, 0, C, 3),
-        ("dgrad_qkv", BT, C, 3 * C, 1, 3 * C, 0, C, 0),
+        # dgrads read the transposed weight copy (K-contiguous), as the trainer does
+        ("dgrad_fcproj", BT, 4 * C, C, 1, C, 1, C, 6),
+        ("dgrad_fc", BT, C, 4 * C, 1, 4 * C, 1, 4 * C, 3),
+        ("dgrad_proj", BT, C, C, 1, C, 1, C, 3),
+        ("dgrad_qkv", BT, C, 3 * C, 1, 3 * C, 1, 3 * C, 3),
         ("wgrad_fcproj", C, 4 * C, BT, 0, C, 0, 4 * C, 2),
         ("wgrad_fc", 4 * C, C, BT, 0, 4 * C, 0, C, 2),
         ("wgrad_proj", C, C, BT, 0, C, 0, C, 2),
@@ -69,10 +77,18 @@ def main():
     if args.only:
         keep = set(args.only.split(","))
         g = [x for x in g if x[0] in keep]
-    variants = [int(v) for v in args.variants.split(",")]
+    variants = [int(v) for v in args.variants.split(",")] + ([8] if args.fp8 else [])
     modes = [int(x) for x in args.modes.split(",")] if args.modes else ([0, 2] if args.no_epi else [0])
 
-    def run(name, M, N, K, ak, lda, bk, ldb, epi):
+    def run(name, M, N, K, ak, lda, bk, ldb, epi, var=2):
+        if var == 8:
+            if epi == 2:
+                return
+            aux = aux16.ptr if epi == 6 else (aux32.ptr if epi == 5 else None)
+            L.gemm_fp8_fused(out.ptr if epi in (0, 5) else out2.ptr, out.ptr if epi == 4 else None, N, aux, N,
+                             q_act.ptr, s_act.ptr, K, q_w.ptr, s_w.ptr, K, bias.ptr if epi != 6 else None,
+                             csum.ptr if epi == 6 else None, M, N, K, epi)
+            return
         if epi == 2:
             L.gemm_bf16_ex(out.ptr, N, act.ptr, lda, ak, act2.ptr, ldb, bk, None, None, M, N, K, 2, 0)
         else:
@@ -86,15 +102,20 @@ def main():
         for sh in g:
             for var in variants:
                 for mode in modes:
-                    L.gemm_bf16_set_variant(var)
+                    if var == 8 and sh[8] == 2:
+                        continue
+                    if var == 8:  # operands of this shape quantized (untimed)
+                        L.quantize_mx_bf16_ex(q_act.ptr, s_act.ptr, act.ptr, sh[1], sh[3], sh[3], sh[3])
+                        L.quantize_mx_bf16_ex(q_w.ptr, s_w.ptr, wts.ptr, sh[2], sh[3], sh[3], sh[3])
+                    L.gemm_bf16_set_variant(var if var != 8 else 2)
                     L.gemm_bf16_set_debug(mode)
                     for _ in range(2):
-                        run(*sh)
+                        run(*sh, var=var)
                     L.vit_sync()
                     vit.check(sh[0])
                     L.vit_event_record(e0)
                     for _ in range(args.iters):
-                        run(*sh)
+                        run(*sh, var=var)
                     L.vit_event_record(e1)
                     L.vit_sync()
                     ms = L.vit_event_elapsed_ms(e0, e1) / args.iters
@@ -110,6 +131,9 @@ def main():
         cells = []
         for v in variants:
             for m in modes:
+                if (name, v, m) not in res:
+                    cells.append("-")
+                    continue
                 ms = float(np.median(res[(name, v, m)]))
                 tot[(v, m)] = tot.get((v, m), 0.0) + ms
                 cells.append(f"{ms * 1e3:7.1f}us {fl / ms / 1e9:6.0f}TF")
@@ -117,7 +141,7 @@ def main():
     fl_all = sum(2.0 * x[1] * x[2] * x[3] for x in g)
     print("total per layer: " + "  ".join(
         f"v{v}/f{m} {tot[(v, m)]:.3f} ms ({fl_all / tot[(v, m)] / 1e9:.0f} TF/s)"
-        for v in variants for m in modes))
+        for v in variants for m in modes if v != 8))
 
 
 if __name__ == "__main__":

@@ -95,6 +95,9 @@ _SIGS = {
     "vit_attention_kernel_kind": (I, [I, I, I]),
     "attention_backward_fused_bf16": (None, [P, P, P, P, P, I, I, I, I]),
     "layernorm_forward_bf16": (None, [P, P, P, P, P, P, I, I, I]),
+    "layernorm_backward_bf16": (None, [P, P, P, P, P, P, P, P, I, I, I]),
+    "gelu_forward_bf16": (None, [P, P, I]),
+    "gelu_backward_bf16": (None, [P, P, P, I]),
     "gemm_bf16_ex": (None, [P, LL, P, LL, I, P, LL, I, P, P, I, I, I, I, I]),
     "gemm_bf16_fused": (None, [P, P, LL, P, LL, P, LL, I, P, LL, I, P, P, I, I, I, I]),
     "mx_scale_size": (LL, [LL, I]),

@@ -3,6 +3,9 @@
 // Format: the llm.c convention of ViT::build_from_checkpoint (/root/reference/train_vit.rs:
 // 89-143: 256-int header at byte 0, fp32 type-major parameters at byte 1024) completed with the
 // ViT tensors and an optional AdamW state; see the header file for the field table.
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -165,7 +168,8 @@ int vit_checkpoint_write(const char* path, const vit_config_t* cfg, const float*
         bool ok = write_all(fh.f, hdr.data(), VIT_CKPT_HEADER_BYTES) &&
                   write_all(fh.f, params, (size_t)n * 4);
         if (ok && m) ok = write_all(fh.f, m, (size_t)n * 4) && write_all(fh.f, v, (size_t)n * 4);
-        ok = ok && fflush(fh.f) == 0;
+        // durable before the rename: the data blocks must reach the disk before the new name does
+        ok = ok && fflush(fh.f) == 0 && fsync(fileno(fh.f)) == 0;
         if (!ok) {
             set_error("checkpoint %s: write failed", tmp.c_str());
             fclose(fh.f);
@@ -178,6 +182,15 @@ int vit_checkpoint_write(const char* path, const vit_config_t* cfg, const float*
         set_error("checkpoint %s: rename failed", path);
         remove(tmp.c_str());
         return 1;
+    }
+    // and the rename itself: fsync the directory entry
+    std::string dir(path);
+    const size_t slash = dir.find_last_of('/');
+    dir = slash == std::string::npos ? "." : (slash == 0 ? "/" : dir.substr(0, slash));
+    const int dfd = open(dir.c_str(), O_RDONLY | O_DIRECTORY);
+    if (dfd >= 0) {
+        fsync(dfd);
+        close(dfd);
     }
     return 0;
 }

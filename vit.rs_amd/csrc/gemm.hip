@@ -899,6 +899,14 @@ __device__ __forceinline__ void group_order(int t, int ntm, int ntn, int& tm, in
 template <bool AK, bool BKC, int EPI>
 __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
     __shared__ __attribute__((aligned(1024))) char smem[NSLOT * SLOT_BYTES];
+    // phase offset (debug flag 256*n): the second resident workgroup of each CU (dispatch slots
+    // 256..511) starts n x s_sleep(127) later, so the two workgroups of a CU reach their epilogues
+    // at different times and one's stores overlap the other's main loop
+    if (p.stagger) {
+        const int lin = blockIdx.y * gridDim.x + blockIdx.x;
+        if (lin >= 256 && lin < 512)
+            for (int k = 0; k < p.stagger; k++) __builtin_amdgcn_s_sleep(127);
+    }
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 1, wn = wave & 1;

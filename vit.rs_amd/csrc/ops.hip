@@ -34,6 +34,18 @@ __global__ void gelu_bwd_k(float* __restrict__ dinp, const float* __restrict__ i
          i += (long long)gridDim.x * blockDim.x)
         dinp[i] += gelu_grad_f(inp[i]) * dout[i];
 }
+// bf16 GELU pair of the fused epilogues (gelu_fast_f / gelu_grad_fast_f, common.h), standalone
+__global__ void gelu_fwd_bf16_k(bf16_t* __restrict__ out, const bf16_t* __restrict__ inp, long long n) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        out[i] = f2bf(gelu_fast_f(bf2f(inp[i])));
+}
+__global__ void gelu_bwd_bf16_k(float* __restrict__ dinp, const bf16_t* __restrict__ inp,
+                                const bf16_t* __restrict__ dout, long long n) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        dinp[i] += gelu_grad_fast_f(bf2f(inp[i])) * bf2f(dout[i]);
+}
 __global__ void sgd_k(float* __restrict__ p, const float* __restrict__ g, long long n, float lr) {
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
          i += (long long)gridDim.x * blockDim.x)
@@ -348,7 +360,9 @@ __global__ __launch_bounds__(256) void softmax_k(float* __restrict__ probs,
 __global__ void ce_fwd_k(float* __restrict__ losses, const float* __restrict__ probs,
                          const int* __restrict__ targets, long long rows, int V) {
     const long long r = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (r < rows) losses[r] = -logf(probs[r * V + targets[r]]);
+    if (r >= rows) return;
+    const int t = targets[r];  // out-of-range labels (the host checks host arrays) give NaN, never an OOB read
+    losses[r] = (t >= 0 && t < V) ? -logf(probs[r * V + t]) : __builtin_nanf("");
 }
 __global__ void ce_bwd_k(float* __restrict__ dlogits, const float* __restrict__ dlosses,
                          const float* __restrict__ probs, const int* __restrict__ targets,
@@ -759,6 +773,22 @@ void matmul_backward_bf16(float* dinp, float* dweight, float* dbias, const uint1
         a.dbias = dbias;  // fused column sum of dout
         gemm_bf16(a, stream());
     }
+}
+void layernorm_backward_bf16(float* dinp, float* dweight, float* dbias, const uint16_t* dout,
+                             const float* inp, const float* weight, const float* mean,
+                             const float* rstd, int B, int T, int C) {
+    ln_backward_any(dinp, nullptr, nullptr, dweight, dbias, nullptr, (const bf16_t*)dout, inp, weight,
+                    mean, rstd, (long long)B * T, C, stream());
+}
+void gelu_forward_bf16(uint16_t* out, const uint16_t* inp, int N) {
+    if (N <= 0) return;
+    gelu_fwd_bf16_k<<<grid_for(N, 256), 256, 0, stream()>>>(out, inp, N);
+    after_launch("gelu_forward_bf16");
+}
+void gelu_backward_bf16(float* dinp, const uint16_t* inp, const uint16_t* dout, int N) {
+    if (N <= 0) return;
+    gelu_bwd_bf16_k<<<grid_for(N, 256), 256, 0, stream()>>>(dinp, inp, dout, N);
+    after_launch("gelu_backward_bf16");
 }
 void layernorm_forward_bf16(uint16_t* out, float* mean, float* rstd, const float* inp,
                             const float* weight, const float* bias, int B, int T, int C) {

@@ -502,7 +502,7 @@ struct Trainer {
         la.resize(L);
         if (lowp()) {
             if (!(attn_fused_supported(T, C, NH) || attn_generic_supported(T, C, NH)) || C % 8) {
-                set_error("trainer: bf16 path needs an even head size <= 128 and C%%8==0 (T=%d C=%d NH=%d)", T, C, NH);
+                set_error("trainer: bf16 / fp8 path needs head size 32, 64, 80, 96 or 128 and C %% 8 == 0 (T=%d C=%d NH=%d)", T, C, NH);
                 return false;
             }
             // a patch whose im2col row (3*P*P) is not a multiple of 8 bf16 (ViT-H/14: 588) cannot
@@ -1211,8 +1211,17 @@ int vit_trainer_get_grads(vit_trainer_t* h, float* hg) {
     h->t.device_to_canon(h->t.grads, hg);
     return vit::has_error();
 }
+static bool labels_ok(const int* lab, int n, int nc) {
+    for (int i = 0; i < n; i++)
+        if (lab[i] < 0 || lab[i] >= nc) {
+            set_error("label %d of the batch is %d, outside [0, %d)", i, lab[i], nc);
+            return false;
+        }
+    return true;
+}
 int vit_trainer_set_batch(vit_trainer_t* h, const float* px, const int* lab) {
     auto& t = h->t;
+    if (lab && !labels_ok(lab, t.B, t.NC)) return 1;
     VIT_HIP(hipMemcpyAsync(t.pixels, px, (size_t)t.B * 3 * t.cfg.img * t.cfg.img * 4, hipMemcpyHostToDevice, t.s));
     t.has_targets = lab != nullptr;
     if (lab) VIT_HIP(hipMemcpyAsync(t.labels, lab, (size_t)t.B * 4, hipMemcpyHostToDevice, t.s));
@@ -1268,6 +1277,7 @@ int vit_trainer_set_batch_u8(vit_trainer_t* h, const unsigned char* images, cons
         set_error("vit_trainer_set_batch_u8: null argument");
         return 1;
     }
+    if (labels && !labels_ok(labels, h->t.B, h->t.NC)) return 1;
     return h->t.set_batch_u8(images, labels, mean3, std3) ? 0 : 1;
 }
 int vit_trainer_step_adamw(vit_trainer_t* h, float lr, float beta1, float beta2, float eps,
