@@ -1,7 +1,7 @@
 """Per-tensor parity of the native trainer against the fp32 CPU oracle (the reference loops,
 oracle/oracle.c), for every precision mode, written as JSON (profiles/<tag>_parity.json).
 
-    python tools/parity_report.py [--out profiles/r02_parity.json]
+    python tests/parity_report.py [--out profiles/r02_parity.json]
 
 For each (config, batch, mode): relative error of the loss, and for the logits and each of the 20
 parameter-gradient tensors (canonical order, train_vit.rs:10-27 + ViT tensors):
@@ -18,7 +18,7 @@ import time
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # tests/ -> repo root
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 from vitpkg import vit  # noqa: E402

@@ -248,17 +248,24 @@ def test_matmul_bf16(gpu, oracle64, M, N, K):
     # past the LDS range (T > 320): the generic VALU kernels
     (1, 330, 1, 64, "auto"), (1, 400, 2, 32, "auto"),
     # the generic kernels forced on shapes the MFMA kernels also take (same outputs)
-    (2, 257, 2, 80, "generic"), (1, 70, 2, 96, "generic")])
+    (2, 257, 2, 80, "generic"), (1, 70, 2, 96, "generic"),
+    # the backward variants (VIT_ATTN_BWD): paired roles, and the non-persistent one-pass kernel
+    # on shapes the persistent one-pass kernel takes by default (B*NH > CUs: several items per WG)
+    (2, 197, 3, 64, "pair"), (3, 33, 4, 64, "pair"), (1, 70, 1, 128, "pair"),
+    (2, 197, 3, 64, "one"), (3, 33, 4, 64, "one"),
+    (24, 197, 12, 64, "mfma"), (30, 77, 12, 32, "mfma"), (30, 100, 12, 64, "mfma"), (50, 40, 8, 64, "mfma")])
 def test_attention_fused_bf16(gpu, oracle64, monkeypatch, B, T, NH, HS, path):
     """bf16 attention (fused MFMA kernels for head sizes 32/64/80/96/128 while the head's images fit
     the LDS, generic VALU kernels past that) vs the fp64 oracle of the reference loops on the same
     bf16-rounded inputs."""
     if path == "generic":
         monkeypatch.setenv("VIT_ATTN_GENERIC", "1")
+    if path in ("pair", "one"):
+        monkeypatch.setenv("VIT_ATTN_BWD", path)
     v, o = gpu, oracle64
     C = HS * NH
     kind = v.lib().vit_attention_kernel_kind(T, C, NH)
-    assert kind == {"mfma": 1, "generic": 2}.get(path, 2), (path, kind)
+    assert kind == {"mfma": 1, "pair": 1, "one": 1, "generic": 2}.get(path, 2), (path, kind)
     rng = np.random.default_rng(T * 7 + NH)
     qkv = rng.normal(size=B * T * 3 * C).astype(np.float32)
     qb = v.bf16_bits(qkv)
@@ -287,6 +294,46 @@ def test_attention_fused_bf16(gpu, oracle64, monkeypatch, B, T, NH, HS, path):
     r = dinp.reshape(B, T, 3, C)
     for k, name in enumerate("qkv"):
         assert rel_err(g[:, :, k], r[:, :, k]) < 3e-2, name
+
+
+@pytest.mark.parametrize("B,T,NH", [(2, 197, 3), (24, 197, 12), (30, 100, 12)])
+def test_attention_backward_variants(gpu, oracle64, monkeypatch, B, T, NH):
+    """Every backward kernel (VIT_ATTN_BWD: persistent one-pass default, one workgroup per item,
+    paired roles) on the same inputs: each within the bf16 gate of the fp64 oracle, the variants
+    within bf16 rounding of each other, and each deterministic (two launches bitwise equal)."""
+    v, o = gpu, oracle64
+    HS = 64
+    C = HS * NH
+    rng = np.random.default_rng(T * 7 + NH)  # the seed of test_attention_fused_bf16
+    qkv = rng.normal(size=B * T * 3 * C).astype(np.float32)
+    qb = v.bf16_bits(qkv)
+    qr = v.bf16_to_f32(qb).astype(np.float64)
+    n = B * T * NH * T
+    out, pre, att = np.zeros(B * T * C), np.zeros(n), np.zeros(n)
+    o.call("attention_forward", out, pre, att, qr, B, T, C, NH)
+    gq = D(v, qb, np.uint16)
+    gout, glse = Z(v, B * T * C, np.uint16), Z(v, B * NH * T)
+    v.call("attention_forward_fused_bf16", gout, glse, gq, B, T, C, NH)
+    dyb = v.bf16_bits(rng.normal(size=B * T * C).astype(np.float32))
+    dinp = np.zeros(B * T * 3 * C)
+    o.call("attention_backward", dinp, np.zeros(n), np.zeros(n), v.bf16_to_f32(dyb).astype(np.float64), qr, att,
+           B, T, C, NH)
+    r = dinp.reshape(B, T, 3, C)
+    res = {}
+    for variant in ["persistent", "one", "pair"]:
+        monkeypatch.setenv("VIT_ATTN_BWD", variant)
+        outs = []
+        for _ in range(2):
+            gd = Z(v, B * T * 3 * C, np.uint16)
+            v.call("attention_backward_fused_bf16", gd, D(v, dyb, np.uint16), gq, gout, glse, B, T, C, NH)
+            outs.append(gd.numpy())
+        assert np.array_equal(outs[0], outs[1]), (variant, "nondeterministic")
+        res[variant] = v.bf16_to_f32(outs[0]).reshape(B, T, 3, C)
+        errs = [rel_err(res[variant][:, :, k], r[:, :, k]) for k in range(3)]
+        print("\n", variant, " ".join(f"{e:.4f}" for e in errs))
+        assert max(errs) < 3e-2, (variant, errs)
+    for variant in ["one", "pair"]:
+        assert rel_err(res[variant], res["persistent"]) < 2e-2, variant
 
 
 def test_error_channel(gpu):

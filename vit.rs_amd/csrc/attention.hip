@@ -8,6 +8,8 @@
 // bf16 trainer path: the fused MFMA kernels of attn_fused.h (head sizes 32/64/80/96/128, T up to
 // what LDS holds — 320 at every supported head size), instantiated per head size in attn_h*.hip,
 // dispatched here.  Longer sequences fall back to the generic VALU kernels below (same outputs).
+#include <string>
+
 #include "attn_fused.h"
 
 namespace vit {
@@ -474,6 +476,22 @@ static bool gen_lds_attr(const void* k, size_t bytes) {
     return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) == hipSuccess;
 }
 
+int fa::attn_bwd_variant() {  // read per launch (host-side, cheap) so tests can A/B in one process
+    const char* e = getenv("VIT_ATTN_BWD");
+    if (!e) return 0;
+    const std::string v(e);
+    return v == "one" ? 1 : v == "pair" ? 2 : 0;
+}
+int fa::attn_cu_count() {
+    static int n = [] {
+        int dev = 0, cu = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
+        return cu > 0 ? cu : 256;
+    }();
+    return n;
+}
+
 // head sizes with MFMA instantiations (attn_h*.hip) and the longest T their LDS images hold
 static int fa_max_t(int hs) {
     switch (hs) {
@@ -511,6 +529,11 @@ __global__ __launch_bounds__(1024) void attn_colsum_reduce_k(float* __restrict__
         for (int j = 0; j < nb; j++) a += red[j * HS + d];
         atomicAdd(out + sct * C + h * HS + d, a);
     }
+}
+
+size_t attn_backward_ws_floats(int B, int T, int C, int NH) {
+    const size_t per_bh = std::max((size_t)T, (size_t)3 * (C / NH) * fa::ATTN_PART_ROWS);
+    return (size_t)B * NH * per_bh;
 }
 
 void attn_forward_fused(bf16_t* out, float* lse, const bf16_t* qkv, int B, int T, int C, int NH,
@@ -580,23 +603,22 @@ void attn_backward_fused(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, co
         return;
     }
     const int HS = C / NH;
-    // ws: [B*NH*3*HS] per-(b,h) bias partial sums
-    const size_t need = (size_t)B * NH * 3 * HS * sizeof(float);
-    if (!ws) ws = (float*)workspace(need);
+    // ws: per-(b,h) bias partial sums, up to ATTN_PART_ROWS rows of 3*HS each
+    if (!ws) ws = (float*)workspace(attn_backward_ws_floats(B, T, C, NH) * sizeof(float));
     if (!ws) return;
     float* part = dqkv_colsum ? ws : nullptr;
-    bool ok = false;
+    int rows = 0;
     switch (HS) {
-        case 32: ok = fa_backward_h32(dqkv, dout, qkv, out, lse, B, T, C, NH, part, s); break;
-        case 64: ok = fa_backward_h64(dqkv, dout, qkv, out, lse, B, T, C, NH, part, s); break;
-        case 80: ok = fa_backward_h80(dqkv, dout, qkv, out, lse, B, T, C, NH, part, s); break;
-        case 96: ok = fa_backward_h96(dqkv, dout, qkv, out, lse, B, T, C, NH, part, s); break;
-        case 128: ok = fa_backward_h128(dqkv, dout, qkv, out, lse, B, T, C, NH, part, s); break;
+        case 32: rows = fa_backward_h32(dqkv, dout, qkv, out, lse, B, T, C, NH, part, s); break;
+        case 64: rows = fa_backward_h64(dqkv, dout, qkv, out, lse, B, T, C, NH, part, s); break;
+        case 80: rows = fa_backward_h80(dqkv, dout, qkv, out, lse, B, T, C, NH, part, s); break;
+        case 96: rows = fa_backward_h96(dqkv, dout, qkv, out, lse, B, T, C, NH, part, s); break;
+        case 128: rows = fa_backward_h128(dqkv, dout, qkv, out, lse, B, T, C, NH, part, s); break;
     }
-    if (!ok) { set_error("fused attention backward: no kernel for T=%d head size %d", T, HS); return; }
+    if (!rows) { set_error("fused attention backward: no kernel for T=%d head size %d", T, HS); return; }
     after_launch("attention_backward_fused");
-    if (dqkv_colsum) {
-        attn_colsum_reduce_k<<<3 * NH, 1024, 0, s>>>(dqkv_colsum, part, B, NH, C, HS);
+    if (dqkv_colsum) {  // the partial rows are laid out as B*rows batch entries
+        attn_colsum_reduce_k<<<3 * NH, 1024, 0, s>>>(dqkv_colsum, part, B * rows, NH, C, HS);
         after_launch("attention_colsum_reduce");
     }
 }

@@ -109,6 +109,18 @@ __device__ __forceinline__ void load_images(bf16_t* const (&img)[NOP], const int
             if (idx < TP * CH) *reinterpret_cast<uint4*>(img[o] + t * stride[o] + c * 8) = v[o][j];
         }
 }
+// sum of the 8 bf16 products of two 16-B pieces
+__device__ __forceinline__ float dot8_bf16(uint4 a, uint4 b) {
+    const uint32_t* a32 = reinterpret_cast<const uint32_t*>(&a);
+    const uint32_t* b32 = reinterpret_cast<const uint32_t*>(&b);
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        s += __uint_as_float(a32[e] << 16) * __uint_as_float(b32[e] << 16);
+        s += __uint_as_float(a32[e] & 0xffff0000u) * __uint_as_float(b32[e] & 0xffff0000u);
+    }
+    return s;
+}
 __device__ __forceinline__ void store4(bf16_t* dst, f32x4_t v, float mul) {
     *reinterpret_cast<uint2*>(dst) =
         make_uint2(pack_bf16x2(v[0] * mul, v[1] * mul), pack_bf16x2(v[2] * mul, v[3] * mul));
@@ -565,6 +577,507 @@ __global__ __launch_bounds__(256, (bwd_occ<HS, NKT>())) void attn_bwd_pair_k(
     else bwd_q_body<HS, NKT>(lds, bh, dqkv, dout, qkv, out, lse, T, C, NH, dsum);
 }
 
+// ------------------------------------------------------------------ backward, one pass (default)
+// One workgroup per (b,h) item, NW = TP/32 waves; wave w owns keys [32w, 32w+32): its K, V
+// fragments (B operands of S and dP) and dK^T, dV^T accumulators stay in registers while the
+// workgroup sweeps the queries in 32-row slices (Q / dO slices double-buffered in LDS, the next
+// one prefetched into registers during the current one).  Per slice:
+//   A: S, dP with the key on the lane; P = exp2(S c - lse), dS = P (dP - delta) — each score's
+//      exp computed once; dV^T += dO^T P, dK^T += Q^T dS (transposed slice reads); dS^T (bf16)
+//      into LDS [key][query];                                                      barrier
+//   B: dQ^T = K^T . dS^T for the slice's 2·HS/16 output tiles, spread over the waves (K image
+//      and dS^T both read transposed); stores.                                    barrier
+// = the five products of the flash backward (train_vit.rs:559-601 with the O(T^2) softmax
+// Jacobian form) with no recomputation: per 32x32 block 5 x (HS/16 or 2·KS) MFMAs instead of
+// the paired roles' 7.  dQ needs no cross-workgroup sum: the workgroup holds every key.
+// Two forms: attn_bwdp_k (persistent: one workgroup per CU walks the items and fetches the next
+// item's K / V rows and the next slice's Q / dO / O rows under the current slice's MFMA work) and
+// attn_bwd1_k (one workgroup per item, blocking prologue) where the persistent LDS does not fit.
+constexpr int BWD_SDS = 48;
+constexpr int ATTN_PART_ROWS = 8;
+   // column-sum partial rows per (b,h) a backward kernel may write  // dS^T [key][query] row stride: (SDS/2) = 8*odd dwords (tr reads)
+
+template <int HS>
+struct BwdRegs {  // per-wave state of the one-pass backward
+    bf16x8_t kf[2][Geo<HS>::KS], vf[2][Geo<HS>::KS];  // K, V rows of the wave's 32 keys (B operands)
+    f32x4_t dv[2][Geo<HS>::DT], dk[2][Geo<HS>::DT];   // [kk][dt]: lane (i,g) -> [d = 16dt+4g+r][key = 16kk+i]
+    // per-key sums of dS over the queries: the dQ column sums (qkv-bias gradient) follow as
+    // sum_q dQ[q][d] = scale * sum_key (sum_q dS[q][key]) K[key][d], with K in registers
+    float sds[2];
+    __device__ __forceinline__ void zero() {
+#pragma unroll
+        for (int kk = 0; kk < 2; kk++) {
+#pragma unroll
+            for (int dt = 0; dt < Geo<HS>::DT; dt++) dv[kk][dt] = dk[kk][dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+            sds[kk] = 0.f;
+        }
+    }
+};
+
+// phase A of one 32-query slice for the wave's keys: Qc / Dc slice images (stride SK), lq / dl the
+// slice's lse / delta, dSk = dS^T rows of the wave's first key
+// MASK: for operands whose rows past T are copies of row T-1 (not zero), the probabilities
+// of padded queries (q >= T) and keys (key >= T) are masked to 0 (nq / nk: valid queries / keys
+// counted from the slice's and the wave's first one)
+template <int HS, bool MASK = false>
+__device__ __forceinline__ void bwd_slice_a(BwdRegs<HS>& R, const bf16_t* Qc, const bf16_t* Dc, const float* lq_s,
+                                            const float* dl_s, bf16_t* dSk, float c, int lane, int nq = 0,
+                                            int nk = 0) {
+    using G = Geo<HS>;
+    constexpr int KS = G::KS, DT = G::DT, SK = G::SK;
+    const int i = lane & 15, g = lane >> 4;
+    f32x4_t P[2][2], dS[2][2];  // [kk][u]: lane (i,g) -> [q = 16u+4g+r][key = 16kk+i]
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+        bf16x8_t qr[KS], dr[KS];
+#pragma unroll
+        for (int s = 0; s < KS; s++) {
+            qr[s] = frag_row<HS>(Qc, SK, 16 * u, s, lane);
+            dr[s] = frag_row<HS>(Dc, SK, 16 * u, s, lane);
+        }
+        float lq[4], dq[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            lq[r] = lq_s[16 * u + 4 * g + r];
+            dq[r] = dl_s[16 * u + 4 * g + r];
+        }
+#pragma unroll
+        for (int kk = 0; kk < 2; kk++) {
+            f32x4_t s_ = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < KS; s++) {
+                s_ = mfma(qr[s], R.kf[kk][s], s_);
+                dp = mfma(dr[s], R.vf[kk][s], dp);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                float pv = fexp2(s_[r] * c - lq[r]);
+                if constexpr (MASK) pv = (16 * u + 4 * g + r < nq && 16 * kk + i < nk) ? pv : 0.f;
+                P[kk][u][r] = pv;
+                dS[kk][u][r] = pv * (dp[r] - dq[r]);
+                R.sds[kk] += dS[kk][u][r];
+            }
+        }
+    }
+    bf16x8_t pb[2], db[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; kk++) {
+        pb[kk] = pack_acc(P[kk][0], P[kk][1]);
+        db[kk] = pack_acc(dS[kk][0], dS[kk][1]);
+    }
+#pragma unroll
+    for (int dt = 0; dt < DT; dt++) {
+        const bf16x8_t td = frag_tr(Dc, SK, 0, 16 * dt, lane);
+        const bf16x8_t tq = frag_tr(Qc, SK, 0, 16 * dt, lane);
+#pragma unroll
+        for (int kk = 0; kk < 2; kk++) {
+            R.dv[kk][dt] = mfma(td, pb[kk], R.dv[kk][dt]);
+            R.dk[kk][dt] = mfma(tq, db[kk], R.dk[kk][dt]);
+        }
+    }
+    // dS^T -> LDS [key][query] (bf16, the MFMA operand's values): 4 consecutive queries per lane
+    // and tile.  Without MASK, padded keys carry P != 0 (their K, V rows are zero): their dS is
+    // finite and multiplies the zero K rows in dQ.
+#pragma unroll
+    for (int kk = 0; kk < 2; kk++)
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const bf16x4_t h4 = u ? __builtin_shufflevector(db[kk], db[kk], 4, 5, 6, 7)
+                                  : __builtin_shufflevector(db[kk], db[kk], 0, 1, 2, 3);
+            *reinterpret_cast<bf16x4_t*>(dSk + (16 * kk + i) * BWD_SDS + 16 * u + 4 * g) = h4;
+        }
+}
+
+// phase B: dQ^T tiles (dt, u) of the slice at q0, spread over the NW waves; dq = dqkv Q rows of the item
+template <int HS, int NSL, int NW>
+__device__ __forceinline__ void bwd_slice_b(const bf16_t* Ks, const bf16_t* dSs, bf16_t* dq, long long C3, int q0,
+                                            int T, float scale, int w, int lane) {
+    constexpr int DT = Geo<HS>::DT, SV = Geo<HS>::SV;
+    const int i = lane & 15, g = lane >> 4;
+    for (int j = w; j < 2 * DT; j += NW) {
+        const int dt = j >> 1, u = j & 1;
+        // two accumulation chains (even / odd key blocks) halve the dependent-MFMA latency
+        f32x4_t acc = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < NSL; ks++) {
+            const bf16x8_t a = frag_tr(Ks, SV, 32 * ks, 16 * dt, lane), b = frag_tr(dSs, BWD_SDS, 32 * ks, 16 * u, lane);
+            if (ks & 1) acc1 = mfma(a, b, acc1);
+            else acc = mfma(a, b, acc);
+        }
+        acc += acc1;
+        // lane (i,g): d = 16dt + 4g + r, q = q0 + 16u + i (padded queries: dS = 0)
+        const int q = q0 + 16 * u + i;
+        if (q < T) store4(dq + (long long)q * C3 + 16 * dt + 4 * g, acc, scale);
+    }
+}
+
+// end of an item: dK, dV of the wave's keys; per-wave column sums of dQ | dK | dV into part[3 HS]
+// (the caller sums the waves' rows after a barrier)
+template <int HS>
+__device__ __forceinline__ void bwd_item_end(BwdRegs<HS>& R, bf16_t* dq, long long C, int key0, int T, float scale,
+                                             float* part, int lane) {
+    constexpr int KS = Geo<HS>::KS, DT = Geo<HS>::DT;
+    const int i = lane & 15, g = lane >> 4;
+    const long long C3 = 3 * C;
+#pragma unroll
+    for (int kk = 0; kk < 2; kk++) {
+        const int key = key0 + 16 * kk + i;
+        if (key >= T) continue;
+        bf16_t* dst = dq + (long long)key * C3 + 4 * g;
+#pragma unroll
+        for (int dt = 0; dt < DT; dt++) {
+            store4(dst + C + 16 * dt, R.dk[kk][dt], scale);
+            store4(dst + 2 * C + 16 * dt, R.dv[kk][dt], 1.0f);
+        }
+    }
+    if (!part) return;
+#pragma unroll
+    for (int dt = 0; dt < DT; dt++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            float tk = 0.f, tv = 0.f;
+#pragma unroll
+            for (int kk = 0; kk < 2; kk++)
+                if (key0 + 16 * kk + i < T) {
+                    tk += R.dk[kk][dt][r] * scale;
+                    tv += R.dv[kk][dt][r];
+                }
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) {
+                tk += __shfl_xor(tk, o, 64);
+                tv += __shfl_xor(tv, o, 64);
+            }
+            if (i == 0) {
+                part[HS + 16 * dt + 4 * g + r] = tk;
+                part[2 * HS + 16 * dt + 4 * g + r] = tv;
+            }
+        }
+    // dQ: lane (i,g) sums over the 4 g-groups' queries, then over its key column i
+    float sd[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; kk++) {
+        sd[kk] = R.sds[kk] + __shfl_xor(R.sds[kk], 16, 64);
+        sd[kk] += __shfl_xor(sd[kk], 32, 64);
+    }
+#pragma unroll
+    for (int s = 0; s < KS; s++)
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int d = 32 * s + (j < 4 ? 4 * g + j : 16 + 4 * g + j - 4);
+            if (d >= HS) continue;  // zero half of the last k-step (HS % 32 == 16)
+            float t = sd[0] * (float)R.kf[0][s][j] + sd[1] * (float)R.kf[1][s][j];
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) t += __shfl_xor(t, o, 64);
+            if (i == 0) part[d] = t * scale;
+        }
+}
+
+template <int HS, int NKT>
+struct Bwd1 {
+    static constexpr int TP = NKT * 16, NW = NKT / 2, NT = NW * 64, NSL = TP / 32;
+    static constexpr int SK = Geo<HS>::SK;   // Q / dO slices: row and transposed reads
+    static constexpr int SV = Geo<HS>::SV;   // K image: transposed reads only
+    static constexpr int K_OFF = 0;
+    static constexpr int Q_OFF = K_OFF + TP * SV * 2;
+    static constexpr int D_OFF = Q_OFF + 2 * 32 * SK * 2;
+    static constexpr int S_OFF = D_OFF + 2 * 32 * SK * 2;
+    static constexpr int L_OFF = S_OFF + TP * BWD_SDS * 2;
+    static constexpr int BYTES = L_OFF + 2 * TP * 4;
+    static constexpr int PER = (32 * Geo<HS>::CH + NT - 1) / NT;  // 16-B pieces per thread per slice operand
+};
+// LDS, and registers: up to 8 waves (2 per SIMD, 256 VGPRs) for HS <= 80; 4 waves for HS 96/128
+// (more waves -> 3 per SIMD -> 168 VGPRs, which the 32-key accumulators do not fit)
+template <int HS, int NKT>
+constexpr bool bwd1_fits() {
+    return Bwd1<HS, NKT>::BYTES <= 160 * 1024 && (NKT / 2 <= 4 || (NKT / 2 <= 8 && HS <= 80));
+}
+
+template <int HS, int NKT>
+__global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restrict__ dqkv,
+                                                               const bf16_t* __restrict__ dout,
+                                                               const bf16_t* __restrict__ qkv,
+                                                               const bf16_t* __restrict__ out,
+                                                               const float* __restrict__ lse, int T,
+                                                               int C, int NH, float* __restrict__ dsum) {
+    using G = Geo<HS>;
+    using Z = Bwd1<HS, NKT>;
+    constexpr int TP = Z::TP, NW = Z::NW, NT = Z::NT, NSL = Z::NSL, SK = Z::SK, SV = Z::SV;
+    constexpr int KS = G::KS, CH = G::CH, PER = Z::PER;
+    __shared__ __attribute__((aligned(16))) char lds[Z::BYTES];
+    bf16_t* Ks = reinterpret_cast<bf16_t*>(lds + Z::K_OFF);
+    bf16_t* Qs = reinterpret_cast<bf16_t*>(lds + Z::Q_OFF);
+    bf16_t* Ds = reinterpret_cast<bf16_t*>(lds + Z::D_OFF);
+    bf16_t* dSs = reinterpret_cast<bf16_t*>(lds + Z::S_OFF);
+    float* lse_s = reinterpret_cast<float*>(lds + Z::L_OFF);
+    float* del_s = lse_s + TP;
+    const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
+    const long long C3 = 3LL * C;
+    const bf16_t* base = qkv + (long long)b * T * C3 + h * HS;
+    const bf16_t* dbase = dout + (long long)b * T * C + h * HS;
+    const bf16_t* obase = out + (long long)b * T * C + h * HS;
+    bf16_t* dq = dqkv + (long long)b * T * C3 + h * HS;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, i = lane & 15;
+    const int key0 = w * 32;
+    BwdRegs<HS> R;
+    // the wave's K, V fragments (rows >= T -> 0), requested first so their latency hides
+#pragma unroll
+    for (int kk = 0; kk < 2; kk++)
+#pragma unroll
+        for (int s = 0; s < KS; s++) {
+            R.kf[kk][s] = frag_glb<HS>(base + C, C3, key0 + 16 * kk + i, T, s, lane);
+            R.vf[kk][s] = frag_glb<HS>(base + 2 * C, C3, key0 + 16 * kk + i, T, s, lane);
+        }
+    // one slice (32 rows) of Q and dO: PER 16-B pieces per thread and operand
+    uint4 pq[PER], pd[PER];
+    auto fetch_slice = [&](int q0) {
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            const int idx = j * NT + tid, t = idx / CH, c = idx - t * CH;
+            pq[j] = pd[j] = make_uint4(0, 0, 0, 0);
+            if (idx < 32 * CH && q0 + t < T) {
+                pq[j] = *reinterpret_cast<const uint4*>(base + (long long)(q0 + t) * C3 + c * 8);
+                pd[j] = *reinterpret_cast<const uint4*>(dbase + (long long)(q0 + t) * C + c * 8);
+            }
+        }
+    };
+    auto put_slice = [&](int buf) {
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            const int idx = j * NT + tid, t = idx / CH, c = idx - t * CH;
+            if (idx < 32 * CH) {
+                *reinterpret_cast<uint4*>(Qs + buf * 32 * SK + t * SK + c * 8) = pq[j];
+                *reinterpret_cast<uint4*>(Ds + buf * 32 * SK + t * SK + c * 8) = pd[j];
+            }
+        }
+    };
+    fetch_slice(0);
+    {
+        bf16_t* const img[1] = {Ks};
+        const int st[1] = {SV};
+        const bf16_t* const src[1] = {base + C};
+        const long long ld[1] = {C3};
+        load_images<HS, TP, NT, 1>(img, st, src, ld, T);
+    }
+    put_slice(0);
+    // lse and delta = rowsum(dO * O) for every query (padded queries: lse = +inf -> P = 0)
+    for (int t = tid; t < TP; t += NT) {
+        float dl = 0.f, ls = INFINITY;
+        if (t < T) {
+            ls = lse[(long long)bh * T + t];
+#pragma unroll
+            for (int cc = 0; cc < CH; cc++)
+                dl += dot8_bf16(*reinterpret_cast<const uint4*>(obase + (long long)t * C + cc * 8),
+                                *reinterpret_cast<const uint4*>(dbase + (long long)t * C + cc * 8));
+        }
+        lse_s[t] = ls;
+        del_s[t] = dl;
+    }
+    __syncthreads();
+    const float scale = 1.0f / sqrtf((float)HS);
+    const float c = LOG2E * scale;
+    R.zero();
+#pragma unroll 1
+    for (int sl = 0; sl < NSL; sl++) {
+        const int q0 = sl * 32, cur = sl & 1;
+        if (sl + 1 < NSL) fetch_slice(q0 + 32);  // lands in registers during phase A
+        bwd_slice_a<HS>(R, Qs + cur * 32 * SK, Ds + cur * 32 * SK, lse_s + q0, del_s + q0, dSs + key0 * BWD_SDS, c, lane);
+        __syncthreads();
+        if (sl + 1 < NSL) put_slice(cur ^ 1);  // its buffer was last read in the previous slice
+        bwd_slice_b<HS, NSL, NW>(Ks, dSs, dq, C3, q0, T, scale, w, lane);
+        __syncthreads();
+    }
+    float* part = reinterpret_cast<float*>(lds + Z::Q_OFF);  // slices / dS free now: [NW][3 HS]
+    bwd_item_end<HS>(R, dq, C, key0, T, scale, dsum ? part + w * 3 * HS : nullptr, lane);
+    if (dsum) {  // per-(b,h) column sums of dQ | dK | dV -> dsum[bh][3*HS]
+        __syncthreads();
+        for (int t = tid; t < 3 * HS; t += NT) {
+            float a = 0.f;
+#pragma unroll
+            for (int ww = 0; ww < NW; ww++) a += part[ww * 3 * HS + t];
+            dsum[(long long)bh * 3 * HS + t] = a;
+        }
+    }
+}
+
+template <int HS, int NKT>
+struct Bwdp {
+    using G = Geo<HS>;
+    static constexpr int TP = NKT * 16, NW = NKT / 2, NT = NW * 64, NSL = TP / 32, CH = G::CH;
+    static constexpr int SK = G::SK, SV = G::SV;
+    static constexpr int K_OFF = 0;                          // K images [2][TP][SV]: current / next item
+    static constexpr int V_OFF = K_OFF + 2 * TP * SV * 2;    // next item's V rows [TP][SK]
+    static constexpr int Q_OFF = V_OFF + TP * SK * 2;        // Q slices [2][32][SK]
+    static constexpr int D_OFF = Q_OFF + 2 * 32 * SK * 2;    // dO slices [2][32][SK]
+    static constexpr int S_OFF = D_OFF + 2 * 32 * SK * 2;    // dS^T [TP][BWD_SDS]
+    static constexpr int L_OFF = S_OFF + TP * BWD_SDS * 2;   // lse [2][TP] (item parity)
+    static constexpr int E_OFF = L_OFF + 2 * TP * 4;         // delta [2][32] (slice parity)
+    static constexpr int P_OFF = E_OFF + 2 * 32 * 4;         // column-sum partials [NW][3 HS]
+    static constexpr int BYTES = P_OFF + NW * 3 * HS * 4;
+    static constexpr int PER = (32 * CH + NT - 1) / NT;      // 16-B pieces per thread, slice operand
+    static constexpr int PERS = (2 * 32 * CH + NT - 1) / NT; // next item's K + V rows, per slice
+};
+// the delta reduction runs over CH consecutive lanes (a power of two dividing 64)
+template <int HS, int NKT>
+constexpr bool bwdp_fits() {
+    return bwd1_fits<HS, NKT>() && Bwdp<HS, NKT>::BYTES <= 160 * 1024 && (64 % Geo<HS>::CH) == 0 && HS <= 64;
+}
+
+template <int HS, int NKT>
+__global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwdp_k(bf16_t* __restrict__ dqkv,
+                                                               const bf16_t* __restrict__ dout,
+                                                               const bf16_t* __restrict__ qkv,
+                                                               const bf16_t* __restrict__ out,
+                                                               const float* __restrict__ lse, int T,
+                                                               int C, int NH, int BH, float* __restrict__ dsum) {
+    using G = Geo<HS>;
+    using Z = Bwdp<HS, NKT>;
+    constexpr int TP = Z::TP, NW = Z::NW, NT = Z::NT, NSL = Z::NSL, SK = Z::SK, SV = Z::SV;
+    constexpr int KS = G::KS, CH = G::CH, PER = Z::PER, PERS = Z::PERS;
+    __shared__ __attribute__((aligned(16))) char lds[Z::BYTES];
+    bf16_t* Kimg = reinterpret_cast<bf16_t*>(lds + Z::K_OFF);
+    bf16_t* Vst = reinterpret_cast<bf16_t*>(lds + Z::V_OFF);
+    bf16_t* Qs = reinterpret_cast<bf16_t*>(lds + Z::Q_OFF);
+    bf16_t* Ds = reinterpret_cast<bf16_t*>(lds + Z::D_OFF);
+    bf16_t* dSs = reinterpret_cast<bf16_t*>(lds + Z::S_OFF);
+    float* lse_s = reinterpret_cast<float*>(lds + Z::L_OFF);
+    float* del_s = reinterpret_cast<float*>(lds + Z::E_OFF);
+    float* part = reinterpret_cast<float*>(lds + Z::P_OFF);
+    const long long C3 = 3LL * C;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int key0 = w * 32;
+    const float scale = 1.0f / sqrtf((float)HS);
+    const float c = LOG2E * scale;
+    auto qkv_of = [&](int bh) { return qkv + (long long)(bh / NH) * T * C3 + (bh % NH) * HS; };
+    auto row_of = [&](const bf16_t* p, int bh) { return p + (long long)(bh / NH) * T * C + (bh % NH) * HS; };
+    // slice rows (Q, dO, O) of item bh at q0 -> registers; into LDS with delta = rowsum(dO * O)
+    uint4 pq[PER], pd[PER], po[PER];
+    auto fetch_slice = [&](int bh, int q0) {
+        const bf16_t* qb = qkv_of(bh);
+        const bf16_t* db = row_of(dout, bh);
+        const bf16_t* ob = row_of(out, bh);
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            const int idx = j * NT + tid, t = idx / CH, cc = idx - t * CH;
+            pq[j] = pd[j] = po[j] = make_uint4(0, 0, 0, 0);
+            if (idx < 32 * CH && q0 + t < T) {
+                pq[j] = *reinterpret_cast<const uint4*>(qb + (long long)(q0 + t) * C3 + cc * 8);
+                pd[j] = *reinterpret_cast<const uint4*>(db + (long long)(q0 + t) * C + cc * 8);
+                po[j] = *reinterpret_cast<const uint4*>(ob + (long long)(q0 + t) * C + cc * 8);
+            }
+        }
+    };
+    auto put_slice = [&](int buf) {
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            const int idx = j * NT + tid, t = idx / CH, cc = idx - t * CH;
+            float dl = dot8_bf16(po[j], pd[j]);  // the CH lanes of row t are consecutive
+#pragma unroll
+            for (int o = 1; o < CH; o <<= 1) dl += __shfl_xor(dl, o, 64);
+            if (idx < 32 * CH) {
+                *reinterpret_cast<uint4*>(Qs + buf * 32 * SK + t * SK + cc * 8) = pq[j];
+                *reinterpret_cast<uint4*>(Ds + buf * 32 * SK + t * SK + cc * 8) = pd[j];
+                if (cc == 0) del_s[buf * 32 + t] = dl;
+            }
+        }
+    };
+    // next item's K and V rows [32 rb, 32 rb + 32) -> registers; into its K image / the V rows
+    uint4 ps[PERS];
+    float lse_n = INFINITY;
+    auto fetch_side = [&](int bh, int rb) {
+        const bf16_t* kb = qkv_of(bh) + C;
+#pragma unroll
+        for (int j = 0; j < PERS; j++) {
+            const int idx = j * NT + tid, op = idx >= 32 * CH, rem = idx - op * 32 * CH, t = rem / CH,
+                      cc = rem - t * CH, row = 32 * rb + t;
+            ps[j] = make_uint4(0, 0, 0, 0);
+            if (idx < 64 * CH && row < T) ps[j] = *reinterpret_cast<const uint4*>(kb + op * C + (long long)row * C3 + cc * 8);
+        }
+    };
+    auto put_side = [&](int kbuf, int rb) {
+#pragma unroll
+        for (int j = 0; j < PERS; j++) {
+            const int idx = j * NT + tid, op = idx >= 32 * CH, rem = idx - op * 32 * CH, t = rem / CH,
+                      cc = rem - t * CH, row = 32 * rb + t;
+            if (idx < 64 * CH) {
+                bf16_t* dst = op ? Vst + row * SK : Kimg + kbuf * TP * SV + row * SV;
+                *reinterpret_cast<uint4*>(dst + cc * 8) = ps[j];
+            }
+        }
+    };
+    auto load_kv = [&](BwdRegs<HS>& R, int kbuf) {  // the wave's fragments from the staged rows
+#pragma unroll
+        for (int kk = 0; kk < 2; kk++)
+#pragma unroll
+            for (int s = 0; s < KS; s++) {
+                R.kf[kk][s] = frag_row<HS>(Kimg + kbuf * TP * SV, SV, key0 + 16 * kk, s, lane);
+                R.vf[kk][s] = frag_row<HS>(Vst, SK, key0 + 16 * kk, s, lane);
+            }
+    };
+    int bh = blockIdx.x;
+    if (bh >= BH) return;
+    // prologue (first item): K image, V rows, lse, slice 0 — one blocking round trip
+    fetch_slice(bh, 0);
+    {
+        bf16_t* const img[2] = {Kimg, Vst};
+        const int st[2] = {SV, SK};
+        const bf16_t* const src[2] = {qkv_of(bh) + C, qkv_of(bh) + 2 * C};
+        const long long ld[2] = {C3, C3};
+        load_images<HS, TP, NT, 2>(img, st, src, ld, T);
+    }
+    for (int t = tid; t < TP; t += NT) lse_s[t] = t < T ? lse[(long long)bh * T + t] : INFINITY;
+    put_slice(0);
+    __syncthreads();
+    BwdRegs<HS> R;
+    load_kv(R, 0);
+    int kb = 0, it = 0;
+#pragma unroll 1
+    for (int n = 0; bh < BH; n++, bh += gridDim.x) {
+        const int bhn = bh + gridDim.x;
+        const bool has_next = bhn < BH;
+        bf16_t* dq = dqkv + (long long)(bh / NH) * T * C3 + (bh % NH) * HS;
+        const float* lse_cur = lse_s + (n & 1) * TP;
+        R.zero();
+#pragma unroll 1
+        for (int sl = 0; sl < NSL; sl++, it++) {
+            const int cur = it & 1, q0 = sl * 32;
+            const bool next_slice = sl + 1 < NSL || has_next;
+            // one step ahead: the next slice (this item's or the next item's first), the next
+            // item's K / V row block sl and, with its first block, its lse
+            if (next_slice) fetch_slice(sl + 1 < NSL ? bh : bhn, sl + 1 < NSL ? q0 + 32 : 0);
+            if (has_next) {
+                fetch_side(bhn, sl);
+                if (sl == 0 && tid < TP) lse_n = tid < T ? lse[(long long)bhn * T + tid] : INFINITY;
+            }
+            bwd_slice_a<HS>(R, Qs + cur * 32 * SK, Ds + cur * 32 * SK, lse_cur + q0, del_s + cur * 32,
+                            dSs + key0 * BWD_SDS, c, lane);
+            __syncthreads();
+            // buffers written here were last read before the barrier above (slice buffer cur^1 by
+            // the previous slice, the idle K image by the previous item, the V rows by load_kv)
+            if (next_slice) put_slice(cur ^ 1);
+            if (has_next) {
+                put_side(kb ^ 1, sl);
+                if (sl == 0 && tid < TP) lse_s[((n + 1) & 1) * TP + tid] = lse_n;
+            }
+            bwd_slice_b<HS, NSL, NW>(Kimg + kb * TP * SV, dSs, dq, C3, q0, T, scale, w, lane);
+            __syncthreads();
+        }
+        bwd_item_end<HS>(R, dq, C, key0, T, scale, dsum ? part + w * 3 * HS : nullptr, lane);
+        if (dsum) {
+            __syncthreads();
+            for (int t = tid; t < 3 * HS; t += NT) {
+                float a = 0.f;
+#pragma unroll
+                for (int ww = 0; ww < NW; ww++) a += part[ww * 3 * HS + t];
+                dsum[(long long)bh * 3 * HS + t] = a;
+            }
+        }
+        if (has_next) {
+            kb ^= 1;
+            load_kv(R, kb);  // every block was put before the item's last barrier
+        }
+    }
+}
+
 // largest padded length (multiple of 32) whose forward AND backward images fit the 160 KiB LDS
 template <int HS>
 constexpr int max_tp() {
@@ -580,11 +1093,28 @@ template <int HS, int NKT>
 void launch_fwd(bf16_t* out, float* lse, const bf16_t* qkv, int B, int T, int C, int NH, hipStream_t s) {
     attn_fwd_k<HS, NKT><<<B * NH, 256, 0, s>>>(out, lse, qkv, T, C, NH);
 }
+int attn_bwd_variant();  // attention.hip: VIT_ATTN_BWD = pair | one | (default) persistent (A/B)
+int attn_cu_count();     // attention.hip: compute units of the current device
+// returns the column-sum partial rows written per (b,h) (attn_colsum_reduce_k sums B x rows)
 template <int HS, int NKT>
-void launch_bwd(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t* out,
-                const float* lse, int B, int T, int C, int NH, float* part, hipStream_t s) {
-    attn_bwd_pair_k<HS, NKT><<<2 * cdiv(B * NH, 8) * 8, 256, 0, s>>>(dqkv, dout, qkv, out, lse, T, C, NH,
-                                                                     B * NH, part);
+int launch_bwd(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t* out, const float* lse, int B,
+               int T, int C, int NH, float* part, hipStream_t s) {
+    const int v = attn_bwd_variant(), BH = B * NH;
+    if constexpr (bwdp_fits<HS, NKT>()) {
+        if (v == 0) {
+            attn_bwdp_k<HS, NKT><<<std::min(BH, attn_cu_count()), NKT / 2 * 64, 0, s>>>(dqkv, dout, qkv, out, lse, T,
+                                                                                      C, NH, BH, part);
+            return 1;
+        }
+    }
+    if constexpr (bwd1_fits<HS, NKT>()) {
+        if (v != 2) {
+            attn_bwd1_k<HS, NKT><<<BH, NKT / 2 * 64, 0, s>>>(dqkv, dout, qkv, out, lse, T, C, NH, part);
+            return 1;
+        }
+    }
+    attn_bwd_pair_k<HS, NKT><<<2 * cdiv(BH, 8) * 8, 256, 0, s>>>(dqkv, dout, qkv, out, lse, T, C, NH, BH, part);
+    return 1;
 }
 template <int HS, int NKT = 2>
 bool dispatch_fwd(int nkt, bf16_t* out, float* lse, const bf16_t* qkv, int B, int T, int C, int NH,
@@ -597,12 +1127,12 @@ bool dispatch_fwd(int nkt, bf16_t* out, float* lse, const bf16_t* qkv, int B, in
     }
 }
 template <int HS, int NKT = 2>
-bool dispatch_bwd(int nkt, bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t* out,
-                  const float* lse, int B, int T, int C, int NH, float* part, hipStream_t s) {
+int dispatch_bwd(int nkt, bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t* out,
+                 const float* lse, int B, int T, int C, int NH, float* part, hipStream_t s) {
     if constexpr (NKT * 16 > max_tp<HS>()) {
-        return false;
+        return 0;
     } else {
-        if (nkt == NKT) { launch_bwd<HS, NKT>(dqkv, dout, qkv, out, lse, B, T, C, NH, part, s); return true; }
+        if (nkt == NKT) return launch_bwd<HS, NKT>(dqkv, dout, qkv, out, lse, B, T, C, NH, part, s);
         return dispatch_bwd<HS, NKT + 2>(nkt, dqkv, dout, qkv, out, lse, B, T, C, NH, part, s);
     }
 }
@@ -613,8 +1143,8 @@ bool dispatch_bwd(int nkt, bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, 
 #define VIT_FA_DECLARE(HS)                                                                         \
     bool fa_forward_h##HS(bf16_t* out, float* lse, const bf16_t* qkv, int B, int T, int C, int NH, \
                           hipStream_t s);                                                          \
-    bool fa_backward_h##HS(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t* out, \
-                           const float* lse, int B, int T, int C, int NH, float* part, hipStream_t s); \
+    int fa_backward_h##HS(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t* out, \
+                          const float* lse, int B, int T, int C, int NH, float* part, hipStream_t s); \
     int fa_max_t_h##HS();
 VIT_FA_DECLARE(32)
 VIT_FA_DECLARE(64)
@@ -627,8 +1157,8 @@ VIT_FA_DECLARE(128)
                           hipStream_t s) {                                                          \
         return fa::dispatch_fwd<HS>(cdiv(T, 32) * 2, out, lse, qkv, B, T, C, NH, s);                \
     }                                                                                               \
-    bool fa_backward_h##HS(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t* out,  \
-                           const float* lse, int B, int T, int C, int NH, float* part, hipStream_t s) { \
+    int fa_backward_h##HS(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t* out,   \
+                          const float* lse, int B, int T, int C, int NH, float* part, hipStream_t s) {  \
         return fa::dispatch_bwd<HS>(cdiv(T, 32) * 2, dqkv, dout, qkv, out, lse, B, T, C, NH, part, s); \
     }                                                                                               \
     int fa_max_t_h##HS() { return fa::max_tp<HS>(); }

@@ -53,6 +53,8 @@ bool attn_generic_supported(int T, int C, int NH);  // VALU bf16 kernels (other 
 void attn_forward_fused(bf16_t* out, float* lse, const bf16_t* qkv, int B, int T, int C, int NH,
                         hipStream_t s);
 // dqkv_colsum (nullable, [3C]) += column sums of dqkv (the qkv bias gradient, fused)
+// floats of the workspace attn_backward_fused needs (generic delta rows / fused column-sum partials)
+size_t attn_backward_ws_floats(int B, int T, int C, int NH);
 void attn_backward_fused(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t* out,
                          const float* lse, int B, int T, int C, int NH, hipStream_t s,
                          float* dqkv_colsum = nullptr, float* ws = nullptr);

@@ -543,7 +543,7 @@ struct Trainer {
             // slabs: <= 32 splits of the largest weight gradient (4C x C)
             gemm_ws_bytes = (size_t)32 * 4 * C * (size_t)std::max(C, KP) * sizeof(float);
             gemm_ws = alloc<float>((long long)(gemm_ws_bytes / sizeof(float)));
-            attn_part = alloc<float>((long long)B * NH * (3 * (C / NH) + T));  // bias partials | delta
+            attn_part = alloc<float>((long long)attn_backward_ws_floats(B, T, C, NH));  // bias partials | delta
             if (fp8()) {
                 const long long ns[NWK] = {3LL * C, C, 4LL * C, C}, ks[NWK] = {C, C, C, 4LL * C};
                 for (int k = 0; k < NWK; k++) {
@@ -895,7 +895,7 @@ struct Trainer {
                 tbeg(TC_ATTN_BWD, 8.0 * Bm * (double)T * T * C, ms[mb]);
                 attn_backward_fused(dqkv + r0 * 3 * C, datty + r0 * C, a.qkv + r0 * 3 * C, a.atty + r0 * C,
                                     a.lse + (long long)mb * Bm * NH * T, Bm, T, C, NH, ms[mb], G(P_QKVB, l),
-                                    attn_part + (long long)mb * Bm * NH * (3 * (C / NH) + T));
+                                    attn_part + (long long)attn_backward_ws_floats(mb * Bm, T, C, NH));
                 tend();
             }
             // qkv
