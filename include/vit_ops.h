@@ -121,6 +121,12 @@ void attention_forward_fused_bf16(uint16_t* out, float* lse, const uint16_t* inp
 void attention_backward_fused_bf16(uint16_t* dinp, const uint16_t* dout, const uint16_t* inp,
                                    const uint16_t* out, const float* lse, int B, int T, int C,
                                    int NH);
+/* As attention_backward_fused_bf16, plus the fused qkv-bias gradient the trainer uses:
+ * dqkv_bias[j] += sum over the B*T rows of dinp[row][j] (fp32 sums of the unrounded values,
+ * deterministic order), j < 3C.  dqkv_bias may be NULL. */
+void attention_backward_fused_bf16_ex(uint16_t* dinp, const uint16_t* dout, const uint16_t* inp,
+                                      const uint16_t* out, const float* lse, int B, int T, int C, int NH,
+                                      float* dqkv_bias);
 void layernorm_forward_bf16(uint16_t* out, float* mean, float* rstd, const float* inp,
                             const float* weight, const float* bias, int B, int T, int C);
 /* train_vit.rs:603 with the LN-output gradient in bf16 (as the trainer's dgrad GEMMs write it):

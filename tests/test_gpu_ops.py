@@ -334,6 +334,13 @@ def test_attention_backward_variants(gpu, oracle64, monkeypatch, B, T, NH):
         assert max(errs) < 3e-2, (variant, errs)
     for variant in ["one", "pair"]:
         assert rel_err(res[variant], res["persistent"]) < 2e-2, variant
+    # the fused qkv-bias gradient (trainer form): column sums of dqkv, accumulated (+=)
+    for variant in ["persistent", "one", "pair"]:
+        monkeypatch.setenv("VIT_ATTN_BWD", variant)
+        db = D(v, np.ones(3 * C, np.float32))
+        v.call("attention_backward_fused_bf16_ex", Z(v, B * T * 3 * C, np.uint16), D(v, dyb, np.uint16), gq, gout,
+               glse, B, T, C, NH, db)
+        assert rel_err(db.numpy() - 1.0, dinp.reshape(B * T, 3 * C).sum(0)) < 3e-2, variant
 
 
 def test_error_channel(gpu):

@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--NH", type=int, default=12)
     ap.add_argument("--hs", type=int, default=64)
     ap.add_argument("--generic", action="store_true", help="force the generic VALU kernels")
+    ap.add_argument("--colsum", action="store_true", help="backward with the fused qkv-bias gradient (trainer form)")
     args = ap.parse_args()
     if args.generic:
         os.environ["VIT_ATTN_GENERIC"] = "1"
@@ -33,11 +34,15 @@ def main():
     out = vit.DeviceArray.zeros(B * T * C, np.uint16)
     lse = vit.DeviceArray.zeros(B * NH * T, np.float32)
     dqkv = vit.DeviceArray.zeros(B * T * 3 * C, np.uint16)
+    dbias = vit.DeviceArray.zeros(3 * C, np.float32)
+    bwd = ((lambda: L.attention_backward_fused_bf16_ex(dqkv.ptr, dout.ptr, qkv.ptr, out.ptr, lse.ptr, B, T, C, NH, dbias.ptr))
+           if args.colsum else
+           (lambda: L.attention_backward_fused_bf16(dqkv.ptr, dout.ptr, qkv.ptr, out.ptr, lse.ptr, B, T, C, NH)))
     e0, e1 = L.vit_event_create(), L.vit_event_create()
     fl_f = 4.0 * B * T * T * C
     for name, fn, fl in (
             ("fwd", lambda: L.attention_forward_fused_bf16(out.ptr, lse.ptr, qkv.ptr, B, T, C, NH), fl_f),
-            ("bwd", lambda: L.attention_backward_fused_bf16(dqkv.ptr, dout.ptr, qkv.ptr, out.ptr, lse.ptr, B, T, C, NH), 2 * fl_f)):
+            ("bwd" + ("+colsum" if args.colsum else ""), bwd, 2 * fl_f)):
         for _ in range(2):
             fn()
         L.vit_sync()

@@ -94,6 +94,7 @@ _SIGS = {
     "attention_forward_fused_bf16": (None, [P, P, P, I, I, I, I]),
     "vit_attention_kernel_kind": (I, [I, I, I]),
     "attention_backward_fused_bf16": (None, [P, P, P, P, P, I, I, I, I]),
+    "attention_backward_fused_bf16_ex": (None, [P, P, P, P, P, I, I, I, I, P]),
     "layernorm_forward_bf16": (None, [P, P, P, P, P, P, I, I, I]),
     "layernorm_backward_bf16": (None, [P, P, P, P, P, P, P, P, I, I, I]),
     "gelu_forward_bf16": (None, [P, P, I]),

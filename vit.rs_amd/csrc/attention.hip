@@ -508,31 +508,40 @@ bool attn_fused_supported(int T, int C, int NH) {
     return NH > 0 && C % NH == 0 && T >= 1 && T <= fa_max_t(C / NH) && C % 8 == 0 && !getenv("VIT_ATTN_GENERIC");
 }
 
-// out[s*C + h*HS + d] += sum_b part[(b*NH + h)][s*HS + d]; one 1024-thread block per (s, h):
-// nb = 1024 / HS batch lanes x HS columns, fixed-order tree over the lanes (deterministic order
-// within a launch; the micro-batches' launches add into one bias concurrently).
-__global__ __launch_bounds__(1024) void attn_colsum_reduce_k(float* __restrict__ out,
-                                                             const float* __restrict__ part, int B,
-                                                             int NH, int C, int HS) {
-    __shared__ float red[1024];
-    const int sh = blockIdx.x;  // 0 .. 3*NH-1
-    const int sct = sh / NH, h = sh - sct * NH;
-    const int nb = 1024 / HS;
-    const int d = threadIdx.x % HS, lane_b = threadIdx.x / HS;
+// Column sums of the fused backward's per-(row, h) partials, deterministic two-stage:
+//   part_k : block (s*NH + h, chunk) sums its chunk of the R = B x rows partial rows
+//            part[(r*NH + h)][s*HS + d] -> scratch[chunk][s*C + h*HS + d]
+//   final_k: out[j] += sum over chunks of scratch[chunk][j] (fixed order; one atomicAdd per j, as the
+//            micro-batches' launches add into one bias concurrently)
+__global__ __launch_bounds__(256) void attn_colsum_part_k(float* __restrict__ scratch, const float* __restrict__ part,
+                                                          int R, int NH, int C, int HS) {
+    __shared__ float red[256];
+    const int sh = blockIdx.x, sct = sh / NH, h = sh - sct * NH, ch = blockIdx.y, nch = gridDim.y;
+    const int nb = 256 / HS, d = threadIdx.x % HS, lb = threadIdx.x / HS;
+    const int r0 = (int)((long long)R * ch / nch), r1 = (int)((long long)R * (ch + 1) / nch);
     float t = 0.f;
-    if (lane_b < nb)
-        for (int b = lane_b; b < B; b += nb) t += part[((long long)b * NH + h) * 3 * HS + sct * HS + d];
+    if (lb < nb)
+        for (int r = r0 + lb; r < r1; r += nb) t += part[((long long)r * NH + h) * 3 * HS + sct * HS + d];
     red[threadIdx.x] = t;
     __syncthreads();
-    if (lane_b == 0) {
+    if (lb == 0) {
         float a = 0.f;
         for (int j = 0; j < nb; j++) a += red[j * HS + d];
-        atomicAdd(out + sct * C + h * HS + d, a);
+        scratch[(long long)ch * 3 * C + sct * C + h * HS + d] = a;
     }
+}
+__global__ __launch_bounds__(256) void attn_colsum_final_k(float* __restrict__ out, const float* __restrict__ scratch,
+                                                           int nch, int C3) {
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= C3) return;
+    float a = 0.f;
+    for (int ch = 0; ch < nch; ch++) a += scratch[(long long)ch * C3 + j];
+    atomicAdd(out + j, a);
 }
 
 size_t attn_backward_ws_floats(int B, int T, int C, int NH) {
-    const size_t per_bh = std::max((size_t)T, (size_t)3 * (C / NH) * fa::ATTN_PART_ROWS);
+    // partial rows (up to ATTN_PART_ROWS per (b,h)) + the colsum chunk sums (<= B rows of 3C)
+    const size_t per_bh = std::max((size_t)T, (size_t)3 * (C / NH) * (fa::ATTN_PART_ROWS + 1));
     return (size_t)B * NH * per_bh;
 }
 
@@ -617,8 +626,11 @@ void attn_backward_fused(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, co
     }
     if (!rows) { set_error("fused attention backward: no kernel for T=%d head size %d", T, HS); return; }
     after_launch("attention_backward_fused");
-    if (dqkv_colsum) {  // the partial rows are laid out as B*rows batch entries
-        attn_colsum_reduce_k<<<3 * NH, 1024, 0, s>>>(dqkv_colsum, part, B * rows, NH, C, HS);
+    if (dqkv_colsum) {  // the partial rows are laid out as B*rows batch entries; the chunk sums follow them
+        const int nch = std::min(32, B);
+        float* scratch = part + (size_t)B * rows * NH * 3 * HS;
+        attn_colsum_part_k<<<dim3(3 * NH, nch), 256, 0, s>>>(scratch, part, B * rows, NH, C, HS);
+        attn_colsum_final_k<<<cdiv(3 * C, 256), 256, 0, s>>>(dqkv_colsum, scratch, nch, 3 * C);
         after_launch("attention_colsum_reduce");
     }
 }
@@ -648,5 +660,10 @@ void attention_backward_fused_bf16(uint16_t* dinp, const uint16_t* dout, const u
                                    const uint16_t* out, const float* lse, int B, int T, int C,
                                    int NH) {
     attn_backward_fused(dinp, dout, inp, out, lse, B, T, C, NH, stream());
+}
+void attention_backward_fused_bf16_ex(uint16_t* dinp, const uint16_t* dout, const uint16_t* inp,
+                                      const uint16_t* out, const float* lse, int B, int T, int C, int NH,
+                                      float* dqkv_bias) {
+    attn_backward_fused(dinp, dout, inp, out, lse, B, T, C, NH, stream(), dqkv_bias);
 }
 }

@@ -80,6 +80,15 @@ __device__ __forceinline__ bf16x8_t pack_acc(f32x4_t a, f32x4_t b) {
 // v_exp_f32 (2^x, ~1 ulp; results below 2^-126 flush to 0, irrelevant for probabilities that
 // are rounded to bf16); exp2f adds a denormal range-reduction sequence around it
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+// sum over the 16 lanes of a DPP row, valid in lane 15 of the row (row_shr 1, 2, 4, 8; lanes
+// shifted in from outside the row read 0)
+__device__ __forceinline__ float row_sum16(float v) {
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xF, 0xF, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x112, 0xF, 0xF, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x114, 0xF, 0xF, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x118, 0xF, 0xF, false));
+    return v;
+}
 __device__ __forceinline__ f32x4_t mfma(bf16x8_t a, bf16x8_t b, f32x4_t c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -711,8 +720,8 @@ __device__ __forceinline__ void bwd_slice_b(const bf16_t* Ks, const bf16_t* dSs,
     }
 }
 
-// end of an item: dK, dV of the wave's keys; per-wave column sums of dQ | dK | dV into part[3 HS]
-// (the caller sums the waves' rows after a barrier)
+// end of an item: dK, dV of the wave's keys; the wave's column sums of dQ | dK | dV into its own
+// partial row part[3 HS] (attn_colsum_reduce_k sums the rows: no barrier, no LDS)
 template <int HS>
 __device__ __forceinline__ void bwd_item_end(BwdRegs<HS>& R, bf16_t* dq, long long C, int key0, int T, float scale,
                                              float* part, int lane) {
@@ -731,6 +740,8 @@ __device__ __forceinline__ void bwd_item_end(BwdRegs<HS>& R, bf16_t* dq, long lo
         }
     }
     if (!part) return;
+    // reductions over the 16 key lanes of a DPP row (row_shr 1, 2, 4, 8: the sum lands in lane
+    // 15 of the row), written by lanes i == 15 straight to the wave's partial row in global memory
 #pragma unroll
     for (int dt = 0; dt < DT; dt++)
 #pragma unroll
@@ -742,12 +753,9 @@ __device__ __forceinline__ void bwd_item_end(BwdRegs<HS>& R, bf16_t* dq, long lo
                     tk += R.dk[kk][dt][r] * scale;
                     tv += R.dv[kk][dt][r];
                 }
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) {
-                tk += __shfl_xor(tk, o, 64);
-                tv += __shfl_xor(tv, o, 64);
-            }
-            if (i == 0) {
+            tk = row_sum16(tk);
+            tv = row_sum16(tv);
+            if (i == 15) {
                 part[HS + 16 * dt + 4 * g + r] = tk;
                 part[2 * HS + 16 * dt + 4 * g + r] = tv;
             }
@@ -765,10 +773,8 @@ __device__ __forceinline__ void bwd_item_end(BwdRegs<HS>& R, bf16_t* dq, long lo
         for (int j = 0; j < 8; j++) {
             const int d = 32 * s + (j < 4 ? 4 * g + j : 16 + 4 * g + j - 4);
             if (d >= HS) continue;  // zero half of the last k-step (HS % 32 == 16)
-            float t = sd[0] * (float)R.kf[0][s][j] + sd[1] * (float)R.kf[1][s][j];
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) t += __shfl_xor(t, o, 64);
-            if (i == 0) part[d] = t * scale;
+            const float t = row_sum16(sd[0] * (float)R.kf[0][s][j] + sd[1] * (float)R.kf[1][s][j]);
+            if (i == 15) part[d] = t * scale;
         }
 }
 
@@ -789,7 +795,8 @@ struct Bwd1 {
 // (more waves -> 3 per SIMD -> 168 VGPRs, which the 32-key accumulators do not fit)
 template <int HS, int NKT>
 constexpr bool bwd1_fits() {
-    return Bwd1<HS, NKT>::BYTES <= 160 * 1024 && (NKT / 2 <= 4 || (NKT / 2 <= 8 && HS <= 80));
+    return Bwd1<HS, NKT>::BYTES <= 160 * 1024 && (NKT / 2 <= 4 || (NKT / 2 <= 8 && HS <= 80)) &&
+           NKT / 2 <= ATTN_PART_ROWS;
 }
 
 template <int HS, int NKT>
@@ -886,17 +893,9 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
         bwd_slice_b<HS, NSL, NW>(Ks, dSs, dq, C3, q0, T, scale, w, lane);
         __syncthreads();
     }
-    float* part = reinterpret_cast<float*>(lds + Z::Q_OFF);  // slices / dS free now: [NW][3 HS]
-    bwd_item_end<HS>(R, dq, C, key0, T, scale, dsum ? part + w * 3 * HS : nullptr, lane);
-    if (dsum) {  // per-(b,h) column sums of dQ | dK | dV -> dsum[bh][3*HS]
-        __syncthreads();
-        for (int t = tid; t < 3 * HS; t += NT) {
-            float a = 0.f;
-#pragma unroll
-            for (int ww = 0; ww < NW; ww++) a += part[ww * 3 * HS + t];
-            dsum[(long long)bh * 3 * HS + t] = a;
-        }
-    }
+    // per-wave column-sum rows: dsum[((b NW + w) NH + h)][3 HS]
+    bwd_item_end<HS>(R, dq, C, key0, T, scale,
+                     dsum ? dsum + ((long long)(b * NW + w) * NH + h) * 3 * HS : nullptr, lane);
 }
 
 template <int HS, int NKT>
@@ -911,8 +910,7 @@ struct Bwdp {
     static constexpr int S_OFF = D_OFF + 2 * 32 * SK * 2;    // dS^T [TP][BWD_SDS]
     static constexpr int L_OFF = S_OFF + TP * BWD_SDS * 2;   // lse [2][TP] (item parity)
     static constexpr int E_OFF = L_OFF + 2 * TP * 4;         // delta [2][32] (slice parity)
-    static constexpr int P_OFF = E_OFF + 2 * 32 * 4;         // column-sum partials [NW][3 HS]
-    static constexpr int BYTES = P_OFF + NW * 3 * HS * 4;
+    static constexpr int BYTES = E_OFF + 2 * 32 * 4;
     static constexpr int PER = (32 * CH + NT - 1) / NT;      // 16-B pieces per thread, slice operand
     static constexpr int PERS = (2 * 32 * CH + NT - 1) / NT; // next item's K + V rows, per slice
 };
@@ -941,7 +939,6 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwdp_k(bf16_t* __restric
     bf16_t* dSs = reinterpret_cast<bf16_t*>(lds + Z::S_OFF);
     float* lse_s = reinterpret_cast<float*>(lds + Z::L_OFF);
     float* del_s = reinterpret_cast<float*>(lds + Z::E_OFF);
-    float* part = reinterpret_cast<float*>(lds + Z::P_OFF);
     const long long C3 = 3LL * C;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int key0 = w * 32;
@@ -1061,16 +1058,8 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwdp_k(bf16_t* __restric
             bwd_slice_b<HS, NSL, NW>(Kimg + kb * TP * SV, dSs, dq, C3, q0, T, scale, w, lane);
             __syncthreads();
         }
-        bwd_item_end<HS>(R, dq, C, key0, T, scale, dsum ? part + w * 3 * HS : nullptr, lane);
-        if (dsum) {
-            __syncthreads();
-            for (int t = tid; t < 3 * HS; t += NT) {
-                float a = 0.f;
-#pragma unroll
-                for (int ww = 0; ww < NW; ww++) a += part[ww * 3 * HS + t];
-                dsum[(long long)bh * 3 * HS + t] = a;
-            }
-        }
+        bwd_item_end<HS>(R, dq, C, key0, T, scale,
+                         dsum ? dsum + ((long long)((bh / NH) * NW + w) * NH + bh % NH) * 3 * HS : nullptr, lane);
         if (has_next) {
             kb ^= 1;
             load_kv(R, kb);  // every block was put before the item's last barrier
@@ -1104,13 +1093,13 @@ int launch_bwd(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t
         if (v == 0) {
             attn_bwdp_k<HS, NKT><<<std::min(BH, attn_cu_count()), NKT / 2 * 64, 0, s>>>(dqkv, dout, qkv, out, lse, T,
                                                                                       C, NH, BH, part);
-            return 1;
+            return NKT / 2;
         }
     }
     if constexpr (bwd1_fits<HS, NKT>()) {
         if (v != 2) {
             attn_bwd1_k<HS, NKT><<<BH, NKT / 2 * 64, 0, s>>>(dqkv, dout, qkv, out, lse, T, C, NH, part);
-            return 1;
+            return NKT / 2;
         }
     }
     attn_bwd_pair_k<HS, NKT><<<2 * cdiv(BH, 8) * 8, 256, 0, s>>>(dqkv, dout, qkv, out, lse, T, C, NH, BH, part);
