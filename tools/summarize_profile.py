@@ -31,8 +31,8 @@ CLASS_KERNELS = {
     "gemm_fc_fwd": (r"g2::gemm_kernel<true, true, 4\b", None),
     "gemm_qkv_fwd": (r"g2::gemm_kernel<true, true, 3\b", None),
     "gemm_proj_dgrad": (r"g2::gemm_kernel<true, false, 3\b", None),
-    "attention_bwd": (r"attn_bwd_fused_k", None),
-    "attention_fwd": (r"attn_fwd_fused_k", None),
+    "attention_bwd": (r"attn_bwd(p|1|_pair)_k", None),
+    "attention_fwd": (r"attn_fwd_k", None),
 }
 
 
