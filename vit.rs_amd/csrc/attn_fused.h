@@ -602,20 +602,19 @@ __global__ __launch_bounds__(256, (bwd_occ<HS, NKT>())) void attn_bwd_pair_k(
 // Two forms: attn_bwdp_k (persistent: one workgroup per CU walks the items and fetches the next
 // item's K / V rows and the next slice's Q / dO / O rows under the current slice's MFMA work) and
 // attn_bwd1_k (one workgroup per item, blocking prologue) where the persistent LDS does not fit.
-constexpr int BWD_SDS = 48;
-constexpr int ATTN_PART_ROWS = 8;
-   // column-sum partial rows per (b,h) a backward kernel may write  // dS^T [key][query] row stride: (SDS/2) = 8*odd dwords (tr reads)
+constexpr int BWD_SDS = 48;          // dS^T [key][query] row stride: (SDS/2) = 8*odd dwords (tr reads)
+constexpr int ATTN_PART_ROWS = 16;   // column-sum partial rows per (b,h) a backward kernel may write
 
-template <int HS>
-struct BwdRegs {  // per-wave state of the one-pass backward
-    bf16x8_t kf[2][Geo<HS>::KS], vf[2][Geo<HS>::KS];  // K, V rows of the wave's 32 keys (B operands)
-    f32x4_t dv[2][Geo<HS>::DT], dk[2][Geo<HS>::DT];   // [kk][dt]: lane (i,g) -> [d = 16dt+4g+r][key = 16kk+i]
+template <int HS, int KK = 2>
+struct BwdRegs {  // per-wave state of the one-pass backward: the wave owns KK 16-key tiles
+    bf16x8_t kf[KK][Geo<HS>::KS], vf[KK][Geo<HS>::KS];  // K, V rows of the wave's keys (B operands)
+    f32x4_t dv[KK][Geo<HS>::DT], dk[KK][Geo<HS>::DT];   // [kk][dt]: lane (i,g) -> [d = 16dt+4g+r][key = 16kk+i]
     // per-key sums of dS over the queries: the dQ column sums (qkv-bias gradient) follow as
     // sum_q dQ[q][d] = scale * sum_key (sum_q dS[q][key]) K[key][d], with K in registers
-    float sds[2];
+    float sds[KK];
     __device__ __forceinline__ void zero() {
 #pragma unroll
-        for (int kk = 0; kk < 2; kk++) {
+        for (int kk = 0; kk < KK; kk++) {
 #pragma unroll
             for (int dt = 0; dt < Geo<HS>::DT; dt++) dv[kk][dt] = dk[kk][dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
             sds[kk] = 0.f;
@@ -628,14 +627,14 @@ struct BwdRegs {  // per-wave state of the one-pass backward
 // MASK: for operands whose rows past T are copies of row T-1 (not zero), the probabilities
 // of padded queries (q >= T) and keys (key >= T) are masked to 0 (nq / nk: valid queries / keys
 // counted from the slice's and the wave's first one)
-template <int HS, bool MASK = false>
-__device__ __forceinline__ void bwd_slice_a(BwdRegs<HS>& R, const bf16_t* Qc, const bf16_t* Dc, const float* lq_s,
+template <int HS, int KK = 2, bool MASK = false>
+__device__ __forceinline__ void bwd_slice_a(BwdRegs<HS, KK>& R, const bf16_t* Qc, const bf16_t* Dc, const float* lq_s,
                                             const float* dl_s, bf16_t* dSk, float c, int lane, int nq = 0,
                                             int nk = 0) {
     using G = Geo<HS>;
     constexpr int KS = G::KS, DT = G::DT, SK = G::SK;
     const int i = lane & 15, g = lane >> 4;
-    f32x4_t P[2][2], dS[2][2];  // [kk][u]: lane (i,g) -> [q = 16u+4g+r][key = 16kk+i]
+    f32x4_t P[KK][2], dS[KK][2];  // [kk][u]: lane (i,g) -> [q = 16u+4g+r][key = 16kk+i]
 #pragma unroll
     for (int u = 0; u < 2; u++) {
         bf16x8_t qr[KS], dr[KS];
@@ -651,7 +650,7 @@ __device__ __forceinline__ void bwd_slice_a(BwdRegs<HS>& R, const bf16_t* Qc, co
             dq[r] = dl_s[16 * u + 4 * g + r];
         }
 #pragma unroll
-        for (int kk = 0; kk < 2; kk++) {
+        for (int kk = 0; kk < KK; kk++) {
             f32x4_t s_ = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int s = 0; s < KS; s++) {
@@ -668,9 +667,9 @@ __device__ __forceinline__ void bwd_slice_a(BwdRegs<HS>& R, const bf16_t* Qc, co
             }
         }
     }
-    bf16x8_t pb[2], db[2];
+    bf16x8_t pb[KK], db[KK];
 #pragma unroll
-    for (int kk = 0; kk < 2; kk++) {
+    for (int kk = 0; kk < KK; kk++) {
         pb[kk] = pack_acc(P[kk][0], P[kk][1]);
         db[kk] = pack_acc(dS[kk][0], dS[kk][1]);
     }
@@ -679,7 +678,7 @@ __device__ __forceinline__ void bwd_slice_a(BwdRegs<HS>& R, const bf16_t* Qc, co
         const bf16x8_t td = frag_tr(Dc, SK, 0, 16 * dt, lane);
         const bf16x8_t tq = frag_tr(Qc, SK, 0, 16 * dt, lane);
 #pragma unroll
-        for (int kk = 0; kk < 2; kk++) {
+        for (int kk = 0; kk < KK; kk++) {
             R.dv[kk][dt] = mfma(td, pb[kk], R.dv[kk][dt]);
             R.dk[kk][dt] = mfma(tq, db[kk], R.dk[kk][dt]);
         }
@@ -688,7 +687,7 @@ __device__ __forceinline__ void bwd_slice_a(BwdRegs<HS>& R, const bf16_t* Qc, co
     // and tile.  Without MASK, padded keys carry P != 0 (their K, V rows are zero): their dS is
     // finite and multiplies the zero K rows in dQ.
 #pragma unroll
-    for (int kk = 0; kk < 2; kk++)
+    for (int kk = 0; kk < KK; kk++)
 #pragma unroll
         for (int u = 0; u < 2; u++) {
             const bf16x4_t h4 = u ? __builtin_shufflevector(db[kk], db[kk], 4, 5, 6, 7)
@@ -722,14 +721,14 @@ __device__ __forceinline__ void bwd_slice_b(const bf16_t* Ks, const bf16_t* dSs,
 
 // end of an item: dK, dV of the wave's keys; the wave's column sums of dQ | dK | dV into its own
 // partial row part[3 HS] (attn_colsum_reduce_k sums the rows: no barrier, no LDS)
-template <int HS>
-__device__ __forceinline__ void bwd_item_end(BwdRegs<HS>& R, bf16_t* dq, long long C, int key0, int T, float scale,
+template <int HS, int KK = 2>
+__device__ __forceinline__ void bwd_item_end(BwdRegs<HS, KK>& R, bf16_t* dq, long long C, int key0, int T, float scale,
                                              float* part, int lane) {
     constexpr int KS = Geo<HS>::KS, DT = Geo<HS>::DT;
     const int i = lane & 15, g = lane >> 4;
     const long long C3 = 3 * C;
 #pragma unroll
-    for (int kk = 0; kk < 2; kk++) {
+    for (int kk = 0; kk < KK; kk++) {
         const int key = key0 + 16 * kk + i;
         if (key >= T) continue;
         bf16_t* dst = dq + (long long)key * C3 + 4 * g;
@@ -748,7 +747,7 @@ __device__ __forceinline__ void bwd_item_end(BwdRegs<HS>& R, bf16_t* dq, long lo
         for (int r = 0; r < 4; r++) {
             float tk = 0.f, tv = 0.f;
 #pragma unroll
-            for (int kk = 0; kk < 2; kk++)
+            for (int kk = 0; kk < KK; kk++)
                 if (key0 + 16 * kk + i < T) {
                     tk += R.dk[kk][dt][r] * scale;
                     tv += R.dv[kk][dt][r];
@@ -761,9 +760,9 @@ __device__ __forceinline__ void bwd_item_end(BwdRegs<HS>& R, bf16_t* dq, long lo
             }
         }
     // dQ: lane (i,g) sums over the 4 g-groups' queries, then over its key column i
-    float sd[2];
+    float sd[KK];
 #pragma unroll
-    for (int kk = 0; kk < 2; kk++) {
+    for (int kk = 0; kk < KK; kk++) {
         sd[kk] = R.sds[kk] + __shfl_xor(R.sds[kk], 16, 64);
         sd[kk] += __shfl_xor(sd[kk], 32, 64);
     }
@@ -773,7 +772,10 @@ __device__ __forceinline__ void bwd_item_end(BwdRegs<HS>& R, bf16_t* dq, long lo
         for (int j = 0; j < 8; j++) {
             const int d = 32 * s + (j < 4 ? 4 * g + j : 16 + 4 * g + j - 4);
             if (d >= HS) continue;  // zero half of the last k-step (HS % 32 == 16)
-            const float t = row_sum16(sd[0] * (float)R.kf[0][s][j] + sd[1] * (float)R.kf[1][s][j]);
+            float t = 0.f;
+#pragma unroll
+            for (int kk = 0; kk < KK; kk++) t += sd[kk] * (float)R.kf[kk][s][j];
+            t = row_sum16(t);
             if (i == 15) part[d] = t * scale;
         }
 }
@@ -898,10 +900,10 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
                      dsum ? dsum + ((long long)(b * NW + w) * NH + h) * 3 * HS : nullptr, lane);
 }
 
-template <int HS, int NKT>
+template <int HS, int NKT, int KK = 2>
 struct Bwdp {
     using G = Geo<HS>;
-    static constexpr int TP = NKT * 16, NW = NKT / 2, NT = NW * 64, NSL = TP / 32, CH = G::CH;
+    static constexpr int TP = NKT * 16, NW = NKT / KK, NT = NW * 64, NSL = TP / 32, CH = G::CH;
     static constexpr int SK = G::SK, SV = G::SV;
     static constexpr int K_OFF = 0;                          // K images [2][TP][SV]: current / next item
     static constexpr int V_OFF = K_OFF + 2 * TP * SV * 2;    // next item's V rows [TP][SK]
@@ -914,21 +916,25 @@ struct Bwdp {
     static constexpr int PER = (32 * CH + NT - 1) / NT;      // 16-B pieces per thread, slice operand
     static constexpr int PERS = (2 * 32 * CH + NT - 1) / NT; // next item's K + V rows, per slice
 };
-// the delta reduction runs over CH consecutive lanes (a power of two dividing 64)
-template <int HS, int NKT>
+// the delta reduction runs over CH consecutive lanes (a power of two dividing 64).  KK = 2: 32 keys
+// per wave, up to 8 waves (bwd1's register rule).  KK = 1 (16 keys per wave, twice the waves and
+// the LDS reads, <= 128 VGPRs) measured 377 vs 296 us at ViT-B/16 (spills; LDS-bound): not launched.
+template <int HS, int NKT, int KK = 2>
 constexpr bool bwdp_fits() {
-    return bwd1_fits<HS, NKT>() && Bwdp<HS, NKT>::BYTES <= 160 * 1024 && (64 % Geo<HS>::CH) == 0 && HS <= 64;
+    using Z = Bwdp<HS, NKT, KK>;
+    return Z::BYTES <= 160 * 1024 && (64 % Geo<HS>::CH) == 0 && HS <= 64 && Z::NW <= ATTN_PART_ROWS &&
+           (KK == 2 ? bwd1_fits<HS, NKT>() : Z::NW <= 16);
 }
 
-template <int HS, int NKT>
-__global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwdp_k(bf16_t* __restrict__ dqkv,
+template <int HS, int NKT, int KK>
+__global__ __launch_bounds__(NKT / KK * 64, 1) void attn_bwdp_k(bf16_t* __restrict__ dqkv,
                                                                const bf16_t* __restrict__ dout,
                                                                const bf16_t* __restrict__ qkv,
                                                                const bf16_t* __restrict__ out,
                                                                const float* __restrict__ lse, int T,
                                                                int C, int NH, int BH, float* __restrict__ dsum) {
     using G = Geo<HS>;
-    using Z = Bwdp<HS, NKT>;
+    using Z = Bwdp<HS, NKT, KK>;
     constexpr int TP = Z::TP, NW = Z::NW, NT = Z::NT, NSL = Z::NSL, SK = Z::SK, SV = Z::SV;
     constexpr int KS = G::KS, CH = G::CH, PER = Z::PER, PERS = Z::PERS;
     __shared__ __attribute__((aligned(16))) char lds[Z::BYTES];
@@ -941,7 +947,7 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwdp_k(bf16_t* __restric
     float* del_s = reinterpret_cast<float*>(lds + Z::E_OFF);
     const long long C3 = 3LL * C;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int key0 = w * 32;
+    const int key0 = w * 16 * KK;
     const float scale = 1.0f / sqrtf((float)HS);
     const float c = LOG2E * scale;
     auto qkv_of = [&](int bh) { return qkv + (long long)(bh / NH) * T * C3 + (bh % NH) * HS; };
@@ -1001,9 +1007,9 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwdp_k(bf16_t* __restric
             }
         }
     };
-    auto load_kv = [&](BwdRegs<HS>& R, int kbuf) {  // the wave's fragments from the staged rows
+    auto load_kv = [&](BwdRegs<HS, KK>& R, int kbuf) {  // the wave's fragments from the staged rows
 #pragma unroll
-        for (int kk = 0; kk < 2; kk++)
+        for (int kk = 0; kk < KK; kk++)
 #pragma unroll
             for (int s = 0; s < KS; s++) {
                 R.kf[kk][s] = frag_row<HS>(Kimg + kbuf * TP * SV, SV, key0 + 16 * kk, s, lane);
@@ -1024,7 +1030,7 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwdp_k(bf16_t* __restric
     for (int t = tid; t < TP; t += NT) lse_s[t] = t < T ? lse[(long long)bh * T + t] : INFINITY;
     put_slice(0);
     __syncthreads();
-    BwdRegs<HS> R;
+    BwdRegs<HS, KK> R;
     load_kv(R, 0);
     int kb = 0, it = 0;
 #pragma unroll 1
@@ -1045,7 +1051,7 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwdp_k(bf16_t* __restric
                 fetch_side(bhn, sl);
                 if (sl == 0 && tid < TP) lse_n = tid < T ? lse[(long long)bhn * T + tid] : INFINITY;
             }
-            bwd_slice_a<HS>(R, Qs + cur * 32 * SK, Ds + cur * 32 * SK, lse_cur + q0, del_s + cur * 32,
+            bwd_slice_a<HS, KK>(R, Qs + cur * 32 * SK, Ds + cur * 32 * SK, lse_cur + q0, del_s + cur * 32,
                             dSs + key0 * BWD_SDS, c, lane);
             __syncthreads();
             // buffers written here were last read before the barrier above (slice buffer cur^1 by
@@ -1058,7 +1064,7 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwdp_k(bf16_t* __restric
             bwd_slice_b<HS, NSL, NW>(Kimg + kb * TP * SV, dSs, dq, C3, q0, T, scale, w, lane);
             __syncthreads();
         }
-        bwd_item_end<HS>(R, dq, C, key0, T, scale,
+        bwd_item_end<HS, KK>(R, dq, C, key0, T, scale,
                          dsum ? dsum + ((long long)((bh / NH) * NW + w) * NH + bh % NH) * 3 * HS : nullptr, lane);
         if (has_next) {
             kb ^= 1;
@@ -1089,10 +1095,10 @@ template <int HS, int NKT>
 int launch_bwd(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t* out, const float* lse, int B,
                int T, int C, int NH, float* part, hipStream_t s) {
     const int v = attn_bwd_variant(), BH = B * NH;
-    if constexpr (bwdp_fits<HS, NKT>()) {
+    if constexpr (bwdp_fits<HS, NKT, 2>()) {
         if (v == 0) {
-            attn_bwdp_k<HS, NKT><<<std::min(BH, attn_cu_count()), NKT / 2 * 64, 0, s>>>(dqkv, dout, qkv, out, lse, T,
-                                                                                      C, NH, BH, part);
+            attn_bwdp_k<HS, NKT, 2><<<std::min(BH, attn_cu_count()), NKT / 2 * 64, 0, s>>>(dqkv, dout, qkv, out, lse,
+                                                                                         T, C, NH, BH, part);
             return NKT / 2;
         }
     }
