@@ -334,6 +334,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
     int wg, split;
     split_remap(ntm * ntn, wg, split);
     int tm0 = (wg / ntn) * BM, tn0 = (wg % ntn) * BN;
+    if (p.group_m > 0) {  // grouped order: GM M-rows x all N-columns, walked column-major
+        const int GM = p.group_m, per = GM * ntn, grp = wg / per, first = grp * GM;
+        const int gsz = min(GM, ntm - first), r = wg - grp * per;
+        tm0 = (first + r % gsz) * BM;
+        tn0 = (r / gsz) * BN;
+    }
     if (p.debug_same_tile) { tm0 = 0; tn0 = 0; }  // diagnostic: every block streams one tile (L2)
     const int kbeg = split * p.kchunk;
     const int kend = min(p.K, kbeg + p.kchunk);
@@ -1120,6 +1126,7 @@ GemmParams make_gemm_params(const GemmArgs& a, int kchunk) {
     p.no_epi = (g_debug_flags & 2) ? 1 : 0;
     p.epi_generic = (g_debug_flags & 32) ? 1 : 0;
     p.stagger = (g_debug_flags >> 8) & 63;
+    p.group_m = (g_debug_flags >> 16) & 63;
     p.tiles = 1;
     return p;
 }

@@ -22,6 +22,7 @@ struct GemmParams {
     int epi_generic;  // A/B (debug flag 32): the generic (bounds-checked) staged epilogue everywhere
     int tiles;   // output tiles of the launch (the grid is tiles x K-splits)
     int stagger;  // first-round start delay of every other workgroup, in s_sleep(127) units
+    int group_m;  // > 0: tiles walk groups of group_m M-rows column by column (L2 reuse of B panels)
 };
 
 // (tile, K-split) of this workgroup.  Workgroups are dealt round-robin over the 8 XCDs in
