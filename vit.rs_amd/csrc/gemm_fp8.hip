@@ -249,64 +249,59 @@ __device__ __forceinline__ int mx_scale_byte(float amax) {
     int s = e - 8 + (mant > 0x600000 ? 1 : 0);  // X + 127 with X = ceil(log2(amax / 448))
     return s < 0 ? 0 : (s > 254 ? 254 : s);
 }
-// blockIdx.y: matrix of a batch (x, q, sl advance by xs elements, qs bytes, ss bytes)
+// One wave per (32-row group, 64-k step) was the round-1 form: a wave instruction moved 32 rows x
+// 16 B (partial lines); the row-major form below replaced it (ViT-H/14 fp8: 18.8 -> 14.2 ms/step).
+// blockIdx.y: matrix of a batch (x, q, sl advance by xs elements, qs bytes, ss bytes).
+// Row-major: 8 consecutive elements per lane, 4 lanes per 32-element MX
+// block (amax by two xor-shuffles), so a wave instruction moves 512 consecutive elements of a row
+// (1 KiB of bf16 in, 512 B of fp8 out).  Rows R .. Rpad-1 write scale 0 and no data.
 template <typename TX>
-__global__ __launch_bounds__(256) void quantize_mx_k(uint8_t* __restrict__ q, uint8_t* __restrict__ sl,
-                                                     const TX* __restrict__ x, int R, int K, long long ldx,
-                                                     long long ldq, int rg_tot, long long xs, long long qs,
-                                                     long long ss) {
+__global__ __launch_bounds__(256) void quantize_mx_rows_k(uint8_t* __restrict__ q, uint8_t* __restrict__ sl,
+                                                          const TX* __restrict__ x, int R, int Rpad, int K,
+                                                          long long ldx, long long ldq, int rg_tot, long long xs,
+                                                          long long qs, long long ss) {
     x += blockIdx.y * xs;
     q += blockIdx.y * qs;
     sl += blockIdx.y * ss;
-    const int lane = threadIdx.x & 63;
-    const long long wv = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int nks = K / 64;
-    if (wv >= (long long)rg_tot * nks) return;
-    const int ks = (int)(wv / rg_tot), rg = (int)(wv - (long long)ks * rg_tot);
-    const int r = lane & 31, h = lane >> 5;
-    const int row = rg * 32 + r;
-    const int k0 = ks * 64 + h * 32;
-    float v[32];
+    const int kc = K / 8;  // granules per row (K % 64 == 0: a block's 4 granules never straddle rows)
+    const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (gid >= (long long)Rpad * kc) return;  // whole 4-lane groups (Rpad * kc % 4 == 0)
+    const int row = (int)(gid / kc), g8 = (int)(gid - (long long)row * kc), col = g8 * 8;
+    float v[8];
     if (row < R) {
-        const TX* src = x + (long long)row * ldx + k0;
+        const TX* src = x + (long long)row * ldx + col;
         if constexpr (sizeof(TX) == 2) {
+            const u32x4 w = *reinterpret_cast<const u32x4*>(src);
 #pragma unroll
-            for (int c = 0; c < 4; c++) {
-                const u32x4 w = reinterpret_cast<const u32x4*>(src)[c];
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    v[8 * c + 2 * e] = __uint_as_float(w[e] << 16);
-                    v[8 * c + 2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
-                }
+            for (int e = 0; e < 4; e++) {
+                v[2 * e] = __uint_as_float(w[e] << 16);
+                v[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
             }
         } else {
-#pragma unroll
-            for (int c = 0; c < 8; c++) {
-                const float4 w = reinterpret_cast<const float4*>(src)[c];
-                v[4 * c] = w.x; v[4 * c + 1] = w.y; v[4 * c + 2] = w.z; v[4 * c + 3] = w.w;
-            }
+            const float4 a = reinterpret_cast<const float4*>(src)[0], b = reinterpret_cast<const float4*>(src)[1];
+            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
         }
     } else {
 #pragma unroll
-        for (int j = 0; j < 32; j++) v[j] = 0.f;
+        for (int j = 0; j < 8; j++) v[j] = 0.f;
     }
     float amax = 0.f;
 #pragma unroll
-    for (int j = 0; j < 32; j++) amax = fmaxf(amax, fabsf(v[j]));
+    for (int j = 0; j < 8; j++) amax = fmaxf(amax, fabsf(v[j]));
+    amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+    amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
     const int sb = row < R ? mx_scale_byte(amax) : 0;
-    sl[((long long)ks * rg_tot + rg) * 64 + lane] = (uint8_t)sb;
+    if ((g8 & 3) == 0) {
+        const int kb = col >> 5, ks = kb >> 1, h = kb & 1;
+        sl[((long long)ks * rg_tot + (row >> 5)) * 64 + h * 32 + (row & 31)] = (uint8_t)sb;
+    }
     if (row >= R) return;
     const float inv = __uint_as_float((uint32_t)(254 - sb) << 23);  // 2^(127 - sb), exact
-    uint32_t w[8];
-#pragma unroll
-    for (int c = 0; c < 8; c++) {
-        int t = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * c] * inv, v[4 * c + 1] * inv, 0, false);
-        t = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * c + 2] * inv, v[4 * c + 3] * inv, t, true);
-        w[c] = (uint32_t)t;
-    }
-    u32x4* dst = reinterpret_cast<u32x4*>(q + (long long)row * ldq + k0);
-    dst[0] = u32x4{w[0], w[1], w[2], w[3]};
-    dst[1] = u32x4{w[4], w[5], w[6], w[7]};
+    int t0 = __builtin_amdgcn_cvt_pk_fp8_f32(v[0] * inv, v[1] * inv, 0, false);
+    t0 = __builtin_amdgcn_cvt_pk_fp8_f32(v[2] * inv, v[3] * inv, t0, true);
+    int t1 = __builtin_amdgcn_cvt_pk_fp8_f32(v[4] * inv, v[5] * inv, 0, false);
+    t1 = __builtin_amdgcn_cvt_pk_fp8_f32(v[6] * inv, v[7] * inv, t1, true);
+    *reinterpret_cast<uint2*>(q + (long long)row * ldq + col) = make_uint2((uint32_t)t0, (uint32_t)t1);
 }
 }  // namespace f8
 
@@ -359,9 +354,10 @@ static void quantize_mx(uint8_t* q, uint8_t* sl, const TX* x, long long R, int K
         set_error("quantize_mx: K %% 64 and 16-B aligned rows required (K=%d)", K);
         return;
     }
-    const int rg = (int)(mx_rows_padded(R) / 32);
-    const long long waves = (long long)rg * (K / 64);
-    f8::quantize_mx_k<TX><<<dim3(cdiv(waves, 4), count), 256, 0, s>>>(q, sl, x, (int)R, K, ldx, ldq, rg, xs, qs, ss);
+    const long long rp = mx_rows_padded(R);
+    const int rg = (int)(rp / 32);
+    f8::quantize_mx_rows_k<TX><<<dim3(cdiv(rp * (K / 8), 256), count), 256, 0, s>>>(q, sl, x, (int)R, (int)rp, K, ldx,
+                                                                                      ldq, rg, xs, qs, ss);
     after_launch("quantize_mx");
 }
 void quantize_mx_bf16(uint8_t* q, uint8_t* sl, const bf16_t* x, long long R, int K, long long ldx,
