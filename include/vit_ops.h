@@ -172,6 +172,13 @@ void gemm_fp8_fused(void* C, void* C2, long long ldc, const void* aux, long long
                     const uint8_t* A, const uint8_t* a_scale, long long lda, const uint8_t* B,
                     const uint8_t* b_scale, long long ldb, const float* bias, float* colsum_out,
                     int M, int N, int K, int epi);
+/* gemm_fp8_fused with the fused MX copy of the bf16 output (epi 4: the GELU output C2; epi 6: C):
+ * mx_q [M][N] e4m3 (ld N), mx_s lane-native scales for mx_rows_padded(M) rows, bit-identical to
+ * quantize_mx_bf16_ex of that bf16 output (padding rows' scales are left as given). */
+void gemm_fp8_fused_mx(void* C, void* C2, long long ldc, const void* aux, long long ldaux, const uint8_t* A,
+                       const uint8_t* a_scale, long long lda, const uint8_t* B, const uint8_t* b_scale,
+                       long long ldb, const float* bias, float* colsum_out, int M, int N, int K, int epi,
+                       uint8_t* mx_q, uint8_t* mx_s);
 /* tools: GEMM engine selection (1 = 128x128, 2 = 256x256 one workgroup per CU, the default,
  * 4 = 256x128 two per CU) and diagnostics (flag 2: skip epilogues, main-loop timing only) */
 void gemm_bf16_set_variant(int variant);

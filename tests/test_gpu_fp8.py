@@ -130,3 +130,40 @@ def test_gemm_fp8_quantization_error_vs_bf16(gpu):
     err = np.abs(c.numpy().reshape(M, N) - exact)
     assert err.max() / np.abs(exact).max() < 1e-1
     assert np.sqrt((err ** 2).mean() / (exact ** 2).mean()) < 4.5e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 512, 128), (1576, 3072, 192), (777, 3840, 320)])
+def test_gemm_fp8_fused_mx_output(gpu, M, N, K):
+    """The MX copy a GELU / GELU' epilogue writes next to its bf16 output (the trainer's fp8 mode
+    feeds it to the next GEMM instead of re-quantizing) is byte-identical to quantize_mx_bf16_ex of
+    that bf16 output: every e4m3 byte and the whole lane-native scale array (padding rows 0)."""
+    v = gpu
+    rng = np.random.default_rng(M + N + K)
+    a = rng.normal(size=(M, K)).astype(np.float32)
+    w = (rng.normal(size=(N, K)) * 0.05).astype(np.float32)
+    qa, sa, _, _ = quant_gpu(v, a, "bf16")
+    qw, sw, _, _ = quant_gpu(v, w, "f32")
+    bias = D(v, rng.normal(size=N).astype(np.float32))
+    nsc = int(v.lib().mx_scale_size(M, N))
+    xb = D(v, v.bf16_bits(rng.normal(size=(M, N)).astype(np.float32)), np.uint16)
+    for epi in (4, 6):
+        c, c2 = Z(v, M * N, np.uint16), Z(v, M * N, np.uint16)
+        fq, fs = Z(v, M * N, np.uint8), Z(v, nsc, np.uint8)
+        if epi == 4:
+            v.call("gemm_fp8_fused_mx", c, c2, N, None, 0, qa, sa, K, qw, sw, K, bias, None, M, N, K, 4, fq, fs)
+            out = c2
+        else:
+            v.call("gemm_fp8_fused_mx", c, None, N, xb, N, qa, sa, K, qw, sw, K, None, None, M, N, K, 6, fq, fs)
+            out = c
+        rq, rs = Z(v, M * N, np.uint8), Z(v, nsc, np.uint8)
+        v.call("quantize_mx_bf16_ex", rq, rs, out, M, N, N, N)
+        assert np.array_equal(fs.numpy(), rs.numpy()), f"epi {epi}: scale bytes differ"
+        assert np.array_equal(fq.numpy(), rq.numpy()), f"epi {epi}: e4m3 bytes differ"
+        # the bf16 outputs are unchanged by the extra output
+        c0, c02 = Z(v, M * N, np.uint16), Z(v, M * N, np.uint16)
+        if epi == 4:
+            v.call("gemm_fp8_fused", c0, c02, N, None, 0, qa, sa, K, qw, sw, K, bias, None, M, N, K, 4)
+            assert np.array_equal(c02.numpy(), c2.numpy())
+        else:
+            v.call("gemm_fp8_fused", c0, None, N, xb, N, qa, sa, K, qw, sw, K, None, None, M, N, K, 6)
+        assert np.array_equal(c0.numpy(), c.numpy())

@@ -400,6 +400,32 @@ def test_fp8_trainer_vs_oracle(gpu, oracle32, name, B):
     assert max(ef.values()) <= 1.5e-1, ef
 
 
+def test_fp8_fused_mx_epilogues_bit_identical(gpu, monkeypatch):
+    """fp8 mode's fused MX outputs (fc fwd's GELU output and fcproj dgrad's GELU' output written
+    straight to e4m3 + scales by those GEMMs) against the separate quantize passes (VIT_FP8_FUSE=0):
+    the same loss, logits and gradients up to the wgrad atomics' summation order (1e-5; a wrong
+    block scale would show as ~1e-2), micro-batched (B=8 in 2) and not."""
+    v = gpu
+    cfg = v.data.CONFIGS["test_h64"]
+    params = v.data.init_params(cfg, "parity", seed=3)
+    px, lab = v.data.synthetic_batch(cfg, 8, seed=4)
+    for mb in ("1", "2"):
+        monkeypatch.setenv("VIT_MICROBATCH", mb)
+        res = {}
+        for fuse in ("1", "0"):
+            monkeypatch.setenv("VIT_FP8_FUSE", fuse)
+            m = v.ViT.build(cfg, 8, v.VIT_FP8, params=params)
+            m.zero_grad()
+            loss = m.forward(px, lab)
+            m.backward()
+            res[fuse] = (loss, m.logits(), m.grads())
+            m.close()
+        # identical GEMM operands; only the split-K wgrad atomics' order may differ run to run
+        assert abs(res["1"][0] - res["0"][0]) <= 1e-6 * abs(res["0"][0])
+        assert rel_err(res["1"][1], res["0"][1]) < 1e-5
+        assert rel_err(res["1"][2], res["0"][2]) < 1e-5
+
+
 def test_fp8_training_reduces_loss(gpu):
     """fp8 mode fits one batch like the bf16 mode (40 SGD steps, loss / 10) and its first steps
     track the bf16 trajectory within 1e-1 (measured 6 %: e4m3 rounding of every GEMM operand)."""

@@ -105,6 +105,7 @@ _SIGS = {
     "quantize_mx_bf16_ex": (None, [P, P, P, LL, I, LL, LL]),
     "quantize_mx_f32_ex": (None, [P, P, P, LL, I, LL, LL]),
     "gemm_fp8_fused": (None, [P, P, LL, P, LL, P, P, LL, P, P, LL, P, P, I, I, I, I]),
+    "gemm_fp8_fused_mx": (None, [P, P, LL, P, LL, P, P, LL, P, P, LL, P, P, I, I, I, I, P, P]),
     "gemm_bf16_set_variant": (None, [I]), "gemm_bf16_set_debug": (None, [I]),
     "convert_f32_to_bf16": (None, [P, P, LL]),
     "convert_bf16_to_f32": (None, [P, P, LL]),

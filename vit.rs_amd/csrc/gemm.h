@@ -53,6 +53,13 @@ struct GemmArgs {
     // fp8 operands (gemm_fp8): MX scales of A and B in the lane-native layout of gemm_fp8.hip
     const void* a_scale = nullptr;
     const void* b_scale = nullptr;
+    // fused MX copy of the epilogue's bf16 output (EPI_BF16_GELU: the GELU output C2;
+    // EPI_BF16_DGELU: C), laid out as the next GEMM's A operand ([M][N] fp8, ld N, lane-native
+    // scales for mx_rows_padded(M) rows; the padding rows' scales are the caller's zeros).  Staged
+    // epilogues of the 256x256 engines only (N % 64 == 0); bit-identical to quantize_mx_bf16 of
+    // the bf16 output.
+    uint8_t* mx_q = nullptr;
+    uint8_t* mx_s = nullptr;
 };
 size_t gemm_sk_bytes();
 

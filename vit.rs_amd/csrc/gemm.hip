@@ -507,7 +507,7 @@ __device__ __forceinline__ void staged_epilogue16(const GemmParams& p, f32x4_t (
             const int m = m0 + a * 16 + r, n = n0 + c8 * 8;
             if (m >= p.M) continue;
             if (n + 8 <= p.N) {
-                epilogue8<EPI>(p, m, n, v, cs);
+                epilogue8<EPI>(p, m, n, v, cs, lane);
             } else if (n + 4 <= p.N) {
                 f32x4_t t = lo;
                 epilogue<EPI>(p, m, n, t);
@@ -1127,6 +1127,9 @@ GemmParams make_gemm_params(const GemmArgs& a, int kchunk) {
     p.epi_generic = (g_debug_flags & 32) ? 1 : 0;
     p.stagger = (g_debug_flags >> 8) & 63;
     p.group_m = (g_debug_flags >> 16) & 63;
+    p.mx_q = a.mx_q;
+    p.mx_s = a.mx_s;
+    p.mx_rg = (int)(mx_rows_padded(a.M) / 32);
     p.tiles = 1;
     return p;
 }
@@ -1158,6 +1161,10 @@ static int choose_split(int tiles, int K, int ktile, int want_blocks) {
 
 void gemm_f32(const GemmArgs& a, hipStream_t s) {
     if (a.M <= 0 || a.N <= 0) return;
+    if (a.mx_q) {
+        set_error("gemm_f32: the fused MX output is an fp8-engine feature");
+        return;
+    }
     const int tiles = cdiv(a.M, f32::BM) * cdiv(a.N, f32::BN);
     int split = 1;
     if (a.epi == EPI_F32_ATOMIC) split = a.splitk > 0 ? a.splitk : choose_split(tiles, a.K, f32::BK, 512);
@@ -1357,6 +1364,10 @@ static bool gemm_bf16_g3(const GemmArgs& a, hipStream_t s, bool whole) {
 
 void gemm_bf16(const GemmArgs& a, hipStream_t s) {
     if (a.M <= 0 || a.N <= 0) return;
+    if (a.mx_q) {
+        set_error("gemm_bf16: the fused MX output is an fp8-engine feature");
+        return;
+    }
     if (!gemm_bf16_supported(a)) {
         set_error("gemm_bf16: unsupported shape/alignment M=%d N=%d K=%d lda=%lld ldb=%lld",
                   a.M, a.N, a.K, a.lda, a.ldb);

@@ -23,7 +23,48 @@ struct GemmParams {
     int tiles;   // output tiles of the launch (the grid is tiles x K-splits)
     int stagger;  // first-round start delay of every other workgroup, in s_sleep(127) units
     int group_m;  // > 0: tiles walk groups of group_m M-rows column by column (L2 reuse of B panels)
+    uint8_t* mx_q;  // fused MX output (GemmArgs::mx_q / mx_s); mx_rg = padded rows / 32
+    uint8_t* mx_s;
+    int mx_rg;
 };
+
+// E8M0 scale byte of an MX block: X + 127 with X = ceil(log2(amax / 448)) (no element overflows
+// e4m3's 448), clamped to [0, 254]; 127 (scale 1) for an all-zero block
+__device__ __forceinline__ int mx_scale_byte(float amax) {
+    if (!(amax > 0.f)) return 127;
+    const uint32_t u = __float_as_uint(amax);
+    const int e = (int)((u >> 23) & 0xff), mant = (int)(u & 0x7fffff);
+    int s = e - 8 + (mant > 0x600000 ? 1 : 0);
+    return s < 0 ? 0 : (s > 254 ? 254 : s);
+}
+// the MX copy of 8 bf16 output values (packed as stored) at row m, columns n..n+7: the 4 lanes of
+// a 32-column block (lane bits 0-1 in the staged layout) share one scale
+__device__ __forceinline__ void mx_out8(const GemmParams& p, int m, int n, uint32_t w0, uint32_t w1, uint32_t w2,
+                                        uint32_t w3, int lane) {
+    const uint32_t w[4] = {w0, w1, w2, w3};
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        v[2 * e] = __uint_as_float(w[e] << 16);
+        v[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+    }
+    float amax = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; j++) amax = fmaxf(amax, fabsf(v[j]));
+    amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+    amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+    const int sb = mx_scale_byte(amax);
+    if ((lane & 3) == 0) {
+        const int kb = n >> 5;
+        p.mx_s[((long long)(kb >> 1) * p.mx_rg + (m >> 5)) * 64 + (kb & 1) * 32 + (m & 31)] = (uint8_t)sb;
+    }
+    const float inv = __uint_as_float((uint32_t)(254 - sb) << 23);  // 2^(127 - sb), exact
+    int t0 = __builtin_amdgcn_cvt_pk_fp8_f32(v[0] * inv, v[1] * inv, 0, false);
+    t0 = __builtin_amdgcn_cvt_pk_fp8_f32(v[2] * inv, v[3] * inv, t0, true);
+    int t1 = __builtin_amdgcn_cvt_pk_fp8_f32(v[4] * inv, v[5] * inv, 0, false);
+    t1 = __builtin_amdgcn_cvt_pk_fp8_f32(v[6] * inv, v[7] * inv, t1, true);
+    *reinterpret_cast<uint2*>(p.mx_q + (long long)m * p.N + n) = make_uint2((uint32_t)t0, (uint32_t)t1);
+}
 
 // (tile, K-split) of this workgroup.  Workgroups are dealt round-robin over the 8 XCDs in
 // linear-id order (x fastest), so the XCD-aware remap runs over the whole (split, tile) grid: the
@@ -110,7 +151,7 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, int m, int n, f32x
 // the column sums of the DGELU output (fused bias gradient).
 template <int EPI>
 __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, float (&v)[8],
-                                          float (&cs)[8]) {
+                                          float (&cs)[8], int lane = 0) {
     if constexpr (EPI != EPI_F32_ATOMIC && EPI != EPI_BF16_DGELU && EPI != EPI_F32_SLAB) {
         if (p.bias) {
             const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
@@ -150,7 +191,9 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, flo
 #pragma unroll
         for (int j = 0; j < 8; j++) gv[j] = gelu_fast_f(v[j]);
         *reinterpret_cast<uint4*>((bf16_t*)p.C + off) = pack8(v);
-        *reinterpret_cast<uint4*>((bf16_t*)p.C2 + off) = pack8(gv);
+        const uint4 g8 = pack8(gv);
+        *reinterpret_cast<uint4*>((bf16_t*)p.C2 + off) = g8;
+        if (p.mx_q) mx_out8(p, m, n, g8.x, g8.y, g8.z, g8.w, lane);
     } else if constexpr (EPI == EPI_F32_RESID) {
         const float* r = (const float*)p.aux + (long long)m * p.ldaux + n;
         const float4 r0 = reinterpret_cast<const float4*>(r)[0];
@@ -168,7 +211,9 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, flo
         }
 #pragma unroll
         for (int j = 0; j < 8; j++) cs[j] += v[j];
-        *reinterpret_cast<uint4*>((bf16_t*)p.C + off) = pack8(v);
+        const uint4 d8 = pack8(v);
+        *reinterpret_cast<uint4*>((bf16_t*)p.C + off) = d8;
+        if (p.mx_q) mx_out8(p, m, n, d8.x, d8.y, d8.z, d8.w, lane);
     }
 }
 
@@ -188,6 +233,7 @@ constexpr int STG_WAVE_BYTES = 64 * STG_LD * 4;  // 17,408 B per wave
 template <int EPI>
 __device__ __forceinline__ void staged_pass_interior(const GemmParams& p, const float* st, int rr,
                                                      int cc, int mrow, int n, float (&cs)[8]) {
+    const int cc_lane = cc >> 3;  // the lane's column group (lane bits 0-2): mx_out8's block lanes
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if constexpr (EPI != EPI_F32_ATOMIC && EPI != EPI_BF16_DGELU && EPI != EPI_F32_SLAB) {
@@ -252,7 +298,9 @@ __device__ __forceinline__ void staged_pass_interior(const GemmParams& p, const 
 #pragma unroll
             for (int j = 0; j < 8; j++) gv[j] = gelu_fast_f(v[j]);
             *reinterpret_cast<u32x4*>((bf16_t*)p.C + off) = pack8(v);
-            *reinterpret_cast<u32x4*>((bf16_t*)p.C2 + off) = pack8(gv);
+            const u32x4 g8 = pack8(gv);
+            *reinterpret_cast<u32x4*>((bf16_t*)p.C2 + off) = g8;
+            if (p.mx_q) mx_out8(p, mrow + r, n, g8[0], g8[1], g8[2], g8[3], cc_lane);
         } else if constexpr (EPI == EPI_BF16_DGELU) {
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -261,7 +309,9 @@ __device__ __forceinline__ void staged_pass_interior(const GemmParams& p, const 
             }
 #pragma unroll
             for (int j = 0; j < 8; j++) cs[j] += v[j];
-            *reinterpret_cast<u32x4*>((bf16_t*)p.C + off) = pack8(v);
+            const u32x4 d8 = pack8(v);
+            *reinterpret_cast<u32x4*>((bf16_t*)p.C + off) = d8;
+            if (p.mx_q) mx_out8(p, mrow + r, n, d8[0], d8[1], d8[2], d8[3], cc_lane);
         }
     }
 }
@@ -289,7 +339,7 @@ __device__ __forceinline__ void staged_pass(const GemmParams& p, const float* st
         const int m = m0 + pass * 64 + r, n = n0 + cc;
         if (m >= p.M) continue;
         if (n + 8 <= p.N) {
-            epilogue8<EPI>(p, m, n, v, cs);
+            epilogue8<EPI>(p, m, n, v, cs, lane);
         } else if (n + 4 <= p.N) {  // ragged N (N % 8 == 4): the 4-wide form
             f32x4_t t = lo;
             epilogue<EPI>(p, m, n, t);

@@ -242,13 +242,6 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(F8Params fp) {
 // lane (r, h) owns row 32g + r, k-block 2s + h (32 elements): amax -> the smallest power of two
 // 2^X with amax / 2^X <= 448 (the e4m3 maximum; v_cvt_pk_fp8_f32 does not saturate) -> E8M0 byte
 // X + 127 -> x * 2^-X (exact) rounded to nearest even by v_cvt_pk_fp8_f32.  Rows >= R get scale 0.
-__device__ __forceinline__ int mx_scale_byte(float amax) {
-    if (!(amax > 0.f)) return 127;
-    const uint32_t u = __float_as_uint(amax);
-    const int e = (int)((u >> 23) & 0xff), mant = (int)(u & 0x7fffff);
-    int s = e - 8 + (mant > 0x600000 ? 1 : 0);  // X + 127 with X = ceil(log2(amax / 448))
-    return s < 0 ? 0 : (s > 254 ? 254 : s);
-}
 // One wave per (32-row group, 64-k step) was the round-1 form: a wave instruction moved 32 rows x
 // 16 B (partial lines); the row-major form below replaced it (ViT-H/14 fp8: 18.8 -> 14.2 ms/step).
 // blockIdx.y: matrix of a batch (x, q, sl advance by xs elements, qs bytes, ss bytes).
@@ -312,7 +305,9 @@ bool gemm_fp8_supported(const GemmArgs& a) {
     auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
     return a.a_kcontig && a.b_kcontig && a.K % 64 == 0 && a.lda % 16 == 0 && a.ldb % 16 == 0 &&
            a.N % 4 == 0 && a.ldc % 4 == 0 && al16(a.A) && al16(a.B) && a.a_scale && a.b_scale &&
-           a.epi != EPI_F32_ATOMIC && a.epi != EPI_F32_SLAB;
+           a.epi != EPI_F32_ATOMIC && a.epi != EPI_F32_SLAB &&
+           // fused MX output: whole 32-column blocks, GELU/GELU' epilogues only (4 lanes per block)
+           (!a.mx_q || (a.mx_s && a.N % 32 == 0 && (a.epi == EPI_BF16_GELU || a.epi == EPI_BF16_DGELU)));
 }
 
 void gemm_fp8(const GemmArgs& a, hipStream_t s) {
@@ -390,6 +385,21 @@ void quantize_mx_bf16_ex(uint8_t* q, uint8_t* scales, const uint16_t* x, long lo
 void quantize_mx_f32_ex(uint8_t* q, uint8_t* scales, const float* x, long long R, int K, long long ldx,
                         long long ldq) {
     quantize_mx_f32(q, scales, x, R, K, ldx, ldq, stream());
+}
+void gemm_fp8_fused_mx(void* C, void* C2, long long ldc, const void* aux, long long ldaux, const uint8_t* A,
+                       const uint8_t* a_scale, long long lda, const uint8_t* B, const uint8_t* b_scale,
+                       long long ldb, const float* bias, float* colsum_out, int M, int N, int K, int epi,
+                       uint8_t* mx_q, uint8_t* mx_s) {
+    GemmArgs a;
+    a.C = C; a.C2 = C2; a.ldc = ldc; a.aux = aux; a.ldaux = ldaux;
+    a.A = A; a.a_scale = a_scale; a.lda = lda; a.B = B; a.b_scale = b_scale; a.ldb = ldb;
+    a.bias = bias; a.colsum_out = colsum_out; a.M = M; a.N = N; a.K = K; a.epi = epi;
+    a.mx_q = mx_q; a.mx_s = mx_s;
+    if (mx_q && (epi != EPI_BF16_GELU && epi != EPI_BF16_DGELU)) {
+        set_error("gemm_fp8_fused_mx: the MX output needs epi 4 (GELU) or 6 (GELU')");
+        return;
+    }
+    gemm_fp8(a, stream());
 }
 void gemm_fp8_fused(void* C, void* C2, long long ldc, const void* aux, long long ldaux, const uint8_t* A,
                     const uint8_t* a_scale, long long lda, const uint8_t* B, const uint8_t* b_scale,

@@ -290,6 +290,12 @@ struct Trainer {
     long long wq_n[NWK]{}, wq_k[NWK]{};  // forward view: N x K per layer
     uint8_t* act_q[4]{};
     uint8_t* act_s[4]{};
+    // fused MX outputs (fp8 mode): the GELU output of fc fwd / the GELU' output of fcproj dgrad,
+    // written by those GEMMs' epilogues and read as the next GEMM's A operand (VIT_FP8_FUSE=0
+    // quantizes them in separate passes instead, for A/B)
+    uint8_t* act_q2[4]{};
+    uint8_t* act_s2[4]{};
+    bool fuse_mx = true;
     int wslot(int k, int l) const {    // memory-order index of layer l's copy of weight kind k
         const long long stride = L > 1 ? off[wkinds[k] * L + 1] - off[wkinds[k] * L] : 0;
         return stride < 0 ? L - 1 - l : l;
@@ -558,7 +564,13 @@ struct Trainer {
                 for (int k = 0; k < MAXMB; k++) {
                     act_q[k] = alloc<uint8_t>(BT * 4 * C);
                     act_s[k] = alloc<uint8_t>((long long)mx_scale_bytes(BT, 4 * C));
+                    act_q2[k] = alloc<uint8_t>(BT * 4 * C);
+                    act_s2[k] = alloc<uint8_t>((long long)mx_scale_bytes(BT, 4 * C));
+                    // the padding rows' scales (never written by the fused epilogues) stay 0
+                    VIT_HIP(hipMemset(act_s2[k], 0, mx_scale_bytes(BT, 4 * C)));
                 }
+                const char* fe = getenv("VIT_FP8_FUSE");
+                fuse_mx = !(fe && fe[0] == '0');
             }
         } else {
             patches_f = alloc<float>((long long)B * NP * KP);
@@ -677,13 +689,24 @@ struct Trainer {
     // a forward (transposed = false) or input-gradient (true) GEMM of weight ti, layer l: bf16
     // mode as given; fp8 mode quantizes the bf16 A operand into the stream's scratch and runs the
     // MXFP8 engine against the weight's fp8 copy
-    void gemm_w(int cls, GemmArgs a, int ti, int l, bool transposed, int mb, hipStream_t st) {
+    // pre: the A operand already in MX form (a fused epilogue wrote it); otherwise it is quantized
+    // here.  mx_out: ask this GEMM's epilogue for the MX copy of its bf16 output (fp8 mode, fused)
+    void gemm_w(int cls, GemmArgs a, int ti, int l, bool transposed, int mb, hipStream_t st, bool pre = false,
+                bool mx_out = false) {
         if (!fp8()) { gemm(cls, a, true, st); return; }
-        tbeg(TC_QUANT, 0, st);
-        quantize_mx_bf16(act_q[mb], act_s[mb], (const bf16_t*)a.A, a.M, a.K, a.lda, a.K, st);
-        tend();
+        if (mx_out) { a.mx_q = act_q2[mb]; a.mx_s = act_s2[mb]; }
+        const uint8_t* aq = act_q[mb];
+        const uint8_t* as = act_s[mb];
+        if (pre) {
+            aq = act_q2[mb];
+            as = act_s2[mb];
+        } else {
+            tbeg(TC_QUANT, 0, st);
+            quantize_mx_bf16(act_q[mb], act_s[mb], (const bf16_t*)a.A, a.M, a.K, a.lda, a.K, st);
+            tend();
+        }
         const QMat w = transposed ? wtq_of(ti, l) : wq_of(ti, l);
-        a.A = act_q[mb]; a.lda = a.K; a.a_scale = act_s[mb];
+        a.A = aq; a.lda = a.K; a.a_scale = as;
         a.B = w.q; a.ldb = a.K; a.b_scale = w.s; a.b_kcontig = true;
         tbeg(cls, 2.0 * a.M * (double)a.N * a.K, st);
         gemm_fp8(a, st);
@@ -794,12 +817,12 @@ struct Trainer {
                 f.A = a.ln2 + r0 * C; f.lda = C; f.B = W(P_FCW, l); f.ldb = C; f.C = a.fch + r0 * 4 * C;
                 f.C2 = a.fchg + r0 * 4 * C; f.ldc = 4 * C; f.bias = P(P_FCB, l); f.M = (int)R; f.N = 4 * C;
                 f.K = C; f.epi = EPI_BF16_GELU;
-                gemm_w(TC_FC_FWD, f, P_FCW, l, false, mb, st);
+                gemm_w(TC_FC_FWD, f, P_FCW, l, false, mb, st, false, fuse_mx);
                 GemmArgs fp;
                 fp.A = a.fchg + r0 * 4 * C; fp.lda = 4 * C; fp.B = W(P_FCPROJW, l); fp.ldb = 4 * C;
                 fp.C = a.res3 + r0 * C; fp.ldc = C; fp.bias = P(P_FCPROJB, l); fp.aux = a.res2 + r0 * C;
                 fp.ldaux = C; fp.M = (int)R; fp.N = C; fp.K = 4 * C; fp.epi = EPI_F32_RESID;
-                gemm_w(TC_FCPROJ_FWD, fp, P_FCPROJW, l, false, mb, st);
+                gemm_w(TC_FCPROJ_FWD, fp, P_FCPROJW, l, false, mb, st, fuse_mx);
             }
         }
         mb_join();
@@ -863,7 +886,7 @@ struct Trainer {
                 d1.C = dfch + r0 * 4 * C; d1.ldc = 4 * C; d1.aux = a.fch + r0 * 4 * C; d1.ldaux = 4 * C;
                 d1.M = (int)R; d1.N = 4 * C; d1.K = C; d1.epi = EPI_BF16_DGELU;
                 d1.colsum_out = G(P_FCB, l);
-                gemm_w(TC_FCPROJ_DGRAD, d1, P_FCPROJW, l, true, mb, ms[mb]);
+                gemm_w(TC_FCPROJ_DGRAD, d1, P_FCPROJW, l, true, mb, ms[mb], false, fuse_mx);
             }
             // fc: dln2 = dfch . fcw;  fcw += dfch^T . ln2
             wgrad(TC_FC_WGRAD, dfch, 4 * C, a.ln2, C, G(P_FCW, l), EV_DFCH, EV_W2);
@@ -872,7 +895,7 @@ struct Trainer {
                 GemmArgs d2;
                 d2.A = dfch + r0 * 4 * C; d2.lda = 4 * C; dgrad_b(d2, P_FCW, l, 4 * C, C);
                 d2.C = dln_bf + r0 * C; d2.ldc = C; d2.M = (int)R; d2.N = C; d2.K = 4 * C; d2.epi = EPI_BF16_STORE;
-                gemm_w(TC_FC_DGRAD, d2, P_FCW, l, true, mb, ms[mb]);
+                gemm_w(TC_FC_DGRAD, d2, P_FCW, l, true, mb, ms[mb], fuse_mx);
                 // ln2 backward + residual: dres2 = dres3 + LN2'(dln2); attproj_b += colsum(dres2)
                 after_wgrad(EV_W3, ms[mb]);  // the previous layer's attproj wgrad has read rbB
                 tbeg(TC_LN_BWD, 0, ms[mb]);
