@@ -13,6 +13,20 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 
+// ds_read_b64_tr_b16 at LDS byte address a + OFF, issued as inline asm.  With the builtin
+// (__builtin_amdgcn_ds_read_tr16_b64_v4bf16) hipcc (ROCm 7.2) puts `s_waitcnt vmcnt(0)` in front
+// of the read whenever an LDS-DMA (global_load_lds) may be in flight, which drains the whole
+// prefetch ring of a pipelined GEMM at every phase (plain ds_read_b128 loads do not get that
+// wait).  The compiler does not count an asm read on lgkmcnt: callers must wait lgkmcnt(0) and
+// fence with sched_barrier(0) before the first use of the result.
+template <int OFF>
+__device__ __forceinline__ bf16x4_t ds_read_tr16_asm(const void* lds) {
+    bf16x4_t r;
+    const uint32_t a = (uint32_t)(uintptr_t)LDS_PTR(const char, lds);
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+    return r;
+}
+
 // ---------------------------------------------------------------- host context
 namespace vit {
 // Sticky, thread-local error (the reference ops return () — train_vit.rs:376-670 — so errors

@@ -256,10 +256,11 @@ __device__ __forceinline__ bf16x8_t frag(const char* img, int r0, int lane) {
         const int q = i >> 2, p = i & 3;
         const int ch = (r0 >> 3) + (p >> 1);
         const int k0 = 8 * g + q, k1 = k0 + 4;
+        // k1 = k0 + 4 lies in k0's 8-row group, so mn_swz(k1) == mn_swz(k0): a1 = a0 + 4 rows
+        (void)k1;
         const char* a0 = img + k0 * 512 + ((ch ^ mn_swz(k0)) << 4) + (p & 1) * 8;
-        const char* a1 = img + k1 * 512 + ((ch ^ mn_swz(k1)) << 4) + (p & 1) * 8;
-        const bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4_t, a0));
-        const bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4_t, a1));
+        const bf16x4_t lo = ds_read_tr16_asm<0>(a0);
+        const bf16x4_t hi = ds_read_tr16_asm<4 * 512>(a0);
         return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     }
 }
@@ -881,10 +882,10 @@ __device__ __forceinline__ bf16x8_t frag(const char* img, int r0, int lane) {
         const int q = i >> 2, p = i & 3;
         const int ch = (r0 >> 3) + (p >> 1);
         const int k0 = 8 * g + q, k1 = k0 + 4;
+        (void)k1;  // mn_swz<R>(k0 + 4) == mn_swz<R>(k0): a1 = a0 + 4 rows
         const char* a0 = img + k0 * (2 * R) + ((ch ^ mn_swz<R>(k0)) << 4) + (p & 1) * 8;
-        const char* a1 = img + k1 * (2 * R) + ((ch ^ mn_swz<R>(k1)) << 4) + (p & 1) * 8;
-        const bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4_t, a0));
-        const bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4_t, a1));
+        const bf16x4_t lo = ds_read_tr16_asm<0>(a0);
+        const bf16x4_t hi = ds_read_tr16_asm<4 * 2 * R>(a0);
         return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     }
 }
@@ -1127,6 +1128,8 @@ GemmParams make_gemm_params(const GemmArgs& a, int kchunk) {
     p.epi_generic = (g_debug_flags & 32) ? 1 : 0;
     p.stagger = (g_debug_flags >> 8) & 63;
     p.group_m = (g_debug_flags >> 16) & 63;
+    p.nt = (g_debug_flags & 64) ? 1 : 0;
+    p.dbg_l2 = (g_debug_flags & 128) ? 1 : 0;
     p.mx_q = a.mx_q;
     p.mx_s = a.mx_s;
     p.mx_rg = (int)(mx_rows_padded(a.M) / 32);
@@ -1377,6 +1380,17 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s) {
     if (gemm_variant() == 5 && a.M >= 256 && a.N >= 256 && gemm_bf16_g3(a, s, true)) return;
     if (gemm_variant() == 4 && a.K % g4::KTILE == 0 && a.M >= 256 && a.N >= 128 &&
         (a.epi != EPI_F32_ATOMIC || a.N % 4 == 0)) {
+        gemm_bf16_g4(a, s);
+        return;
+    }
+    // split-K weight gradients (M/N-contiguous operands, K = the token count) run on the 256x128
+    // two-per-CU engine: 3-9 % faster than 256x256 on every ViT-B/16 wgrad shape (r02,
+    // tools/bench_gemm.py), the other GEMMs are faster on 256x256
+    if (gemm_variant() == 2 && a.epi == EPI_F32_ATOMIC && !a.a_kcontig && !a.b_kcontig &&
+        a.K % g4::KTILE == 0 && a.M >= 256 && a.N >= 128 && a.N % 4 == 0 && !getenv("VIT_WGRAD_G2") &&
+        (a.splitk > 0 || !a.ws ||
+         (size_t)choose_split_g4(cdiv(a.M, g4::BM) * cdiv(a.N, g4::BN), a.K / g4::KTILE) * a.M * a.N * sizeof(float) <=
+             a.ws_bytes)) {
         gemm_bf16_g4(a, s);
         return;
     }

@@ -23,6 +23,8 @@ struct GemmParams {
     int tiles;   // output tiles of the launch (the grid is tiles x K-splits)
     int stagger;  // first-round start delay of every other workgroup, in s_sleep(127) units
     int group_m;  // > 0: tiles walk groups of group_m M-rows column by column (L2 reuse of B panels)
+    int dbg_l2;   // debug flag 128: epilogue rows taken mod 256 (its HBM traffic becomes L2 hits; output garbage)
+    int nt;       // debug flag 64: epilogue stores / aux loads non-temporal (streaming, L2 evict-first)
     uint8_t* mx_q;  // fused MX output (GemmArgs::mx_q / mx_s); mx_rg = padded rows / 32
     uint8_t* mx_s;
     int mx_rg;
@@ -80,6 +82,18 @@ __device__ __forceinline__ int split_index(int tiles) {
     int t, s;
     split_remap(tiles, t, s);
     return s;
+}
+
+// epilogue 16-B global access, optionally non-temporal (p.nt: the output / aux streams are touched
+// once, so they should not evict the operand panels the main loop re-reads from L2)
+typedef unsigned int epi_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void epi_st16(const GemmParams& p, void* q, epi_u32x4 v) {
+    if (p.nt) __builtin_nontemporal_store(v, reinterpret_cast<epi_u32x4*>(q));
+    else *reinterpret_cast<epi_u32x4*>(q) = v;
+}
+__device__ __forceinline__ epi_u32x4 epi_ld16(const GemmParams& p, const void* q) {
+    if (p.nt) return __builtin_nontemporal_load(reinterpret_cast<const epi_u32x4*>(q));
+    return *reinterpret_cast<const epi_u32x4*>(q);
 }
 
 // diagnostic: time the main loop alone (the accumulators stay live so nothing is eliminated)
@@ -233,6 +247,7 @@ constexpr int STG_WAVE_BYTES = 64 * STG_LD * 4;  // 17,408 B per wave
 template <int EPI>
 __device__ __forceinline__ void staged_pass_interior(const GemmParams& p, const float* st, int rr,
                                                      int cc, int mrow, int n, float (&cs)[8]) {
+    if (p.dbg_l2) mrow &= 255;
     const int cc_lane = cc >> 3;  // the lane's column group (lane bits 0-2): mx_out8's block lanes
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -250,15 +265,15 @@ __device__ __forceinline__ void staged_pass_interior(const GemmParams& p, const 
     if constexpr (AUX16) {
 #pragma unroll
         for (int it = 0; it < 8; it++)
-            ax[it] = *reinterpret_cast<const u32x4*>((const bf16_t*)p.aux + (long long)(mrow + it * 8 + rr) * p.ldaux + n);
+            ax[it] = epi_ld16(p, (const bf16_t*)p.aux + (long long)(mrow + it * 8 + rr) * p.ldaux + n);
     } else if constexpr (AUX32) {
         const float* src = EPI == EPI_F32_RESID ? (const float*)p.aux : (const float*)p.C;
         const long long ld = EPI == EPI_F32_RESID ? p.ldaux : p.ldc;
 #pragma unroll
         for (int it = 0; it < 8; it++) {
-            const u32x4* q = reinterpret_cast<const u32x4*>(src + (long long)(mrow + it * 8 + rr) * ld + n);
-            ax[2 * it] = q[0];
-            ax[2 * it + 1] = q[1];
+            const float* q = src + (long long)(mrow + it * 8 + rr) * ld + n;
+            ax[2 * it] = epi_ld16(p, q);
+            ax[2 * it + 1] = epi_ld16(p, q + 4);
         }
     }
     float* slab = nullptr;
@@ -277,8 +292,8 @@ __device__ __forceinline__ void staged_pass_interior(const GemmParams& p, const 
                          pack_bf16x2(w[6], w[7])};
         };
         auto st_f32 = [&](float* q) {
-            reinterpret_cast<float4*>(q)[0] = make_float4(v[0], v[1], v[2], v[3]);
-            reinterpret_cast<float4*>(q)[1] = make_float4(v[4], v[5], v[6], v[7]);
+            epi_st16(p, q, u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])});
+            epi_st16(p, q + 4, u32x4{__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7])});
         };
         if constexpr (EPI == EPI_F32_STORE) {
             st_f32((float*)p.C + off);
@@ -292,14 +307,14 @@ __device__ __forceinline__ void staged_pass_interior(const GemmParams& p, const 
             }
             st_f32((float*)p.C + off);
         } else if constexpr (EPI == EPI_BF16_STORE) {
-            *reinterpret_cast<u32x4*>((bf16_t*)p.C + off) = pack8(v);
+            epi_st16(p, (bf16_t*)p.C + off, pack8(v));
         } else if constexpr (EPI == EPI_BF16_GELU) {
             float gv[8];
 #pragma unroll
             for (int j = 0; j < 8; j++) gv[j] = gelu_fast_f(v[j]);
-            *reinterpret_cast<u32x4*>((bf16_t*)p.C + off) = pack8(v);
+            epi_st16(p, (bf16_t*)p.C + off, pack8(v));
             const u32x4 g8 = pack8(gv);
-            *reinterpret_cast<u32x4*>((bf16_t*)p.C2 + off) = g8;
+            epi_st16(p, (bf16_t*)p.C2 + off, g8);
             if (p.mx_q) mx_out8(p, mrow + r, n, g8[0], g8[1], g8[2], g8[3], cc_lane);
         } else if constexpr (EPI == EPI_BF16_DGELU) {
 #pragma unroll
@@ -310,7 +325,7 @@ __device__ __forceinline__ void staged_pass_interior(const GemmParams& p, const 
 #pragma unroll
             for (int j = 0; j < 8; j++) cs[j] += v[j];
             const u32x4 d8 = pack8(v);
-            *reinterpret_cast<u32x4*>((bf16_t*)p.C + off) = d8;
+            epi_st16(p, (bf16_t*)p.C + off, d8);
             if (p.mx_q) mx_out8(p, mrow + r, n, d8[0], d8[1], d8[2], d8[3], cc_lane);
         }
     }
