@@ -148,7 +148,10 @@ void gemm_bf16_ex(void* C, long long ldc, const uint16_t* A, long long lda, int 
                   float* dbias, int M, int N, int K, int epi, int splitk);
 /* the fused epilogues of the trainer's GEMMs: epi 4 C = pre = acc + bias, C2 = gelu(pre)
  * (both bf16); 5 C_f32 = acc + bias + aux_f32; 6 C_bf16 = acc * gelu'(aux_bf16) and, when
- * colsum_out is not NULL, colsum_out[n] += sum_m C[m][n]; 0 / 3 as gemm_bf16_ex. */
+ * colsum_out is not NULL, colsum_out[n] += sum_m C[m][n]; 0 / 3 as gemm_bf16_ex.  The pair the
+ * trainer uses for the MLP (fc forward -> fcproj dgrad): epi 8 C = gelu'(pre), C2 = gelu(pre)
+ * (both bf16, pre = acc + bias, one sigmoid for both); 9 C_bf16 = acc * aux_bf16 (aux = the
+ * stored gelu') with the colsum_out of epi 6. */
 void gemm_bf16_fused(void* C, void* C2, long long ldc, const void* aux, long long ldaux,
                      const uint16_t* A, long long lda, int a_kcontig, const uint16_t* B,
                      long long ldb, int b_kcontig, const float* bias, float* colsum_out, int M,
@@ -162,7 +165,7 @@ void gemm_bf16_fused(void* C, void* C2, long long ldc, const void* aux, long lon
  * bytes per operand.  quantize_mx_*: x [R][K] (row stride ldx elements, K % 64 == 0) -> q [R][K]
  * e4m3 (row stride ldq bytes) + scales; scale 2^X with X = ceil(log2(amax / 448)) per block,
  * x * 2^-X rounded to nearest even.  gemm_fp8_fused: C = A . B^T with A [M][K], B [N][K]
- * (K-contiguous bytes) and the epilogues of gemm_bf16_fused (epi 0, 1, 3, 4, 5, 6). */
+ * (K-contiguous bytes) and the epilogues of gemm_bf16_fused (epi 0, 1, 3, 4, 5, 6, 8, 9). */
 long long mx_scale_size(long long rows, int K);
 void quantize_mx_bf16_ex(uint8_t* q, uint8_t* scales, const uint16_t* x, long long R, int K,
                          long long ldx, long long ldq);
@@ -172,7 +175,7 @@ void gemm_fp8_fused(void* C, void* C2, long long ldc, const void* aux, long long
                     const uint8_t* A, const uint8_t* a_scale, long long lda, const uint8_t* B,
                     const uint8_t* b_scale, long long ldb, const float* bias, float* colsum_out,
                     int M, int N, int K, int epi);
-/* gemm_fp8_fused with the fused MX copy of the bf16 output (epi 4: the GELU output C2; epi 6: C):
+/* gemm_fp8_fused with the fused MX copy of the bf16 output (epi 4 / 8: the GELU output C2; epi 6 / 9: C):
  * mx_q [M][N] e4m3 (ld N), mx_s lane-native scales for mx_rows_padded(M) rows, bit-identical to
  * quantize_mx_bf16_ex of that bf16 output (padding rows' scales are left as given). */
 void gemm_fp8_fused_mx(void* C, void* C2, long long ldc, const void* aux, long long ldaux, const uint8_t* A,

@@ -111,6 +111,16 @@ def test_gemm_fp8_epilogues(gpu, M, N, K):
     want = acc * _gelu_grad64(xr)
     assert rel_err(v.bf16_to_f32(c5.numpy()).reshape(M, N), want) < 1e-2
     assert rel_err(cs.numpy(), 1.0 + want.sum(0)) < 1e-3
+    # 8: gelu' / gelu pair (the trainer's fc forward); 9: product with a stored gelu' + column sums
+    c6, c7 = Z(v, M * N, np.uint16), Z(v, M * N, np.uint16)
+    v.call("gemm_fp8_fused", c6, c7, N, None, 0, qa, sa, K, qw, sw, K, D(v, bias), None, M, N, K, 8)
+    assert rel_err(v.bf16_to_f32(c6.numpy()).reshape(M, N), _gelu_grad64(pre)) < 1e-2
+    assert np.array_equal(c7.numpy(), c3.numpy())
+    c8, cs2 = Z(v, M * N, np.uint16), D(v, np.ones(N, np.float32))
+    v.call("gemm_fp8_fused", c8, None, N, D(v, xb, np.uint16), N, qa, sa, K, qw, sw, K, None, cs2, M, N, K, 9)
+    want = acc * xr
+    assert rel_err(v.bf16_to_f32(c8.numpy()).reshape(M, N), want) < 1e-2
+    assert rel_err(cs2.numpy(), 1.0 + want.sum(0)) < 1e-3
 
 
 def test_gemm_fp8_quantization_error_vs_bf16(gpu):
@@ -146,14 +156,14 @@ def test_gemm_fp8_fused_mx_output(gpu, M, N, K):
     bias = D(v, rng.normal(size=N).astype(np.float32))
     nsc = int(v.lib().mx_scale_size(M, N))
     xb = D(v, v.bf16_bits(rng.normal(size=(M, N)).astype(np.float32)), np.uint16)
-    for epi in (4, 6):
+    for epi in (4, 6, 8, 9):
         c, c2 = Z(v, M * N, np.uint16), Z(v, M * N, np.uint16)
         fq, fs = Z(v, M * N, np.uint8), Z(v, nsc, np.uint8)
-        if epi == 4:
-            v.call("gemm_fp8_fused_mx", c, c2, N, None, 0, qa, sa, K, qw, sw, K, bias, None, M, N, K, 4, fq, fs)
+        if epi in (4, 8):
+            v.call("gemm_fp8_fused_mx", c, c2, N, None, 0, qa, sa, K, qw, sw, K, bias, None, M, N, K, epi, fq, fs)
             out = c2
         else:
-            v.call("gemm_fp8_fused_mx", c, None, N, xb, N, qa, sa, K, qw, sw, K, None, None, M, N, K, 6, fq, fs)
+            v.call("gemm_fp8_fused_mx", c, None, N, xb, N, qa, sa, K, qw, sw, K, None, None, M, N, K, epi, fq, fs)
             out = c
         rq, rs = Z(v, M * N, np.uint8), Z(v, nsc, np.uint8)
         v.call("quantize_mx_bf16_ex", rq, rs, out, M, N, N, N)
@@ -161,9 +171,9 @@ def test_gemm_fp8_fused_mx_output(gpu, M, N, K):
         assert np.array_equal(fq.numpy(), rq.numpy()), f"epi {epi}: e4m3 bytes differ"
         # the bf16 outputs are unchanged by the extra output
         c0, c02 = Z(v, M * N, np.uint16), Z(v, M * N, np.uint16)
-        if epi == 4:
-            v.call("gemm_fp8_fused", c0, c02, N, None, 0, qa, sa, K, qw, sw, K, bias, None, M, N, K, 4)
+        if epi in (4, 8):
+            v.call("gemm_fp8_fused", c0, c02, N, None, 0, qa, sa, K, qw, sw, K, bias, None, M, N, K, epi)
             assert np.array_equal(c02.numpy(), c2.numpy())
         else:
-            v.call("gemm_fp8_fused", c0, None, N, xb, N, qa, sa, K, qw, sw, K, None, None, M, N, K, 6)
+            v.call("gemm_fp8_fused", c0, None, N, xb, N, qa, sa, K, qw, sw, K, None, None, M, N, K, epi)
         assert np.array_equal(c0.numpy(), c.numpy())

@@ -441,6 +441,21 @@ def test_gemm_bf16_fused_epilogues(gpu, engine, M, N, K):
     want = (ar @ wkr) * _gelu_grad64(xr)
     assert rel_err(v.bf16_to_f32(c4.numpy()).reshape(M, N), want) < 1e-2
     assert rel_err(cs.numpy(), 1.0 + want.sum(0)) < 1e-2
+    # 8: C = gelu'(pre), C2 = gelu(pre) (the trainer's fc forward); 9: C = acc * aux (its fcproj
+    # dgrad, aux = the stored gelu') with the column sums
+    c5, c6 = Z(v, M * N, np.uint16), Z(v, M * N, np.uint16)
+    v.call("gemm_bf16_fused", c5, c6, N, None, 0, A, K, 1, W, K, 1, D(v, bias), None, M, N, K, 8)
+    assert rel_err(v.bf16_to_f32(c5.numpy()).reshape(M, N), _gelu_grad64(pre)) < 1e-2
+    if engine in (2, 4):  # same engine for both: the GELU output is the epi-4 one, bit for bit
+        assert np.array_equal(c6.numpy(), c2.numpy())
+    else:  # stream-K engines (3, 5) take epi 4 only; epi 8 runs on the 256x256 engine
+        assert rel_err(v.bf16_to_f32(c6.numpy()).reshape(M, N), _gelu64(pre)) < 1e-2
+    c7, cs2 = Z(v, M * N, np.uint16), D(v, np.ones(N, np.float32))
+    v.call("gemm_bf16_fused", c7, None, N, D(v, xb, np.uint16), N, A, K, 1, D(v, wkb, np.uint16), N, 0,
+           None, cs2, M, N, K, 9)
+    want = (ar @ wkr) * xr
+    assert rel_err(v.bf16_to_f32(c7.numpy()).reshape(M, N), want) < 1e-2
+    assert rel_err(cs2.numpy(), 1.0 + want.sum(0)) < 1e-2
 
 
 # ------------------------------------------------------------------ bf16 op-level family

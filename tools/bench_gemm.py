@@ -62,10 +62,10 @@ def main():
     g = [
         ("fwd_qkv", BT, 3 * C, C, 1, C, 1, C, 3),
         ("fwd_proj", BT, C, C, 1, C, 1, C, 5),
-        ("fwd_fc", BT, 4 * C, C, 1, C, 1, C, 4),
+        ("fwd_fc", BT, 4 * C, C, 1, C, 1, C, 8),  # the trainer's gelu' / gelu pair (epi 4: pre / gelu)
         ("fwd_fcproj", BT, C, 4 * C, 1, 4 * C, 1, 4 * C, 5),
         # dgrads read the transposed weight copy (K-contiguous), as the trainer does
-        ("dgrad_fcproj", BT, 4 * C, C, 1, C, 1, C, 6),
+        ("dgrad_fcproj", BT, 4 * C, C, 1, C, 1, C, 9),  # x stored gelu' + colsum (epi 6: gelu' here)
         ("dgrad_fc", BT, C, 4 * C, 1, 4 * C, 1, 4 * C, 3),
         ("dgrad_proj", BT, C, C, 1, C, 1, C, 3),
         ("dgrad_qkv", BT, C, 3 * C, 1, 3 * C, 1, 3 * C, 3),
@@ -84,18 +84,19 @@ def main():
         if var == 8:
             if epi == 2:
                 return
-            aux = aux16.ptr if epi == 6 else (aux32.ptr if epi == 5 else None)
-            L.gemm_fp8_fused(out.ptr if epi in (0, 5) else out2.ptr, out.ptr if epi == 4 else None, N, aux, N,
-                             q_act.ptr, s_act.ptr, K, q_w.ptr, s_w.ptr, K, bias.ptr if epi != 6 else None,
-                             csum.ptr if epi == 6 else None, M, N, K, epi)
+            aux = aux16.ptr if epi in (6, 9) else (aux32.ptr if epi == 5 else None)
+            L.gemm_fp8_fused(out.ptr if epi in (0, 5) else out2.ptr, out.ptr if epi in (4, 8) else None, N, aux, N,
+                             q_act.ptr, s_act.ptr, K, q_w.ptr, s_w.ptr, K, bias.ptr if epi not in (6, 9) else None,
+                             csum.ptr if epi in (6, 9) else None, M, N, K, epi)
             return
         if epi == 2:
             L.gemm_bf16_ex(out.ptr, N, act.ptr, lda, ak, act2.ptr, ldb, bk, None, None, M, N, K, 2, 0)
         else:
-            aux = aux16.ptr if epi == 6 else (aux32.ptr if epi == 5 else None)
-            L.gemm_bf16_fused(out.ptr if epi in (0, 5) else out2.ptr, out.ptr if epi == 4 else None, N,
+            aux = aux16.ptr if epi in (6, 9) else (aux32.ptr if epi == 5 else None)
+            L.gemm_bf16_fused(out.ptr if epi in (0, 5) else out2.ptr, out.ptr if epi in (4, 8) else None, N,
                               aux, N, act.ptr, lda, ak, wts.ptr, ldb, bk,
-                              bias.ptr if epi != 6 else None, csum.ptr if epi == 6 else None, M, N, K, epi)
+                              bias.ptr if epi not in (6, 9) else None, csum.ptr if epi in (6, 9) else None,
+                              M, N, K, epi)
 
     res = {}
     for rd in range(args.rounds):

@@ -113,6 +113,17 @@ __device__ __forceinline__ float gelu_grad_fast_f(float x) {
     return fmaf((2.0f * s) * x * u, fmaf(3.0f * 0.044715f, x2, 1.0f), sg);
 }
 
+// gelu_fast_f(x) and gelu_grad_fast_f(x) from one sigmoid (bit-identical to the two calls)
+__device__ __forceinline__ void gelu_pair_fast_f(float x, float& g, float& d) {
+    const float s = 0.7978845608028654f;
+    const float k = -2.0f * s * 1.4426950408889634f;
+    const float x2 = x * x;
+    const float sg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(k * fmaf(0.044715f * x, x2, x)));
+    g = x * sg;
+    const float u = fmaf(-sg, sg, sg);
+    d = fmaf((2.0f * s) * x * u, fmaf(3.0f * 0.044715f, x2, 1.0f), sg);
+}
+
 // optimizer_step (train_vit.rs:740): p -= lr*g with two roundings like the Rust reference
 // (no FMA contraction), so the fp32 update is bit-exact.
 __device__ __forceinline__ float sgd_update(float p, float g, float lr) {

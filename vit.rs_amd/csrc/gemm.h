@@ -21,7 +21,17 @@ enum Epi {
     EPI_F32_RESID = 5,   // C_f32 = acc + bias + aux_f32[m*ldaux + n]
     EPI_BF16_DGELU = 6,  // C_bf16 = acc * gelu'(aux_bf16[m*ldaux + n])
     EPI_F32_SLAB = 7,    // internal: split-K partial -> workspace slab[split][M][N] (float4 stores)
+    // the trainer's pair: the fc forward stores gelu'(pre) in place of pre, so the fcproj dgrad
+    // epilogue is one multiply instead of a second sigmoid (exp + rcp) per element
+    EPI_BF16_GELU_D = 8,  // C_bf16 = gelu'(pre), pre = acc + bias; C2_bf16 = gelu(pre)
+    EPI_BF16_MUL = 9,     // C_bf16 = acc * aux_bf16[m*ldaux + n]   (aux = a stored gelu')
 };
+// epilogues that read a bf16 aux operand / that may sum the output's columns (colsum_out)
+constexpr bool epi_aux16(int e) { return e == EPI_BF16_DGELU || e == EPI_BF16_MUL; }
+// epilogues that add the bias
+constexpr bool epi_bias(int e) { return e != EPI_F32_ATOMIC && e != EPI_F32_SLAB && !epi_aux16(e); }
+// epilogues with an MX copy of a bf16 output (gelu for the GELU pairs, the product for the aux ones)
+constexpr bool epi_mx(int e) { return e == EPI_BF16_GELU || e == EPI_BF16_GELU_D || epi_aux16(e); }
 
 struct GemmArgs {
     const void* A = nullptr;
@@ -37,7 +47,7 @@ struct GemmArgs {
     long long ldaux = 0;
     const float* bias = nullptr;
     float* dbias = nullptr;  // bf16 wgrad with an M-contig A: dbias[m] += sum_k A(m,k) (fused colsum)
-    float* colsum_out = nullptr;  // 256x256 kernel, EPI_BF16_DGELU: += column sums of the output
+    float* colsum_out = nullptr;  // EPI_BF16_DGELU / EPI_BF16_MUL: += column sums of the output
     int M = 0, N = 0, K = 0;
     int epi = EPI_F32_STORE;
     int splitk = 0;  // 0 = choose automatically (only EPI_F32_ATOMIC may split)
@@ -53,8 +63,8 @@ struct GemmArgs {
     // fp8 operands (gemm_fp8): MX scales of A and B in the lane-native layout of gemm_fp8.hip
     const void* a_scale = nullptr;
     const void* b_scale = nullptr;
-    // fused MX copy of the epilogue's bf16 output (EPI_BF16_GELU: the GELU output C2;
-    // EPI_BF16_DGELU: C), laid out as the next GEMM's A operand ([M][N] fp8, ld N, lane-native
+    // fused MX copy of the epilogue's bf16 output (EPI_BF16_GELU / _GELU_D: the GELU output C2;
+    // EPI_BF16_DGELU / _MUL: C), laid out as the next GEMM's A operand ([M][N] fp8, ld N, lane-native
     // scales for mx_rows_padded(M) rows; the padding rows' scales are the caller's zeros).  Staged
     // epilogues of the 256x256 engines only (N % 64 == 0); bit-identical to quantize_mx_bf16 of
     // the bf16 output.
@@ -71,7 +81,10 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s);
 bool gemm_bf16_supported(const GemmArgs& a);
 // engine selection for A/B measurements in one process: 1 = 128x128, 2 = 256x256 (1 WG/CU, default),
 // 4 = 256x128 (2 WG/CU); anything else = 2 (the default); debug flags: 2 = skip epilogues (main
-// loop only), 4 = 256x256 engine with LDS-DMA prefetch depth 3 instead of 2
+// loop only), 4 = 256x256 engine with LDS-DMA prefetch depth 3 instead of 2, 8 / 16 = split-K
+// sized for 1/2 / 1/4 of the CUs, 32 = generic (bounds-checked) epilogue, 64 = non-temporal
+// epilogue accesses, 128 = epilogue rows mod 256 (L2-resident output; diagnostic, wrong results),
+// 256*n (n < 64) = first-round stagger, 65536*g (g < 64) = grouped tile order
 void gemm_set_variant(int v);
 void gemm_set_debug(int flags);
 

@@ -959,6 +959,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
         for (int b = 0; b < 4; b++) fb[b] = frag<BKC, BN>(img + A_BYTES, wn * 64 + b * 16, lane);
 #pragma unroll
         for (int a = 0; a < 8; a++) fa[a] = frag<AK, BM>(img, wm * 128 + a * 16, lane);
+        if constexpr (!AK || !BKC) {  // asm transposed reads are not counted by the compiler
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (int a = 0; a < 8; a++)
 #pragma unroll
@@ -1208,6 +1213,8 @@ static void launch_bf16(const GemmArgs& a, const GemmParams& p, dim3 grid, hipSt
         VIT_CASE(EPI_BF16_GELU)
         VIT_CASE(EPI_F32_RESID)
         VIT_CASE(EPI_BF16_DGELU)
+        VIT_CASE(EPI_BF16_GELU_D)
+        VIT_CASE(EPI_BF16_MUL)
 #undef VIT_CASE
         default: set_error("gemm_bf16: unsupported epilogue %d", a.epi); return;
     }
@@ -1230,6 +1237,8 @@ static void launch_g2(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStre
         VIT_CASE(EPI_F32_RESID)
         VIT_CASE(EPI_BF16_DGELU)
         VIT_CASE(EPI_F32_SLAB)
+        VIT_CASE(EPI_BF16_GELU_D)
+        VIT_CASE(EPI_BF16_MUL)
 #undef VIT_CASE
         default: set_error("gemm_bf16: unsupported epilogue %d", a.epi); return;
     }
@@ -1252,6 +1261,8 @@ static void launch_g4(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStre
         VIT_CASE(EPI_F32_RESID)
         VIT_CASE(EPI_BF16_DGELU)
         VIT_CASE(EPI_F32_SLAB)
+        VIT_CASE(EPI_BF16_GELU_D)
+        VIT_CASE(EPI_BF16_MUL)
 #undef VIT_CASE
         default: set_error("gemm_bf16: unsupported epilogue %d", a.epi); return;
     }
@@ -1346,7 +1357,9 @@ static bool gemm_bf16_g3(const GemmArgs& a, hipStream_t s, bool whole) {
     const int ncu = num_cus();
     const long long tiles = (long long)cdiv(a.M, g3::BM) * cdiv(a.N, g3::BN);
     const int S = a.K / g3::BK;
-    if (a.epi == EPI_F32_ATOMIC || a.epi == EPI_F32_SLAB) return false;
+    // the stream-K engine has its own epilogue copies for the original six epilogues only
+    if (a.epi == EPI_F32_ATOMIC || a.epi == EPI_F32_SLAB || a.epi == EPI_BF16_GELU_D || a.epi == EPI_BF16_MUL)
+        return false;
     if ((!whole && tiles < ncu) || a.K % g3::BK || S < 2 || tiles * S >= (1LL << 31)) return false;
     char* ws = nullptr;
     if (!whole) {
@@ -1442,7 +1455,7 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s) {
     else if (!a.a_kcontig && !a.b_kcontig) launch_bf16<false, false>(a, p, grid, s);
     else launch_bf16<false, true>(a, p, grid, s);
     after_launch("gemm_bf16");
-    if (a.colsum_out && a.epi == EPI_BF16_DGELU)  // the 128x128 kernel has no fused column sums
+    if (a.colsum_out && epi_aux16(a.epi))  // the 128x128 kernel has no fused column sums
         colsum_bf16(a.colsum_out, (const bf16_t*)a.C, a.M, a.N, a.ldc, s);
 }
 

@@ -110,7 +110,7 @@ __device__ __forceinline__ bool skip_epilogue(const GemmParams& p, f32x4_t (&acc
 // epilogue for one lane's C[m][n..n+3] (n % 4 == 0, m < M, n < N)
 template <int EPI>
 __device__ __forceinline__ void epilogue(const GemmParams& p, int m, int n, f32x4_t& v) {
-    if constexpr (EPI != EPI_F32_ATOMIC && EPI != EPI_BF16_DGELU && EPI != EPI_F32_SLAB) {
+    if constexpr (epi_bias(EPI)) {
         if (p.bias) {
             const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
             v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
@@ -147,13 +147,23 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, int m, int n, f32x
     } else if constexpr (EPI == EPI_F32_SLAB) {
         float* slab = (float*)p.C + (long long)split_index(p.tiles) * p.M * p.ldc;
         *reinterpret_cast<float4*>(slab + off) = make_float4(v[0], v[1], v[2], v[3]);
-    } else if constexpr (EPI == EPI_BF16_DGELU) {
+    } else if constexpr (EPI == EPI_BF16_GELU_D) {
+        float g[4], d[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) gelu_pair_fast_f(v[j], g[j], d[j]);
+        *reinterpret_cast<uint2*>((bf16_t*)p.C + off) = make_uint2(pack_bf16x2(d[0], d[1]), pack_bf16x2(d[2], d[3]));
+        *reinterpret_cast<uint2*>((bf16_t*)p.C2 + off) = make_uint2(pack_bf16x2(g[0], g[1]), pack_bf16x2(g[2], g[3]));
+    } else if constexpr (epi_aux16(EPI)) {
         const uint2 h = *reinterpret_cast<const uint2*>((const bf16_t*)p.aux +
                                                         (long long)m * p.ldaux + n);
         const float x0 = __uint_as_float(h.x << 16), x1 = __uint_as_float(h.x & 0xffff0000u);
         const float x2 = __uint_as_float(h.y << 16), x3 = __uint_as_float(h.y & 0xffff0000u);
-        v[0] *= gelu_grad_fast_f(x0); v[1] *= gelu_grad_fast_f(x1);
-        v[2] *= gelu_grad_fast_f(x2); v[3] *= gelu_grad_fast_f(x3);
+        if constexpr (EPI == EPI_BF16_DGELU) {
+            v[0] *= gelu_grad_fast_f(x0); v[1] *= gelu_grad_fast_f(x1);
+            v[2] *= gelu_grad_fast_f(x2); v[3] *= gelu_grad_fast_f(x3);
+        } else {
+            v[0] *= x0; v[1] *= x1; v[2] *= x2; v[3] *= x3;
+        }
         *reinterpret_cast<uint2*>((bf16_t*)p.C + off) =
             make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
     }
@@ -166,7 +176,7 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, int m, int n, f32x
 template <int EPI>
 __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, float (&v)[8],
                                           float (&cs)[8], int lane = 0) {
-    if constexpr (EPI != EPI_F32_ATOMIC && EPI != EPI_BF16_DGELU && EPI != EPI_F32_SLAB) {
+    if constexpr (epi_bias(EPI)) {
         if (p.bias) {
             const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
             const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
@@ -215,13 +225,27 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, flo
         v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
         v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
         st_f32((float*)p.C + off);
-    } else if constexpr (EPI == EPI_BF16_DGELU) {
+    } else if constexpr (EPI == EPI_BF16_GELU_D) {
+        float gv[8], dv[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) gelu_pair_fast_f(v[j], gv[j], dv[j]);
+        *reinterpret_cast<uint4*>((bf16_t*)p.C + off) = pack8(dv);
+        const uint4 g8 = pack8(gv);
+        *reinterpret_cast<uint4*>((bf16_t*)p.C2 + off) = g8;
+        if (p.mx_q) mx_out8(p, m, n, g8.x, g8.y, g8.z, g8.w, lane);
+    } else if constexpr (epi_aux16(EPI)) {
         const uint4 h = *reinterpret_cast<const uint4*>((const bf16_t*)p.aux + (long long)m * p.ldaux + n);
         const uint32_t hw[4] = {h.x, h.y, h.z, h.w};
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            v[2 * j] *= gelu_grad_fast_f(__uint_as_float(hw[j] << 16));
-            v[2 * j + 1] *= gelu_grad_fast_f(__uint_as_float(hw[j] & 0xffff0000u));
+            const float lo = __uint_as_float(hw[j] << 16), hi = __uint_as_float(hw[j] & 0xffff0000u);
+            if constexpr (EPI == EPI_BF16_DGELU) {
+                v[2 * j] *= gelu_grad_fast_f(lo);
+                v[2 * j + 1] *= gelu_grad_fast_f(hi);
+            } else {
+                v[2 * j] *= lo;
+                v[2 * j + 1] *= hi;
+            }
         }
 #pragma unroll
         for (int j = 0; j < 8; j++) cs[j] += v[j];
@@ -251,7 +275,7 @@ __device__ __forceinline__ void staged_pass_interior(const GemmParams& p, const 
     const int cc_lane = cc >> 3;  // the lane's column group (lane bits 0-2): mx_out8's block lanes
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if constexpr (EPI != EPI_F32_ATOMIC && EPI != EPI_BF16_DGELU && EPI != EPI_F32_SLAB) {
+    if constexpr (epi_bias(EPI)) {
         if (p.bias) {
             const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
             const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
@@ -259,7 +283,7 @@ __device__ __forceinline__ void staged_pass_interior(const GemmParams& p, const 
             bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
         }
     }
-    constexpr bool AUX16 = EPI == EPI_BF16_DGELU;
+    constexpr bool AUX16 = epi_aux16(EPI);
     constexpr bool AUX32 = EPI == EPI_F32_RESID || EPI == EPI_F32_ACC;
     u32x4 ax[AUX16 ? 8 : (AUX32 ? 16 : 1)];
     if constexpr (AUX16) {
@@ -316,11 +340,25 @@ __device__ __forceinline__ void staged_pass_interior(const GemmParams& p, const 
             const u32x4 g8 = pack8(gv);
             epi_st16(p, (bf16_t*)p.C2 + off, g8);
             if (p.mx_q) mx_out8(p, mrow + r, n, g8[0], g8[1], g8[2], g8[3], cc_lane);
-        } else if constexpr (EPI == EPI_BF16_DGELU) {
+        } else if constexpr (EPI == EPI_BF16_GELU_D) {
+            float gv[8], dv[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) gelu_pair_fast_f(v[j], gv[j], dv[j]);
+            epi_st16(p, (bf16_t*)p.C + off, pack8(dv));
+            const u32x4 g8 = pack8(gv);
+            epi_st16(p, (bf16_t*)p.C2 + off, g8);
+            if (p.mx_q) mx_out8(p, mrow + r, n, g8[0], g8[1], g8[2], g8[3], cc_lane);
+        } else if constexpr (AUX16) {
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                v[2 * j] *= gelu_grad_fast_f(__uint_as_float(ax[it][j] << 16));
-                v[2 * j + 1] *= gelu_grad_fast_f(__uint_as_float(ax[it][j] & 0xffff0000u));
+                const float lo = __uint_as_float(ax[it][j] << 16), hi = __uint_as_float(ax[it][j] & 0xffff0000u);
+                if constexpr (EPI == EPI_BF16_DGELU) {
+                    v[2 * j] *= gelu_grad_fast_f(lo);
+                    v[2 * j + 1] *= gelu_grad_fast_f(hi);
+                } else {
+                    v[2 * j] *= lo;
+                    v[2 * j + 1] *= hi;
+                }
             }
 #pragma unroll
             for (int j = 0; j < 8; j++) cs[j] += v[j];
@@ -358,12 +396,11 @@ __device__ __forceinline__ void staged_pass(const GemmParams& p, const float* st
         } else if (n + 4 <= p.N) {  // ragged N (N % 8 == 4): the 4-wide form
             f32x4_t t = lo;
             epilogue<EPI>(p, m, n, t);
-            if constexpr (EPI == EPI_BF16_DGELU) {
-                const uint2 h = *reinterpret_cast<const uint2*>((const bf16_t*)p.aux + (long long)m * p.ldaux + n);
-                cs[0] += lo[0] * gelu_grad_fast_f(__uint_as_float(h.x << 16));
-                cs[1] += lo[1] * gelu_grad_fast_f(__uint_as_float(h.x & 0xffff0000u));
-                cs[2] += lo[2] * gelu_grad_fast_f(__uint_as_float(h.y << 16));
-                cs[3] += lo[3] * gelu_grad_fast_f(__uint_as_float(h.y & 0xffff0000u));
+            if constexpr (epi_aux16(EPI)) {  // the 4-wide form does not sum: the output it stored
+                cs[0] += t[0];
+                cs[1] += t[1];
+                cs[2] += t[2];
+                cs[3] += t[3];
             }
         }
     }
@@ -375,7 +412,7 @@ __device__ __forceinline__ bool staged_interior(const GemmParams& p, int m0, int
 // fused bias gradient of the next GEMM: column sums of the DGELU output
 template <int EPI>
 __device__ __forceinline__ void staged_colsum(const GemmParams& p, int lane, int n0, float (&cs)[8]) {
-    if constexpr (EPI == EPI_BF16_DGELU) {
+    if constexpr (epi_aux16(EPI)) {
         if (p.colsum_out) {
             const int rr = lane >> 3, cc = (lane & 7) * 8;
 #pragma unroll

@@ -306,8 +306,8 @@ bool gemm_fp8_supported(const GemmArgs& a) {
     return a.a_kcontig && a.b_kcontig && a.K % 64 == 0 && a.lda % 16 == 0 && a.ldb % 16 == 0 &&
            a.N % 4 == 0 && a.ldc % 4 == 0 && al16(a.A) && al16(a.B) && a.a_scale && a.b_scale &&
            a.epi != EPI_F32_ATOMIC && a.epi != EPI_F32_SLAB &&
-           // fused MX output: whole 32-column blocks, GELU/GELU' epilogues only (4 lanes per block)
-           (!a.mx_q || (a.mx_s && a.N % 32 == 0 && (a.epi == EPI_BF16_GELU || a.epi == EPI_BF16_DGELU)));
+           // fused MX output: whole 32-column blocks, GELU/GELU'/product epilogues only (4 lanes per block)
+           (!a.mx_q || (a.mx_s && a.N % 32 == 0 && epi_mx(a.epi)));
 }
 
 void gemm_fp8(const GemmArgs& a, hipStream_t s) {
@@ -334,6 +334,8 @@ void gemm_fp8(const GemmArgs& a, hipStream_t s) {
         VIT_CASE(EPI_BF16_GELU)
         VIT_CASE(EPI_F32_RESID)
         VIT_CASE(EPI_BF16_DGELU)
+        VIT_CASE(EPI_BF16_GELU_D)
+        VIT_CASE(EPI_BF16_MUL)
 #undef VIT_CASE
         default: set_error("gemm_fp8: unsupported epilogue %d", a.epi); return;
     }
@@ -395,8 +397,8 @@ void gemm_fp8_fused_mx(void* C, void* C2, long long ldc, const void* aux, long l
     a.A = A; a.a_scale = a_scale; a.lda = lda; a.B = B; a.b_scale = b_scale; a.ldb = ldb;
     a.bias = bias; a.colsum_out = colsum_out; a.M = M; a.N = N; a.K = K; a.epi = epi;
     a.mx_q = mx_q; a.mx_s = mx_s;
-    if (mx_q && (epi != EPI_BF16_GELU && epi != EPI_BF16_DGELU)) {
-        set_error("gemm_fp8_fused_mx: the MX output needs epi 4 (GELU) or 6 (GELU')");
+    if (mx_q && !epi_mx(epi)) {
+        set_error("gemm_fp8_fused_mx: the MX output needs epi 4 / 8 (GELU pairs) or 6 / 9 (GELU', product)");
         return;
     }
     gemm_fp8(a, stream());

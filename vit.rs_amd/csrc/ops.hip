@@ -810,7 +810,8 @@ void gemm_bf16_fused(void* C, void* C2, long long ldc, const void* aux, long lon
                      long long ldb, int b_kcontig, const float* bias, float* colsum_out, int M,
                      int N, int K, int epi) {
     VIT_REQUIRE(epi == EPI_BF16_GELU || epi == EPI_F32_RESID || epi == EPI_BF16_DGELU ||
-                    epi == EPI_F32_STORE || epi == EPI_BF16_STORE,
+                    epi == EPI_F32_STORE || epi == EPI_BF16_STORE || epi == EPI_BF16_GELU_D ||
+                    epi == EPI_BF16_MUL,
                 "gemm_bf16_fused: epi %d", epi);
     GemmArgs a;
     a.A = A; a.lda = lda; a.a_kcontig = a_kcontig != 0;

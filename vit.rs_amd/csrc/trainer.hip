@@ -219,7 +219,7 @@ struct Trainer {
 
     // ---- bf16 activations
     struct LayerActs {
-        bf16_t *ln1, *qkv, *atty, *ln2, *fch, *fchg;
+        bf16_t *ln1, *qkv, *atty, *ln2, *fchd, *fchg;  // fchd = gelu'(fc pre-activation), fchg = gelu(.)
         float *ln1_mean, *ln1_rstd, *lse, *res2, *ln2_mean, *ln2_rstd, *res3;
         // fp32-mode extras
         float *ln1f, *qkvf, *attyf, *preatt, *att, *attproj, *ln2f, *fchf, *fchgf, *fcproj;
@@ -535,7 +535,7 @@ struct Trainer {
                 a.ln2 = alloc<bf16_t>(BT * C);
                 a.ln2_mean = alloc<float>(BT);
                 a.ln2_rstd = alloc<float>(BT);
-                a.fch = alloc<bf16_t>(BT * 4 * C);
+                a.fchd = alloc<bf16_t>(BT * 4 * C);
                 a.fchg = alloc<bf16_t>(BT * 4 * C);
                 a.res3 = alloc<float>(BT * C);
             }
@@ -814,9 +814,10 @@ struct Trainer {
                                 P(P_LN2B, l), R, C, st);
                 tend();
                 GemmArgs f;
-                f.A = a.ln2 + r0 * C; f.lda = C; f.B = W(P_FCW, l); f.ldb = C; f.C = a.fch + r0 * 4 * C;
+                // fc: fchg = gelu(pre) for fcproj, fchd = gelu'(pre) for the fcproj dgrad (one sigmoid)
+                f.A = a.ln2 + r0 * C; f.lda = C; f.B = W(P_FCW, l); f.ldb = C; f.C = a.fchd + r0 * 4 * C;
                 f.C2 = a.fchg + r0 * 4 * C; f.ldc = 4 * C; f.bias = P(P_FCB, l); f.M = (int)R; f.N = 4 * C;
-                f.K = C; f.epi = EPI_BF16_GELU;
+                f.K = C; f.epi = EPI_BF16_GELU_D;
                 gemm_w(TC_FC_FWD, f, P_FCW, l, false, mb, st, false, fuse_mx);
                 GemmArgs fp;
                 fp.A = a.fchg + r0 * 4 * C; fp.lda = 4 * C; fp.B = W(P_FCPROJW, l); fp.ldb = 4 * C;
@@ -876,15 +877,15 @@ struct Trainer {
         for (int l = L - 1; l >= 0; l--) {
             LayerActs& a = la[l];
             const float* xl = l == 0 ? encoded : la[l - 1].res3;
-            // fcproj: dfch = (dres3 . fcprojw) * gelu'(fch);  fcprojw += dres3^T . fchg
+            // fcproj: dfch = (dres3 . fcprojw) * gelu'(fch) (stored as fchd);  fcprojw += dres3^T . fchg
             wgrad(TC_FCPROJ_WGRAD, rbA, C, a.fchg, 4 * C, G(P_FCPROJW, l), EV_RESA, EV_W1);
             for (int mb = 0; mb < nmb; mb++) {
                 const long long r0 = mb * R;
                 after_wgrad(EV_W2, ms[mb]);  // the previous layer's fc wgrad has read dfch
                 GemmArgs d1;
                 d1.A = rbA + r0 * C; d1.lda = C; dgrad_b(d1, P_FCPROJW, l, C, 4 * C);
-                d1.C = dfch + r0 * 4 * C; d1.ldc = 4 * C; d1.aux = a.fch + r0 * 4 * C; d1.ldaux = 4 * C;
-                d1.M = (int)R; d1.N = 4 * C; d1.K = C; d1.epi = EPI_BF16_DGELU;
+                d1.C = dfch + r0 * 4 * C; d1.ldc = 4 * C; d1.aux = a.fchd + r0 * 4 * C; d1.ldaux = 4 * C;
+                d1.M = (int)R; d1.N = 4 * C; d1.K = C; d1.epi = EPI_BF16_MUL;
                 d1.colsum_out = G(P_FCB, l);
                 gemm_w(TC_FCPROJ_DGRAD, d1, P_FCPROJW, l, true, mb, ms[mb], false, fuse_mx);
             }
