@@ -84,7 +84,8 @@ bool gemm_bf16_supported(const GemmArgs& a);
 // loop only), 4 = 256x256 engine with LDS-DMA prefetch depth 3 instead of 2, 8 / 16 = split-K
 // sized for 1/2 / 1/4 of the CUs, 32 = generic (bounds-checked) epilogue, 64 = non-temporal
 // epilogue accesses, 128 = epilogue rows mod 256 (L2-resident output; diagnostic, wrong results),
-// 256*n (n < 64) = first-round stagger, 65536*g (g < 64) = grouped tile order
+// 256*n (n < 64) = first-round stagger, 65536*g (g < 64) = grouped tile order, 1<<23 = split-K
+// weight gradients on the 256x256 engine (default: 256x128)
 void gemm_set_variant(int v);
 void gemm_set_debug(int flags);
 

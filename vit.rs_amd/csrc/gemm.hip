@@ -315,6 +315,26 @@ __device__ __forceinline__ void wait_vm(int n) {
         default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     }
 }
+// vector-memory operations one wave issues in direct_epilogue<EPI> on an interior tile (16-B aux
+// loads, 16-B stores, colsum atomics); checked against the disassembly (global_load / _store /
+// _atomic between the persistent kernel's prologue issue and its loop back-edge)
+template <int EPI>
+__host__ __device__ constexpr int direct_vm_ops(bool colsum) {
+    return EPI == EPI_BF16_STORE ? 16
+         : (EPI == EPI_BF16_GELU || EPI == EPI_BF16_GELU_D || EPI == EPI_F32_STORE) ? 32
+         : (EPI == EPI_F32_RESID || EPI == EPI_F32_ACC) ? 64
+         : epi_aux16(EPI) ? 32 + (colsum ? 16 : 0)
+         : 64;
+}
+// s_waitcnt vmcnt(n), n <= 63 a runtime value from a small set (literal immediates)
+__device__ __forceinline__ void wait_vm_any(int n) {
+    switch (n) {
+#define VIT_W(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+        VIT_W(20) VIT_W(36) VIT_W(52) VIT_W(63)
+#undef VIT_W
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+}
 template <bool AK, bool BKC, int EPI, int DEPTH>
 __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
     constexpr int NS = DEPTH + 2;
@@ -448,6 +468,135 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     staged_epilogue<EPI>(p, acc, smem + wave * STG_WAVE_BYTES, lane, tm0 + wm * 128, tn0 + wn * 64);
+}
+
+// Persistent form: one workgroup per CU walks the launch's tiles in the one-tile-per-workgroup
+// launch's XCD-aware order (tile v of workgroup b is v = b + k*gridDim.x, gridDim.x a multiple of
+// 8, so v % 8 is still b's XCD).  After a tile's main loop the NEXT tile's first DEPTH K-steps go
+// into the ring BEFORE this tile's epilogue, which runs LDS-free (direct_epilogue): the
+// prologue's DMA latency and the workgroup relaunch overlap the epilogue's stores.  The first
+// wait of the next tile is vmcnt(0) (vmcnt counts the epilogue's stores too).  Whole-K, N % 256
+// == 0, no split-K / bias-gradient launches.
+template <bool AK, bool BKC, int EPI>
+__global__ __launch_bounds__(NT, 1) void gemm_kernel_p(GemmParams p) {
+    constexpr int DEPTH = 2, NS = DEPTH + 2;
+    __shared__ __attribute__((aligned(1024))) char smem[NS * SLOT_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int ntm = cdiv(p.M, BM), ntn = cdiv(p.N, BN), ntiles = ntm * ntn;
+    const int nk = p.K / BK;
+    const bf16_t* A = (const bf16_t*)p.A;
+    const bf16_t* B = (const bf16_t*)p.B;
+    const bool lagging = wave >= 4;
+    auto slot_of = [&](int st) { return smem + (st % NS) * SLOT_BYTES; };
+    auto tile_of = [&](int v, int& tm0, int& tn0) {
+        const int wg = xcd_remap(v, ntiles);
+        tm0 = (wg / ntn) * BM;
+        tn0 = (wg % ntn) * BN;
+    };
+    auto issue_a = [&](int tm0, int st) {
+        if (st < nk) stage<AK>(A, p.lda, tm0, p.M, st * BK, slot_of(st), wave, lane);
+    };
+    auto issue_b = [&](int tn0, int st) {
+        if (st < nk) stage<BKC>(B, p.ldb, tn0, p.N, st * BK, slot_of(st) + IMG_BYTES, wave, lane);
+    };
+    auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    f32x4_t acc[8][4];
+    auto mfma_half = [&](int half, const bf16x8_t (&fa)[4], const bf16x8_t (&fb)[4]) {
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+                acc[half * 4 + a][b] =
+                    __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[b], fa[a], acc[half * 4 + a][b], 0, 0, 0);
+    };
+    int v = blockIdx.x;
+    if (v >= ntiles || nk <= 0) return;
+    int tm0, tn0;
+    tile_of(v, tm0, tn0);
+#pragma unroll
+    for (int st = 0; st < DEPTH; st++) { issue_a(tm0, st); issue_b(tn0, st); }
+    // memory operations a wave issued after the current tile's step-0 pieces that may stay in
+    // flight at its first wait: step 1's pieces (4), and after the first tile the previous tile's
+    // epilogue (vmcnt counts loads, stores, atomics and LDS-DMA together in issue order,
+    // MI355X_MICROARCH.md); -1 = wait for everything (a ragged previous tile skips stores)
+    int younger = 4 * (min(DEPTH, nk) - 1);
+    for (;;) {
+        if (younger == 0 || younger == 4) wait_vm(younger);
+        else if (younger > 0) wait_vm_any(younger);
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar();
+        if (lagging) {
+            __builtin_amdgcn_s_setprio(1);
+            bar();
+        }
+#pragma unroll
+        for (int a = 0; a < 8; a++)
+#pragma unroll
+            for (int b = 0; b < 4; b++) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        bf16x8_t fb[4], alo[4], ahi[4];
+        for (int kt = 0; kt < nk; kt++) {
+            const char* img = slot_of(kt);
+#pragma unroll
+            for (int b = 0; b < 4; b++) fb[b] = frag<BKC>(img + IMG_BYTES, wn * 64 + b * 16, lane);
+#pragma unroll
+            for (int a = 0; a < 4; a++) alo[a] = frag<AK>(img, wm * 128 + a * 16, lane);
+            issue_a(tm0, kt + DEPTH);
+            bar();
+            mfma_half(0, alo, fb);
+            bar();
+#pragma unroll
+            for (int a = 0; a < 4; a++) ahi[a] = frag<AK>(img, wm * 128 + (4 + a) * 16, lane);
+            wait_vm(4 * max(0, min(kt + DEPTH, nk) - (kt + 2)) + (kt + DEPTH < nk ? 2 : 0));
+            issue_b(tn0, kt + DEPTH);
+            bar();
+            mfma_half(1, ahi, fb);
+            bar();
+        }
+        if (!lagging) bar();  // balance the stagger barrier: every wave is past its last ring read
+        __builtin_amdgcn_s_setprio(0);
+        // this lane's bias columns (older than the next prologue's DMA)
+        float bv[2][8];
+        const int m0 = tm0 + wm * 128, n0 = tn0 + wn * 64;
+#pragma unroll
+        for (int pr = 0; pr < 2; pr++)
+#pragma unroll
+            for (int j = 0; j < 8; j++) bv[pr][j] = 0.f;
+        if constexpr (epi_bias(EPI)) {
+            if (p.bias) {
+#pragma unroll
+                for (int pr = 0; pr < 2; pr++) {
+                    const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n0 + pr * 32 + direct_col(lane));
+                    const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n0 + pr * 32 + direct_col(lane) + 4);
+                    bv[pr][0] = b0.x; bv[pr][1] = b0.y; bv[pr][2] = b0.z; bv[pr][3] = b0.w;
+                    bv[pr][4] = b1.x; bv[pr][5] = b1.y; bv[pr][6] = b1.z; bv[pr][7] = b1.w;
+                }
+            }
+        }
+        const int vn = v + gridDim.x;
+        int tm1 = 0, tn1 = 0;
+        __builtin_amdgcn_sched_barrier(0);  // bias loads stay older than the next prologue
+        if (vn < ntiles) {
+            tile_of(vn, tm1, tn1);
+#pragma unroll
+            for (int st = 0; st < DEPTH; st++) { issue_a(tm1, st); issue_b(tn1, st); }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // and every epilogue access younger than it
+        const bool ragged = tm0 + BM > p.M;  // workgroup-uniform; rows >= M skip their stores
+        if (!skip_epilogue(p, acc)) direct_epilogue<EPI>(p, acc, bv, lane, m0, n0);
+        younger = (ragged || p.no_epi) ? -1 : min(63, 4 * (min(DEPTH, nk) - 1) + direct_vm_ops<EPI>(p.colsum_out != nullptr));
+        if (vn >= ntiles) break;
+        v = vn;
+        tm0 = tm1;
+        tn0 = tn1;
+    }
 }
 }  // namespace g2
 
@@ -1107,10 +1256,11 @@ __global__ __launch_bounds__(256) void slab_reduce_k(float* __restrict__ C, long
 // engine selection (gemm_bf16_set_variant; default from VIT_GEMM, else 2):
 //   1 = 128x128 register-staged, 2 = 256x256 one workgroup per CU, 3 = 2 as stream-K persistent
 //   (launches with >= 1 tile per CU; the rest, e.g. split-K wgrad, take 2), 4 = 256x128 two per CU,
-//   5 = 2 as a persistent launch over whole tiles (no hand-offs; split-K wgrad takes 2)
+//   5 = 2 as a persistent launch over whole tiles (no hand-offs; split-K wgrad takes 2),
+//   6 = 2 persistent with the next tile's prologue under an LDS-free epilogue (g2::gemm_kernel_p)
 static int g_variant = -1;
 static int g_debug_flags = 0;
-static bool known_variant(int v) { return v == 1 || v == 3 || v == 4 || v == 5; }
+static bool known_variant(int v) { return v == 1 || v == 3 || v == 4 || v == 5 || v == 6; }
 static int gemm_variant() {
     if (g_variant < 0) {
         const char* e = getenv("VIT_GEMM");
@@ -1237,6 +1387,24 @@ static void launch_g2(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStre
         VIT_CASE(EPI_F32_RESID)
         VIT_CASE(EPI_BF16_DGELU)
         VIT_CASE(EPI_F32_SLAB)
+        VIT_CASE(EPI_BF16_GELU_D)
+        VIT_CASE(EPI_BF16_MUL)
+#undef VIT_CASE
+        default: set_error("gemm_bf16: unsupported epilogue %d", a.epi); return;
+    }
+}
+
+template <bool AK, bool BKC>
+static void launch_g2p(const GemmArgs& a, const GemmParams& p, int P, hipStream_t s) {
+    switch (a.epi) {
+#define VIT_CASE(E) \
+    case E: g2::gemm_kernel_p<AK, BKC, E><<<P, g2::NT, 0, s>>>(p); break;
+        VIT_CASE(EPI_F32_STORE)
+        VIT_CASE(EPI_F32_ACC)
+        VIT_CASE(EPI_BF16_STORE)
+        VIT_CASE(EPI_BF16_GELU)
+        VIT_CASE(EPI_F32_RESID)
+        VIT_CASE(EPI_BF16_DGELU)
         VIT_CASE(EPI_BF16_GELU_D)
         VIT_CASE(EPI_BF16_MUL)
 #undef VIT_CASE
@@ -1399,8 +1567,8 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s) {
     // split-K weight gradients (M/N-contiguous operands, K = the token count) run on the 256x128
     // two-per-CU engine: 3-9 % faster than 256x256 on every ViT-B/16 wgrad shape (r02,
     // tools/bench_gemm.py), the other GEMMs are faster on 256x256
-    if (gemm_variant() == 2 && a.epi == EPI_F32_ATOMIC && !a.a_kcontig && !a.b_kcontig &&
-        a.K % g4::KTILE == 0 && a.M >= 256 && a.N >= 128 && a.N % 4 == 0 && !getenv("VIT_WGRAD_G2") &&
+    if ((gemm_variant() == 2 || gemm_variant() == 6) && a.epi == EPI_F32_ATOMIC && !a.a_kcontig && !a.b_kcontig &&
+        a.K % g4::KTILE == 0 && a.M >= 256 && a.N >= 128 && a.N % 4 == 0 && !(g_debug_flags & (1 << 23)) &&
         (a.splitk > 0 || !a.ws ||
          (size_t)choose_split_g4(cdiv(a.M, g4::BM) * cdiv(a.N, g4::BN), a.K / g4::KTILE) * a.M * a.N * sizeof(float) <=
              a.ws_bytes)) {
@@ -1429,6 +1597,18 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s) {
         }
         GemmParams p = make_gemm_params(b, kchunk);
         p.tiles = tiles;
+        // persistent form (variant 6): whole-K launches with at least two tiles per CU
+        const int ncu = num_cus();
+        if (gemm_variant() == 6 && split == 1 && a.epi != EPI_F32_ATOMIC && !a.dbias && a.N % 256 == 0 &&
+            tiles >= 2 * ncu && ncu % 8 == 0) {
+            const int P = ncu;
+            if (a.a_kcontig && a.b_kcontig) launch_g2p<true, true>(b, p, P, s);
+            else if (a.a_kcontig && !a.b_kcontig) launch_g2p<true, false>(b, p, P, s);
+            else if (!a.a_kcontig && !a.b_kcontig) launch_g2p<false, false>(b, p, P, s);
+            else launch_g2p<false, true>(b, p, P, s);
+            after_launch("gemm_bf16_256_persistent");
+            return;
+        }
         dim3 grid(tiles, split);
         if (a.a_kcontig && a.b_kcontig) launch_g2<true, true>(b, p, grid, s);
         else if (a.a_kcontig && !a.b_kcontig) launch_g2<true, false>(b, p, grid, s);
