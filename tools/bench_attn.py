@@ -20,6 +20,10 @@ def main():
     ap.add_argument("--hs", type=int, default=64)
     ap.add_argument("--generic", action="store_true", help="force the generic VALU kernels")
     ap.add_argument("--colsum", action="store_true", help="backward with the fused qkv-bias gradient (trainer form)")
+    ap.add_argument("--env-ab", default=None,
+                    help="A/B of backward environments in one process, interleaved round by round, e.g. "
+                         "'VIT_ATTN_BWD_NOPAD=0|VIT_ATTN_BWD_NOPAD=1' (median of --rounds)")
+    ap.add_argument("--rounds", type=int, default=5)
     args = ap.parse_args()
     if args.generic:
         os.environ["VIT_ATTN_GENERIC"] = "1"
@@ -40,6 +44,28 @@ def main():
            (lambda: L.attention_backward_fused_bf16(dqkv.ptr, dout.ptr, qkv.ptr, out.ptr, lse.ptr, B, T, C, NH)))
     e0, e1 = L.vit_event_create(), L.vit_event_create()
     fl_f = 4.0 * B * T * T * C
+    if args.env_ab:
+        confs = args.env_ab.split("|")
+        res = {c: [] for c in confs}
+        for _ in range(args.rounds):
+            for c in confs:
+                for kv in filter(None, c.split(",")):
+                    k, val = kv.split("=")
+                    os.environ[k] = val
+                for _ in range(2):
+                    bwd()
+                L.vit_sync()
+                L.vit_event_record(e0)
+                for _ in range(args.iters):
+                    bwd()
+                L.vit_event_record(e1)
+                res[c].append(L.vit_event_elapsed_ms(e0, e1) / args.iters)
+                vit.check(c)
+        for c in confs:
+            ms = float(np.median(res[c]))
+            print(f"attention bwd [{c}] B={B} T={T} NH={NH} hs={args.hs}: median {ms * 1e3:8.1f} us "
+                  f"min {min(res[c]) * 1e3:8.1f} us  {2 * fl_f / ms / 1e9:7.1f} TFLOP/s", flush=True)
+        return
     for name, fn, fl in (
             ("fwd", lambda: L.attention_forward_fused_bf16(out.ptr, lse.ptr, qkv.ptr, B, T, C, NH), fl_f),
             ("bwd" + ("+colsum" if args.colsum else ""), bwd, 2 * fl_f)):
