@@ -46,25 +46,28 @@ def main():
     fl_f = 4.0 * B * T * T * C
     if args.env_ab:
         confs = args.env_ab.split("|")
-        res = {c: [] for c in confs}
+        fwd = lambda: L.attention_forward_fused_bf16(out.ptr, lse.ptr, qkv.ptr, B, T, C, NH)  # noqa: E731
+        res = {(c, d): [] for c in confs for d in ("fwd", "bwd")}
         for _ in range(args.rounds):
             for c in confs:
                 for kv in filter(None, c.split(",")):
                     k, val = kv.split("=")
                     os.environ[k] = val
-                for _ in range(2):
-                    bwd()
-                L.vit_sync()
-                L.vit_event_record(e0)
-                for _ in range(args.iters):
-                    bwd()
-                L.vit_event_record(e1)
-                res[c].append(L.vit_event_elapsed_ms(e0, e1) / args.iters)
-                vit.check(c)
-        for c in confs:
-            ms = float(np.median(res[c]))
-            print(f"attention bwd [{c}] B={B} T={T} NH={NH} hs={args.hs}: median {ms * 1e3:8.1f} us "
-                  f"min {min(res[c]) * 1e3:8.1f} us  {2 * fl_f / ms / 1e9:7.1f} TFLOP/s", flush=True)
+                for d, fn in (("fwd", fwd), ("bwd", bwd)):
+                    for _ in range(2):
+                        fn()
+                    L.vit_sync()
+                    L.vit_event_record(e0)
+                    for _ in range(args.iters):
+                        fn()
+                    L.vit_event_record(e1)
+                    res[(c, d)].append(L.vit_event_elapsed_ms(e0, e1) / args.iters)
+                    vit.check(c)
+        for (c, d), v in res.items():
+            ms = float(np.median(v))
+            fl = fl_f if d == "fwd" else 2 * fl_f
+            print(f"attention {d} [{c}] B={B} T={T} NH={NH} hs={args.hs}: median {ms * 1e3:8.1f} us "
+                  f"min {min(v) * 1e3:8.1f} us  {fl / ms / 1e9:7.1f} TFLOP/s", flush=True)
         return
     for name, fn, fl in (
             ("fwd", lambda: L.attention_forward_fused_bf16(out.ptr, lse.ptr, qkv.ptr, B, T, C, NH), fl_f),
