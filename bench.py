@@ -378,7 +378,10 @@ def main():
             d = gemms[dom]
             avg_ms = d["ms"] / d["calls"]
             ach = d["flops"] / d["calls"] / (avg_ms * 1e-3) / 1e12
-            traffic, tsrc = pmc_traffic(dom)
+            # the committed PMC passes profile the default workload (ViT-B/16 bf16, B=256); other
+            # models / dtypes have no traffic measurement of their own
+            traffic, tsrc = (pmc_traffic(dom) if args.model == "vit_b16" and args.dtype == "bf16"
+                             and B == 256 else (None, None))
             return {"kernel": dom, "bound": "mfma", "achieved": round(ach, 1), "peak": peak,
                     "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                     "traffic": round(traffic) if traffic else None, "traffic_unit": "bytes/launch",
