@@ -182,8 +182,11 @@ void gemm_fp8_fused_mx(void* C, void* C2, long long ldc, const void* aux, long l
                        const uint8_t* a_scale, long long lda, const uint8_t* B, const uint8_t* b_scale,
                        long long ldb, const float* bias, float* colsum_out, int M, int N, int K, int epi,
                        uint8_t* mx_q, uint8_t* mx_s);
-/* tools: GEMM engine selection (1 = 128x128, 2 = 256x256 one workgroup per CU, the default,
- * 4 = 256x128 two per CU) and diagnostics (flag 2: skip epilogues, main-loop timing only) */
+/* tools: GEMM engine selection (1 = 128x128, 2 = 256x256 one workgroup per CU, the default, with
+ * the split-K weight gradients on 256x128; 3 / 5 = stream-K / whole-tile persistent forms of 2;
+ * 4 = 256x128 two per CU; 6 = 2 persistent with the next tile's prologue under an LDS-free
+ * epilogue) and diagnostics (flag 2: skip epilogues, main-loop timing only; the other flags:
+ * vit.rs_amd/csrc/gemm.h) */
 void gemm_bf16_set_variant(int variant);
 void gemm_bf16_set_debug(int flags);
 void convert_f32_to_bf16(uint16_t* out, const float* inp, long long n);
