@@ -513,21 +513,39 @@ bool attn_fused_supported(int T, int C, int NH) {
 //            part[(r*NH + h)][s*HS + d] -> scratch[chunk][s*C + h*HS + d]
 //   final_k: out[j] += sum over chunks of scratch[chunk][j] (fixed order; one atomicAdd per j, as the
 //            micro-batches' launches add into one bias concurrently)
+// stage 1 of the deterministic qkv-bias column sums: workgroup (section*head, chunk) sums its
+// chunk of the R partial rows for the head's HS columns.  16-B loads: HS/4 lanes cover a row
+// segment, 256/(HS/4) rows are in flight per iteration, four independent accumulators per lane.
 __global__ __launch_bounds__(256) void attn_colsum_part_k(float* __restrict__ scratch, const float* __restrict__ part,
                                                           int R, int NH, int C, int HS) {
-    __shared__ float red[256];
+    __shared__ float4 red[256];
     const int sh = blockIdx.x, sct = sh / NH, h = sh - sct * NH, ch = blockIdx.y, nch = gridDim.y;
-    const int nb = 256 / HS, d = threadIdx.x % HS, lb = threadIdx.x / HS;
+    const int lpr = HS / 4, nb = 256 / lpr, d4 = threadIdx.x % lpr, lb = threadIdx.x / lpr;
     const int r0 = (int)((long long)R * ch / nch), r1 = (int)((long long)R * (ch + 1) / nch);
-    float t = 0.f;
-    if (lb < nb)
-        for (int r = r0 + lb; r < r1; r += nb) t += part[((long long)r * NH + h) * 3 * HS + sct * HS + d];
-    red[threadIdx.x] = t;
+    float4 t[4] = {};
+    const long long rs = (long long)NH * 3 * HS;  // floats between consecutive partial rows
+    const float* base = part + (long long)h * 3 * HS + sct * HS + 4 * d4;
+    int r = lb < nb ? r0 + lb : r1;  // lanes past nb * lpr (HS = 80, 96) take no rows
+    for (; r + 3 * nb < r1; r += 4 * nb)
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const float4 v = *reinterpret_cast<const float4*>(base + (long long)(r + u * nb) * rs);
+            t[u].x += v.x; t[u].y += v.y; t[u].z += v.z; t[u].w += v.w;
+        }
+    for (; r < r1; r += nb) {
+        const float4 v = *reinterpret_cast<const float4*>(base + (long long)r * rs);
+        t[0].x += v.x; t[0].y += v.y; t[0].z += v.z; t[0].w += v.w;
+    }
+    red[threadIdx.x] = make_float4(t[0].x + t[1].x + t[2].x + t[3].x, t[0].y + t[1].y + t[2].y + t[3].y,
+                                   t[0].z + t[1].z + t[2].z + t[3].z, t[0].w + t[1].w + t[2].w + t[3].w);
     __syncthreads();
     if (lb == 0) {
-        float a = 0.f;
-        for (int j = 0; j < nb; j++) a += red[j * HS + d];
-        scratch[(long long)ch * 3 * C + sct * C + h * HS + d] = a;
+        float4 a = red[d4];
+        for (int j = 1; j < nb; j++) {
+            const float4 b = red[j * lpr + d4];
+            a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+        }
+        *reinterpret_cast<float4*>(scratch + (long long)ch * 3 * C + sct * C + h * HS + 4 * d4) = a;
     }
 }
 __global__ __launch_bounds__(256) void attn_colsum_final_k(float* __restrict__ out, const float* __restrict__ scratch,
@@ -627,7 +645,7 @@ void attn_backward_fused(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, co
     if (!rows) { set_error("fused attention backward: no kernel for T=%d head size %d", T, HS); return; }
     after_launch("attention_backward_fused");
     if (dqkv_colsum) {  // the partial rows are laid out as B*rows batch entries; the chunk sums follow them
-        const int nch = std::min(32, B);
+        const int nch = std::min(8, B);
         float* scratch = part + (size_t)B * rows * NH * 3 * HS;
         attn_colsum_part_k<<<dim3(3 * NH, nch), 256, 0, s>>>(scratch, part, B * rows, NH, C, HS);
         attn_colsum_final_k<<<cdiv(3 * C, 256), 256, 0, s>>>(dqkv_colsum, scratch, nch, 3 * C);
