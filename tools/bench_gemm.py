@@ -95,8 +95,7 @@ def main():
             aux = aux16.ptr if epi in (6, 9) else (aux32.ptr if epi == 5 else None)
             L.gemm_bf16_fused(out.ptr if epi in (0, 5) else out2.ptr, out.ptr if epi in (4, 8) else None, N,
                               aux, N, act.ptr, lda, ak, wts.ptr, ldb, bk,
-                              bias.ptr if epi not in (6, 9) else None,
-                              csum.ptr if epi in (6, 9) and not os.environ.get("NO_COLSUM") else None,
+                              bias.ptr if epi not in (6, 9) else None, csum.ptr if epi in (6, 9) else None,
                               M, N, K, epi)
 
     res = {}
