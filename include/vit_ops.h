@@ -44,6 +44,24 @@ int vit_memcpy_h2d(void* dst, const void* src, size_t bytes);
 int vit_memcpy_d2h(void* dst, const void* src, size_t bytes);
 int vit_memcpy_d2d(void* dst, const void* src, size_t bytes);
 int vit_memset(void* dst, int value, size_t bytes);
+/* launch counters: how many launches of each kernel family ran since the last reset (process-wide,
+ * every thread and stream).  GEMM families are indexed base + epilogue (epi < 16, gemm.h Epi). */
+enum {
+    VIT_HIT_GEMM_128 = 0,            /* bf16 128x128 register-staged (small / ragged shapes) */
+    VIT_HIT_GEMM_256x256 = 16,       /* bf16 256x256 LDS-DMA engine, one workgroup per CU */
+    VIT_HIT_GEMM_256x128 = 32,       /* bf16 256x128 LDS-DMA engine, two workgroups per CU */
+    VIT_HIT_GEMM_FP8 = 48,           /* MXFP8 256x256 engine */
+    VIT_HIT_GEMM_F32 = 64,           /* fp32 MFMA (parity path) */
+    VIT_HIT_SPLITK_REDUCE = 80,      /* split-K slab reduction (separate launch) */
+    VIT_HIT_ATTN_FWD_MFMA = 81,      /* fused MFMA attention forward */
+    VIT_HIT_ATTN_BWD_PERSISTENT = 82,/* persistent one-pass MFMA attention backward */
+    VIT_HIT_ATTN_BWD_ONEPASS = 83,   /* one-pass backward, one workgroup per (b,h) */
+    VIT_HIT_ATTN_BWD_PAIR = 84,      /* paired-role backward */
+    VIT_HIT_ATTN_GENERIC = 85,       /* generic VALU attention (T past the MFMA kernels' LDS) */
+    VIT_HIT_COUNT = 96
+};
+int vit_kernel_hits(long long* out, int n); /* copies min(n, VIT_HIT_COUNT); returns VIT_HIT_COUNT */
+void vit_kernel_hits_reset(void);
 /* events for per-kernel timing on the current stream */
 void* vit_event_create(void);
 void vit_event_destroy(void* ev);
@@ -182,11 +200,9 @@ void gemm_fp8_fused_mx(void* C, void* C2, long long ldc, const void* aux, long l
                        const uint8_t* a_scale, long long lda, const uint8_t* B, const uint8_t* b_scale,
                        long long ldb, const float* bias, float* colsum_out, int M, int N, int K, int epi,
                        uint8_t* mx_q, uint8_t* mx_s);
-/* tools: GEMM engine selection (1 = 128x128, 2 = 256x256 one workgroup per CU, the default, with
- * the split-K weight gradients on 256x128; 3 / 5 = stream-K / whole-tile persistent forms of 2;
- * 4 = 256x128 two per CU; 6 = 2 persistent with the next tile's prologue under an LDS-free
- * epilogue) and diagnostics (flag 2: skip epilogues, main-loop timing only; the other flags:
- * vit.rs_amd/csrc/gemm.h) */
+/* tools: GEMM engine selection (1 = 128x128 everywhere, 2 = production: 256x256 one workgroup per
+ * CU with the split-K weight gradients on 256x128, 4 = 256x128 two per CU everywhere) and
+ * diagnostics (flag 2: skip epilogues, main-loop timing only) */
 void gemm_bf16_set_variant(int variant);
 void gemm_bf16_set_debug(int flags);
 void convert_f32_to_bf16(uint16_t* out, const float* inp, long long n);

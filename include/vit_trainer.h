@@ -89,6 +89,15 @@ int vit_trainer_get_logits(vit_trainer_t* t, float* host_logits); /* [batch, num
 int vit_trainer_sync(vit_trainer_t* t);
 void* vit_trainer_stream(vit_trainer_t* t);
 
+/* device gradient-arena layout (host-only, no GPU needed): tensor_off [20 * num_layers] element
+ * offsets of tensor ti (canonical order), layer l at [ti * num_layers + l] (unlayered tensors:
+ * l = 0, the other entries 0); chunk_off [num_layers + 3] boundaries of the all-reduce chunks in
+ * backward's completion order (0 = head + final LN, 1..L = layers L-1..0, L+1 = embedding);
+ * arena_elems = arena size (with 64-element alignment padding).  Returns the chunk count (L + 2),
+ * -1 on a bad config.  Any pointer may be NULL. */
+int vit_layout_query(const vit_config_t* cfg, long long* tensor_off, long long* chunk_off,
+                     long long* arena_elems);
+
 /* ---- data parallelism over RCCL (one process per GPU) ---- */
 int vit_dp_unique_id_size(void);
 int vit_dp_get_unique_id(char* out);   /* rank 0 creates; broadcast the bytes out of band */

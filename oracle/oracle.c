@@ -10,6 +10,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #if defined(ORACLE_F64)
 #define R_EXP exp
@@ -27,14 +30,35 @@
 
 typedef int64_t i64;
 
+/* Threading (test infrastructure speed only): loops are split over OpenMP threads only along
+ * indices whose outputs are disjoint, and every output element keeps the reference's sequential
+ * accumulation order, so results are bitwise identical for any thread count.
+ * ref_set_num_threads(1) gives the single-thread reference timing (bench.py cpu_baseline). */
+void ref_set_num_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}
+int ref_get_num_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
 /* train_vit.rs:376-382 */
 void ref_residual_forward(real* out, const real* inp1, const real* inp2, int N) {
+#pragma omp parallel for schedule(static)
     for (i64 i = 0; i < N; i++) out[i] = inp1[i] + inp2[i];
 }
 
 /* train_vit.rs:384-398 — out[bt,o] = b[o] + sum_i inp[bt,i] * W[o,i], sequential in i */
 void ref_matmul_forward(real* out, const real* inp, const real* weight, const real* bias,
                         int B, int T, int C, int OC) {
+#pragma omp parallel for schedule(static)
     for (i64 bt = 0; bt < (i64)B * T; bt++) {
         for (i64 o = 0; o < OC; o++) {
             real val = bias ? bias[o] : (real)0;
@@ -57,6 +81,7 @@ static void attention_forward_impl(real* out, real* preatt, real* att, const rea
     const i64 C3 = (i64)C * 3;
     const int hs = C / NH;
     const real scale = (real)1.0 / R_SQRT((real)hs);
+#pragma omp parallel for schedule(static)
     for (i64 bth = 0; bth < (i64)B * T * NH; bth++) {
         const i64 b = bth / ((i64)T * NH), t = (bth / NH) % T, h = bth % NH;
         const real* query_t = inp + (b * T + t) * C3 + h * hs;
@@ -105,6 +130,7 @@ void ref_attention_forward_causal(real* out, real* preatt, real* att, const real
 void ref_layernorm_forward(real* out, real* mean, real* rstd, const real* inp,
                            const real* weight, const real* bias, int B, int T, int C) {
     const real eps = (real)1e-5;
+#pragma omp parallel for schedule(static)
     for (i64 bt = 0; bt < (i64)B * T; bt++) {
         const real* x = inp + bt * C;
         real m = 0;
@@ -133,6 +159,7 @@ static real gelu_s(void) { return R_SQRT((real)2.0 / (real)3.1415926535897932384
 /* train_vit.rs:482-491 */
 void ref_gelu_forward(real* out, const real* inp, int N) {
     const real s = gelu_s();
+#pragma omp parallel for schedule(static)
     for (i64 i = 0; i < N; i++) {
         real x = inp[i];
         real cube = (real)0.044715 * x * x * x;
@@ -166,6 +193,7 @@ void ref_crossentropy_forward(real* losses, const real* probs, const int* target
 
 /* train_vit.rs:521-528 */
 void ref_residual_backward(real* dinp1, real* dinp2, const real* dout, int N) {
+#pragma omp parallel for schedule(static)
     for (i64 i = 0; i < N; i++) {
         dinp1[i] += dout[i];
         dinp2[i] += dout[i];
@@ -177,6 +205,7 @@ void ref_matmul_backward(real* dinp, real* dweight, real* dbias, const real* dou
                          const real* inp, const real* weight, int B, int T, int C, int OC) {
     const i64 BT = (i64)B * T;
     if (dinp) {
+#pragma omp parallel for schedule(static)
         for (i64 bt = 0; bt < BT; bt++) {
             for (i64 o = 0; o < OC; o++) {
                 const real d = dout[bt * OC + o];
@@ -186,6 +215,7 @@ void ref_matmul_backward(real* dinp, real* dweight, real* dbias, const real* dou
             }
         }
     }
+#pragma omp parallel for schedule(dynamic, 1)
     for (i64 o = 0; o < OC; o++) {
         for (i64 bt = 0; bt < BT; bt++) {
             const real d = dout[bt * OC + o];
@@ -211,8 +241,12 @@ void ref_attention_backward(real* dinp, real* dpreatt, real* datt, const real* d
     if (!dpreatt) dpreatt = own_dpre = (real*)calloc((size_t)n_scr, sizeof(real));
     if (!datt) datt = own_datt = (real*)calloc((size_t)n_scr, sizeof(real));
 
-    for (i64 bth = 0; bth < (i64)B * T * NH; bth++) {
-        const i64 b = bth / ((i64)T * NH), t = (bth / NH) % T, h = bth % NH;
+    /* (b, h) pairs in parallel: an iteration (b, t, h) touches only head h's columns of image b,
+     * and inside a pair t ascends as in the reference's bth order */
+#pragma omp parallel for schedule(dynamic, 1)
+    for (i64 bh = 0; bh < (i64)B * NH; bh++)
+    for (i64 t = 0; t < T; t++) {
+        const i64 b = bh / NH, h = bh % NH, bth = (b * T + t) * NH + h;
         const real* att_bth = att + bth * T;
         real* datt_bth = datt + bth * T;
         real* dpreatt_bth = dpreatt + bth * T;
@@ -252,6 +286,27 @@ void ref_attention_backward(real* dinp, real* dpreatt, real* datt, const real* d
 void ref_layernorm_backward(real* dinp, real* dweight, real* dbias, const real* dout,
                             const real* inp, const real* weight, const real* mean,
                             const real* rstd, int B, int T, int C) {
+    /* dweight / dbias: each thread owns a column range and walks the rows in order (the
+     * reference's per-element accumulation order); dinp: rows in parallel */
+#pragma omp parallel
+    {
+#ifdef _OPENMP
+        const int nth = omp_get_num_threads(), th = omp_get_thread_num();
+#else
+        const int nth = 1, th = 0;
+#endif
+        const int i0 = (int)((i64)C * th / nth), i1 = (int)((i64)C * (th + 1) / nth);
+        for (i64 bt = 0; bt < (i64)B * T; bt++) {
+            const real* dout_bt = dout + bt * C;
+            const real* inp_bt = inp + bt * C;
+            for (int i = i0; i < i1; i++) {
+                real norm_bti = (inp_bt[i] - mean[bt]) * rstd[bt];
+                dbias[i] += dout_bt[i];
+                dweight[i] += norm_bti * dout_bt[i];
+            }
+        }
+    }
+#pragma omp parallel for schedule(static)
     for (i64 bt = 0; bt < (i64)B * T; bt++) {
         const real* dout_bt = dout + bt * C;
         const real* inp_bt = inp + bt * C;
@@ -271,8 +326,6 @@ void ref_layernorm_backward(real* dinp, real* dweight, real* dbias, const real* 
         for (int i = 0; i < C; i++) {
             real norm_bti = (inp_bt[i] - mean_bt) * rstd_bt;
             real dnorm_i = weight[i] * dout_bt[i];
-            dbias[i] += dout_bt[i];
-            dweight[i] += norm_bti * dout_bt[i];
             real dval = 0;
             dval += dnorm_i;
             dval -= dnorm_mean;
@@ -286,6 +339,7 @@ void ref_layernorm_backward(real* dinp, real* dweight, real* dbias, const real* 
 /* train_vit.rs:639-653.  D4: sech^2 of the tanh argument itself (reference used cosh(2a)). */
 void ref_gelu_backward(real* dinp, const real* inp, const real* dout, int N) {
     const real s = gelu_s();
+#pragma omp parallel for schedule(static)
     for (i64 i = 0; i < N; i++) {
         real x = inp[i];
         real cube = (real)0.044715 * x * x * x;
@@ -334,8 +388,9 @@ void ref_patch_embed_forward(real* encoded, const real* pixels, const real* patc
                              const real* patch_b, const real* cls, const real* wpe,
                              int B, int IMG, int P, int C) {
     const int NP = (IMG / P) * (IMG / P), T = NP + 1, K = 3 * P * P;
-    real* row = (real*)malloc(sizeof(real) * (size_t)K);
+#pragma omp parallel for schedule(static)
     for (int b = 0; b < B; b++) {
+        real* row = (real*)malloc(sizeof(real) * (size_t)K);
         real* enc_b = encoded + (i64)b * T * C;
         for (int o = 0; o < C; o++) enc_b[o] = cls[o] + wpe[o];
         for (int p = 0; p < NP; p++) {
@@ -348,8 +403,8 @@ void ref_patch_embed_forward(real* encoded, const real* pixels, const real* patc
                 dst[o] = val + wpe[(i64)(1 + p) * C + o];
             }
         }
+        free(row);
     }
-    free(row);
 }
 
 /* D7: encoder_backward (called train_vit.rs:371) for the patch embedding; no pixel gradient.
@@ -359,8 +414,10 @@ void ref_patch_embed_backward(real* dpatch_w, real* dpatch_b, real* dcls, real* 
                               int B, int IMG, int P, int C) {
     const int NP = (IMG / P) * (IMG / P), T = NP + 1, K = 3 * P * P;
     real* patches = (real*)malloc(sizeof(real) * (size_t)B * NP * K);
+#pragma omp parallel for schedule(static)
     for (int b = 0; b < B; b++)
         for (int p = 0; p < NP; p++) patch_row(patches + ((i64)b * NP + p) * K, pixels, b, p, IMG, P);
+#pragma omp parallel for schedule(dynamic, 1)
     for (int o = 0; o < C; o++) {
         for (int b = 0; b < B; b++) {
             for (int p = 0; p < NP; p++) {
@@ -372,11 +429,14 @@ void ref_patch_embed_backward(real* dpatch_w, real* dpatch_b, real* dcls, real* 
             }
         }
     }
-    for (int b = 0; b < B; b++) {
-        for (int o = 0; o < C; o++) dcls[o] += dencoded[(i64)b * T * C + o];
-        for (int t = 0; t < T; t++)
+    /* per element, images in ascending order (the reference's b-outer loop) */
+#pragma omp parallel for schedule(static)
+    for (int o = 0; o < C; o++)
+        for (int b = 0; b < B; b++) dcls[o] += dencoded[(i64)b * T * C + o];
+#pragma omp parallel for schedule(static)
+    for (int t = 0; t < T; t++)
+        for (int b = 0; b < B; b++)
             for (int o = 0; o < C; o++) dwpe[(i64)t * C + o] += dencoded[((i64)b * T + t) * C + o];
-    }
     free(patches);
 }
 

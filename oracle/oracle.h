@@ -74,6 +74,10 @@ void ref_patch_embed_backward(real* dpatch_w, real* dpatch_b, real* dcls, real* 
                               int B, int IMG, int P, int C);
 /* optimizer_step (train_vit.rs:737-743): p -= lr * g */
 void ref_sgd_step(real* params, const real* grads, long long n, real lr);
+/* OpenMP thread count of the oracle (bitwise-identical results for any count; 1 = the
+ * single-thread reference timing) */
+void ref_set_num_threads(int n);
+int ref_get_num_threads(void);
 void ref_adamw_step(real* params, const real* grads, real* m, real* v, long long n, real lr,
                     real beta1, real beta2, real eps, real weight_decay, int t);
 

@@ -138,3 +138,47 @@ def test_dp_sum_allreduce_matches_full_batch(vit, oracle64, tmp_path):
     assert abs(loss_dp - loss) <= 1e-12 * abs(loss)
     err = np.abs(g_dp - g).max() / np.abs(g).max()
     assert err <= 1e-12, err   # fp64: only the summation order differs (<= 1e-5)
+
+
+@pytest.mark.parametrize("name,layers", [("vit_b16", None), ("test_h64", None), ("vit_h14", None), ("test", 1)])
+def test_dp_chunk_table_partitions_the_arena(vit, name, layers):
+    """The overlapped all-reduce's chunk table (trainer.hip compute_layout / chunk_done; the layout
+    permutes train_vit.rs:115-131's type-major order): chunks are contiguous, ascending and cover the
+    device gradient arena exactly once; chunk 0 holds the head + final LN, chunk c (1..L) holds all
+    12 tensors of layer L-c and nothing else (backward finishes layers L-1 .. 0 in that order and
+    all-reduces chunk c right after layer L-c), chunk L+1 the patch embedding; tensors do not overlap
+    and every canonical element has its own device slot."""
+    import ctypes
+    cfg = vit.data.CONFIGS[name]
+    if layers:
+        cfg = vit.data.VitCfg(cfg.name, cfg.img, cfg.patch, cfg.channels, layers, cfg.num_heads, cfg.num_classes)
+    L = cfg.num_layers
+    to = (ctypes.c_longlong * (20 * L))()
+    co = (ctypes.c_longlong * (L + 3))()
+    ar = ctypes.c_longlong()
+    c = vit._cfg_c(cfg)
+    n = vit.lib().vit_layout_query(ctypes.byref(c), ctypes.cast(to, ctypes.c_void_p), ctypes.cast(co, ctypes.c_void_p),
+                                   ctypes.byref(ar))
+    assert n == L + 2
+    chunks = list(co)
+    assert chunks[0] == 0 and chunks[-1] == ar.value
+    assert all(a < b for a, b in zip(chunks, chunks[1:]))
+    sizes = cfg.param_sizes()
+    names = vit.data.PARAM_NAMES
+    extents = []  # (start, end, chunk expected)
+    for ti, nm in enumerate(names):
+        if nm in vit.data.LAYER_PARAMS:
+            per = sizes[ti] // L
+            for l in range(L):
+                extents.append((to[ti * L + l], to[ti * L + l] + per, L - l, (nm, l)))
+        else:
+            want = 0 if nm in ("head_w", "head_b", "lnfw", "lnfb") else L + 1
+            extents.append((to[ti * L], to[ti * L] + sizes[ti], want, (nm, 0)))
+    extents.sort()
+    for (s0, e0, _, t0), (s1, _, _, t1) in zip(extents, extents[1:]):
+        assert e0 <= s1, (t0, t1)
+    for s, e, want, tag in extents:
+        assert chunks[want] <= s and e <= chunks[want + 1], (tag, want)
+    # each chunk is fully owned by its tensors (only alignment padding between them)
+    used = sum(e - s for s, e, _, _ in extents)
+    assert used == cfg.num_params() and ar.value - used < 64 * len(extents)

@@ -1,16 +1,20 @@
 """Model-level GPU parity: the native trainer (C ABI) vs the CPU oracle / golden fixtures.
 
-fp32 mode runs the reference op sequence on the GPU: logits, loss and every per-parameter
-gradient within 1e-4 relative (max-normalised per tensor) of the fp32 CPU oracle — the
-north-star parity bar.  bf16 mode (the benchmarked fast path) is gated against the same
-oracle at the SURVEY.md §8d bf16 target: loss 1e-2, logits / every gradient tensor 2e-2
-(max-normalised; measured <= 1.2e-2 at full ViT-B/16 depth, profiles/r02_parity.json).
+Every comparison is per tensor (logits and each of the 20 gradient tensors) with the two-part
+rule of tests/parity.py (floor restated in DESIGN.md §2):
+  fp32 mode (the reference op sequence on the GPU): max-normalised 1e-4 and elementwise
+      |gpu - ref| <= 1e-4 |ref| + 1e-5 max|ref| on >= 99.99 %, loss 1e-4 — the north-star bar;
+  bf16 mode (the benchmarked fast path): 2e-2 / 2e-2 |ref| + 2e-3 max|ref| on >= 99.99 %, loss 1e-2;
+  fp8 mode: the operand-rounding error model of tests/parity.py (<= 1.5 x 16 x the bf16 error).
+These configs are small (B <= 8): their GEMMs run the 128x128 engine.  The kernel set the bench
+times is checked at a production batch in test_gpu_production.py.
 """
 import os
 
 import numpy as np
 import pytest
 
+import parity
 from conftest import ROOT, rel_err
 
 pytestmark = pytest.mark.gpu
@@ -28,16 +32,12 @@ def oracle_step(oc, o, cfg, params, px, lab, b_global=None):
     return loss, m.logits(), g
 
 
-def elementwise_ok(a, r, frac=0.9999):
-    """|gpu - ref| <= 1e-4 |ref| + 1e-6 on >= 99.99 % of elements."""
-    a = np.asarray(a, np.float64).ravel()
-    r = np.asarray(r, np.float64).ravel()
-    ok = np.abs(a - r) <= 1e-4 * np.abs(r) + 1e-6
-    return float(ok.mean()) >= frac, float(ok.mean())
-
-
-def per_tensor_errs(cfg, g, r):
-    return {n: rel_err(a, b) for n, a, b in zip(cfg.split(g).keys(), cfg.split(g).values(), cfg.split(r).values())}
+def gate(cfg, logits, g, logits_r, g_r, rule, label=""):
+    """per-tensor parity (tests/parity.py) of the logits and every gradient tensor"""
+    bad, rep = parity.check(parity.tensors(cfg, logits, g, logits_r, g_r), rule)
+    print(f"\n{label} {parity.summary(rep)}")
+    assert not bad, (label, bad)
+    return rep
 
 
 @pytest.mark.parametrize("name", ["test", "test_t10"])
@@ -52,9 +52,7 @@ def test_fp32_trainer_matches_golden(gpu, name):
     m.backward()
     g = m.grads()
     assert abs(loss - float(z["loss"])) <= 1e-4 * abs(float(z["loss"]))
-    assert rel_err(m.logits(), z["logits"]) <= 1e-4
-    errs = per_tensor_errs(cfg, g, z["grads"])
-    assert max(errs.values()) <= 1e-4, errs
+    gate(cfg, m.logits(), g, z["logits"], z["grads"], parity.FP32, name)
     m.close()
 
 
@@ -73,11 +71,7 @@ def test_fp32_trainer_matches_oracle(gpu, oracle32, name, B):
     m.backward()
     g = m.grads()
     assert abs(loss - loss_r) <= 1e-4 * abs(loss_r)
-    assert rel_err(m.logits(), logits_r) <= 1e-4
-    errs = per_tensor_errs(cfg, g, g_r)
-    assert max(errs.values()) <= 1e-4, errs
-    ok, frac = elementwise_ok(g, g_r)
-    assert ok, frac
+    gate(cfg, m.logits(), g, logits_r, g_r, parity.FP32, name)
     # optimizer_step (train_vit.rs:737): p -= lr*g, bit-exact elementwise
     m.optimizer_step(0.01)
     p_new = m.params()
@@ -99,9 +93,7 @@ def test_bf16_trainer_vs_oracle(gpu, oracle32, name, B):
     m.backward()
     g = m.grads()
     assert abs(loss - loss_r) <= 1e-2 * abs(loss_r)
-    assert rel_err(m.logits(), logits_r) <= 2e-2
-    errs = per_tensor_errs(cfg, g, g_r)
-    assert max(errs.values()) <= 2e-2, errs
+    gate(cfg, m.logits(), g, logits_r, g_r, parity.BF16, name)
     m.close()
 
 
@@ -156,29 +148,22 @@ def test_vit_b16_full_size_step(gpu):
 
 def test_vit_b16_fp32_and_bf16_vs_oracle_one_image(gpu, oracle32):
     """ViT-B/16 224x224 at full width/depth (C=768, L=12, T=197), one image: the fp32 trainer
-    within 1e-4 of the CPU oracle on logits, loss and all 20 gradient tensors; the bf16 fast
-    path within 1e-2 (loss) / 2e-2 (logits, every gradient tensor) of the same oracle."""
+    and the bf16 fast path against the CPU oracle, per tensor (fp32 / bf16 rules of tests/parity.py)."""
     import oracle_ctypes as oc
     v = gpu
     cfg = v.data.CONFIGS["vit_b16"]
     params = v.data.init_params(cfg, "parity", seed=3)
     px, lab = v.data.synthetic_batch(cfg, 1, seed=5)
     loss_r, logits_r, g_r = oracle_step(oc, oracle32, cfg, params, px, lab)
-    res = {}
-    for prec, tol, tol_loss in ((v.VIT_FP32, 1e-4, 1e-4), (v.VIT_BF16, 2e-2, 1e-2)):
+    for prec, rule in ((v.VIT_FP32, parity.FP32), (v.VIT_BF16, parity.BF16)):
         m = v.ViT.build(cfg, 1, prec, params=params)
         m.zero_grad()
         loss = m.forward(px, lab)
         m.backward()
         g = m.grads()
-        errs = per_tensor_errs(cfg, g, g_r)
-        res[prec] = (abs(loss - loss_r) / abs(loss_r), rel_err(m.logits(), logits_r), max(errs.values()))
-        assert res[prec][0] <= tol_loss and res[prec][1] <= tol and res[prec][2] <= tol, (prec, res[prec], errs)
-        if prec == v.VIT_FP32:
-            ok, frac = elementwise_ok(g, g_r)
-            assert ok, frac
+        assert abs(loss - loss_r) <= rule["loss"] * abs(loss_r), (prec, loss, loss_r)
+        gate(cfg, m.logits(), g, logits_r, g_r, rule, f"vit_b16 B=1 prec {prec}")
         m.close()
-    print("vit_b16 B=1 rel errs (loss, logits, max grad tensor):", res)
 
 
 @pytest.mark.parametrize("prec_name", ["VIT_FP32", "VIT_BF16"])
@@ -294,9 +279,7 @@ def test_vit_l16_bf16_vs_fp32_trainer_two_layers(gpu):
     lf, zf, gf = out[v.VIT_FP32]
     lb, zb, gb = out[v.VIT_BF16]
     assert abs(lb - lf) <= 1e-2 * abs(lf)
-    assert rel_err(zb, zf) <= 2e-2
-    errs = per_tensor_errs(cfg, gb, gf)
-    assert max(errs.values()) <= 2e-2, errs
+    gate(cfg, zb, gb, zf, gf, parity.BF16, "vit_l16 L=2 bf16 vs fp32 trainer")
     assert base.channels == cfg.channels
 
 
@@ -319,9 +302,7 @@ def test_vit_h14_geometry_fp32_vs_oracle(gpu, oracle32):
     m.backward()
     g = m.grads()
     assert abs(loss - loss_r) <= 1e-4 * abs(loss_r)
-    assert rel_err(m.logits(), logits_r) <= 1e-4
-    errs = per_tensor_errs(cfg, g, g_r)
-    assert max(errs.values()) <= 1e-4, errs
+    gate(cfg, m.logits(), g, logits_r, g_r, parity.FP32, "vit_h14_l1 fp32")
     m.close()
     m = v.ViT.build(cfg, 1, v.VIT_BF16, params=params)
     m.zero_grad()
@@ -329,9 +310,7 @@ def test_vit_h14_geometry_fp32_vs_oracle(gpu, oracle32):
     m.backward()
     g = m.grads()
     assert abs(loss - loss_r) <= 1e-2 * abs(loss_r)
-    assert rel_err(m.logits(), logits_r) <= 2e-2
-    errs = per_tensor_errs(cfg, g, g_r)
-    assert max(errs.values()) <= 2e-2, errs
+    gate(cfg, m.logits(), g, logits_r, g_r, parity.BF16, "vit_h14_l1 bf16")
     m.close()
 
 
@@ -374,30 +353,35 @@ def _fp8_vs_oracle(v, oracle32, cfg, B, seed):
         m.zero_grad()
         loss = m.forward(px, lab)
         m.backward()
-        g = m.grads()
-        errs = per_tensor_errs(cfg, g, g_r)
-        out[prec] = (abs(loss - loss_r) / abs(loss_r), rel_err(m.logits(), logits_r), errs)
+        out[prec] = (abs(loss - loss_r) / abs(loss_r), parity.tensors(cfg, m.logits(), m.grads(), logits_r, g_r))
         m.close()
     return out
 
 
-@pytest.mark.parametrize("name,B", [("test_h64", 4), ("vit_h14_l1", 1)])
+@pytest.mark.parametrize("name,B", [("test_h64", 4), ("vit_h14_l1", 1), ("vit_b16_l2", 1)])
 def test_fp8_trainer_vs_oracle(gpu, oracle32, name, B):
     """BASELINE config 5's fp8 mode (MXFP8 forward and input-gradient GEMMs) against the fp32 CPU
-    oracle: loss within 2e-2, logits within 1e-1 and every gradient tensor within 1.5e-1
-    (max-normalised) — the e4m3 element rounding (2^-4 relative) through two GEMMs per gradient
-    path; the bf16 mode on the same inputs is reported beside it (its own gate is 2e-2)."""
+    oracle, per tensor, gated by the operand-rounding error model of tests/parity.py: fp8 mode only
+    changes the GEMM operands from bf16 (unit roundoff 2^-8) to e4m3 (2^-4), so each tensor's
+    max-normalised and rms errors stay within 1.5 x 16 x the bf16 mode's errors on the same inputs
+    (bf16 error floored at 2^-8); loss likewise.  ViT-H/14 geometry (head size 80, K=588 patch) and
+    ViT-B/16 width at two layers.  The fp8 path is not pinned by the reference (it has no fp8 path):
+    the bit-exact quantizer / fused-MX tests (test_gpu_fp8.py) are its primary guard."""
     v = gpu
-    cfg = (v.data.VitCfg("vit_h14_l1", img=224, patch=14, channels=1280, num_layers=1, num_heads=16,
-                         num_classes=1000) if name == "vit_h14_l1" else v.data.CONFIGS[name])
+    cfgs = {"vit_h14_l1": v.data.VitCfg("vit_h14_l1", img=224, patch=14, channels=1280, num_layers=1,
+                                        num_heads=16, num_classes=1000),
+            "vit_b16_l2": v.data.VitCfg("vit_b16_l2", img=224, patch=16, channels=768, num_layers=2,
+                                        num_heads=12, num_classes=1000)}
+    cfg = cfgs.get(name) or v.data.CONFIGS[name]
     out = _fp8_vs_oracle(v, oracle32, cfg, B, seed=41)
-    lf, zf, ef = out[v.VIT_FP8]
-    print(f"{name} fp8 vs oracle: loss {lf:.2e} logits {zf:.2e} max grad {max(ef.values()):.2e}",
-          {k: round(e, 4) for k, e in ef.items()})
-    lb, zb, eb = out[v.VIT_BF16]
-    print(f"{name} bf16 vs oracle: loss {lb:.2e} logits {zb:.2e} max grad {max(eb.values()):.2e}")
-    assert lf <= 2e-2 and zf <= 1e-1, (lf, zf)
-    assert max(ef.values()) <= 1.5e-1, ef
+    lb, pb = out[v.VIT_BF16]
+    lf, pf = out[v.VIT_FP8]
+    rf = parity.fp8_report(pf)
+    print(f"\n{name} fp8 vs oracle: loss {lf:.2e} (bf16 {lb:.2e}) max tensor err "
+          f"{max(x['max'] for x in rf.values()):.3f}", {k: round(x["max"], 4) for k, x in rf.items()})
+    assert lf <= parity.fp8_limit(lb), (lf, lb)
+    bad = parity.check_fp8(pf, pb)
+    assert not bad, bad
 
 
 def test_fp8_fused_mx_epilogues_bit_identical(gpu, monkeypatch):

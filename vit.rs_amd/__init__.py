@@ -61,7 +61,7 @@ def build(quiet=True):
 _VOID = [("vit_clear_error", []), ("vit_set_stream", [ctypes.c_void_p]),
          ("vit_free", [ctypes.c_void_p]), ("vit_event_destroy", [ctypes.c_void_p]),
          ("vit_trainer_destroy", [ctypes.c_void_p]), ("vit_trainer_timing_reset", [ctypes.c_void_p]),
-         ("vit_loader_close", [ctypes.c_void_p])]
+         ("vit_loader_close", [ctypes.c_void_p]), ("vit_kernel_hits_reset", [])]
 
 # name -> (restype, argtypes)
 P, I, LL, F, S = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_size_t
@@ -107,6 +107,7 @@ _SIGS = {
     "gemm_fp8_fused": (None, [P, P, LL, P, LL, P, P, LL, P, P, LL, P, P, I, I, I, I]),
     "gemm_fp8_fused_mx": (None, [P, P, LL, P, LL, P, P, LL, P, P, LL, P, P, I, I, I, I, P, P]),
     "gemm_bf16_set_variant": (None, [I]), "gemm_bf16_set_debug": (None, [I]),
+    "vit_kernel_hits": (I, [P, I]),
     "convert_f32_to_bf16": (None, [P, P, LL]),
     "convert_bf16_to_f32": (None, [P, P, LL]),
     # trainer
@@ -120,6 +121,7 @@ _SIGS = {
     "vit_trainer_train_step": (I, [P, F, I]), "vit_trainer_mean_loss": (F, [P]),
     "vit_trainer_get_logits": (I, [P, P]), "vit_trainer_sync": (I, [P]),
     "vit_trainer_stream": (P, [P]),
+    "vit_layout_query": (I, [ctypes.POINTER(VitConfigC), P, P, ctypes.POINTER(LL)]),
     "vit_dp_unique_id_size": (I, []), "vit_dp_get_unique_id": (I, [ctypes.c_char_p]),
     "vit_trainer_dp_init": (I, [P, I, I, ctypes.c_char_p, I]),
     "vit_trainer_dp_ranks": (I, [P]),
@@ -169,6 +171,24 @@ def lib():
         f.argtypes = args
     _lib = L
     return L
+
+
+# launch-counter families (include/vit_ops.h VIT_HIT_*); GEMM families are base + epilogue
+HIT_GEMM_128, HIT_GEMM_256x256, HIT_GEMM_256x128, HIT_GEMM_FP8, HIT_GEMM_F32 = 0, 16, 32, 48, 64
+HIT_SPLITK_REDUCE, HIT_ATTN_FWD_MFMA, HIT_ATTN_BWD_PERSISTENT = 80, 81, 82
+HIT_ATTN_BWD_ONEPASS, HIT_ATTN_BWD_PAIR, HIT_ATTN_GENERIC = 83, 84, 85
+
+
+def kernel_hits():
+    """Launch counts since the last kernel_hits_reset(), indexed by the HIT_* constants."""
+    n = lib().vit_kernel_hits(None, 0)
+    out = (ctypes.c_longlong * n)()
+    lib().vit_kernel_hits(ctypes.cast(out, ctypes.c_void_p), n)
+    return np.array(out[:], dtype=np.int64)
+
+
+def kernel_hits_reset():
+    lib().vit_kernel_hits_reset()
 
 
 def check(what=""):

@@ -582,6 +582,7 @@ void attn_forward_fused(bf16_t* out, float* lse, const bf16_t* qkv, int B, int T
             default: set_error("attention: no generic kernel for head size %d", C / NH); return;
         }
         after_launch("attention_forward_generic");
+        count_hit(VIT_HIT_ATTN_GENERIC);
         return;
     }
     bool ok = false;
@@ -626,6 +627,7 @@ void attn_backward_fused(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, co
             default: set_error("attention: no generic kernel for head size %d", C / NH); return;
         }
         after_launch("attention_backward_generic");
+        count_hit(VIT_HIT_ATTN_GENERIC);
         if (dqkv_colsum) colsum_bf16(dqkv_colsum, dqkv, B * T, 3 * C, 3LL * C, s);
         return;
     }

@@ -1087,6 +1087,7 @@ constexpr int max_tp() {
 template <int HS, int NKT>
 void launch_fwd(bf16_t* out, float* lse, const bf16_t* qkv, int B, int T, int C, int NH, hipStream_t s) {
     attn_fwd_k<HS, NKT><<<B * NH, 256, 0, s>>>(out, lse, qkv, T, C, NH);
+    count_hit(VIT_HIT_ATTN_FWD_MFMA);
 }
 int attn_bwd_variant();  // attention.hip: VIT_ATTN_BWD = pair | one | (default) persistent (A/B)
 int attn_cu_count();     // attention.hip: compute units of the current device
@@ -1099,16 +1100,19 @@ int launch_bwd(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t
         if (v == 0) {
             attn_bwdp_k<HS, NKT, 2><<<std::min(BH, attn_cu_count()), NKT / 2 * 64, 0, s>>>(dqkv, dout, qkv, out, lse,
                                                                                          T, C, NH, BH, part);
+            count_hit(VIT_HIT_ATTN_BWD_PERSISTENT);
             return NKT / 2;
         }
     }
     if constexpr (bwd1_fits<HS, NKT>()) {
         if (v != 2) {
             attn_bwd1_k<HS, NKT><<<BH, NKT / 2 * 64, 0, s>>>(dqkv, dout, qkv, out, lse, T, C, NH, part);
+            count_hit(VIT_HIT_ATTN_BWD_ONEPASS);
             return NKT / 2;
         }
     }
     attn_bwd_pair_k<HS, NKT><<<2 * cdiv(BH, 8) * 8, 256, 0, s>>>(dqkv, dout, qkv, out, lse, T, C, NH, BH, part);
+    count_hit(VIT_HIT_ATTN_BWD_PAIR);
     return 1;
 }
 template <int HS, int NKT = 2>

@@ -6,6 +6,8 @@
 
 #include <cstdio>
 
+#include "../../include/vit_ops.h"
+
 typedef uint16_t bf16_t;  // raw bf16 bits in HBM
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -36,8 +38,8 @@ bool has_error();
 hipStream_t stream();
 bool sync_each_op();
 void* workspace(size_t bytes);  // per-thread device scratch, grown on demand
-void* sk_workspace(size_t bytes);  // per-thread stream-K GEMM scratch, zero-filled on growth
 void after_launch(const char* what);
+void count_hit(int kind);  // VIT_HIT_* (include/vit_ops.h)
 }  // namespace vit
 
 #define VIT_HIP(call)                                                                  \

@@ -1,6 +1,7 @@
 // context.hip — per-thread stream / sticky error / workspace for the C ABI (include/vit_ops.h).
 #include <cstdarg>
 #include <cstdlib>
+#include <atomic>
 #include <cstring>
 
 #include "common.h"
@@ -14,8 +15,6 @@ struct Ctx {
     char msg[512] = {0};
     void* ws = nullptr;
     size_t ws_bytes = 0;
-    void* sk = nullptr;  // stream-K scratch (flags + partial tiles), zero-filled
-    size_t sk_bytes = 0;
 };
 thread_local Ctx g_ctx;
 int g_sync_each = -1;
@@ -56,23 +55,10 @@ void* workspace(size_t bytes) {
     }
     return g_ctx.ws;
 }
-void* sk_workspace(size_t bytes) {
-    if (bytes > g_ctx.sk_bytes) {
-        if (g_ctx.sk) {
-            VIT_HIP(hipDeviceSynchronize());
-            VIT_HIP(hipFree(g_ctx.sk));
-        }
-        g_ctx.sk = nullptr;
-        g_ctx.sk_bytes = 0;
-        if (hipMalloc(&g_ctx.sk, bytes) != hipSuccess) {
-            set_error("sk_workspace: hipMalloc(%zu) failed", bytes);
-            return nullptr;
-        }
-        VIT_HIP(hipMemset(g_ctx.sk, 0, bytes));  // the hand-off flags start (and end) at 0
-        VIT_HIP(hipDeviceSynchronize());
-        g_ctx.sk_bytes = bytes;
-    }
-    return g_ctx.sk;
+// launch counters (vit_kernel_hits): which engine / kernel each call ran
+static std::atomic<long long> g_hits[VIT_HIT_COUNT];
+void count_hit(int k) {
+    if (k >= 0 && k < VIT_HIT_COUNT) g_hits[k].fetch_add(1, std::memory_order_relaxed);
 }
 void after_launch(const char* what) {
     hipError_t e = hipGetLastError();
@@ -119,6 +105,14 @@ void* vit_malloc(size_t bytes) {
         return nullptr;
     }
     return p;
+}
+int vit_kernel_hits(long long* out, int n) {
+    const int m = n < VIT_HIT_COUNT ? n : VIT_HIT_COUNT;
+    for (int k = 0; k < m; k++) out[k] = vit::g_hits[k].load(std::memory_order_relaxed);
+    return VIT_HIT_COUNT;
+}
+void vit_kernel_hits_reset(void) {
+    for (auto& h : vit::g_hits) h.store(0, std::memory_order_relaxed);
 }
 void vit_free(void* p) {
     if (p) VIT_HIP(hipFree(p));

@@ -56,10 +56,6 @@ struct GemmArgs {
     // (ordered on the context stream); the trainer passes its own buffer for its stream.
     float* ws = nullptr;
     size_t ws_bytes = 0;
-    // stream-K scratch (hand-off flags + partial tiles, gemm_sk_bytes()), zero-filled before first
-    // use and left zeroed by every launch; nullptr = the calling thread's.  Launches sharing one
-    // scratch must be ordered (same stream).
-    char* sk_ws = nullptr;
     // fp8 operands (gemm_fp8): MX scales of A and B in the lane-native layout of gemm_fp8.hip
     const void* a_scale = nullptr;
     const void* b_scale = nullptr;
@@ -71,7 +67,6 @@ struct GemmArgs {
     uint8_t* mx_q = nullptr;
     uint8_t* mx_s = nullptr;
 };
-size_t gemm_sk_bytes();
 
 // fp32 operands, exact-fp32 MFMA (v_mfma_f32_16x16x4_f32); any shape/stride. Parity path.
 void gemm_f32(const GemmArgs& a, hipStream_t s);
@@ -79,13 +74,9 @@ void gemm_f32(const GemmArgs& a, hipStream_t s);
 // operands, lda/ldb%8==0, the contiguous dim of an M/N-contig operand %8==0, N%4==0.
 void gemm_bf16(const GemmArgs& a, hipStream_t s);
 bool gemm_bf16_supported(const GemmArgs& a);
-// engine selection for A/B measurements in one process: 1 = 128x128, 2 = 256x256 (1 WG/CU, default),
-// 4 = 256x128 (2 WG/CU); anything else = 2 (the default); debug flags: 2 = skip epilogues (main
-// loop only), 4 = 256x256 engine with LDS-DMA prefetch depth 3 instead of 2, 8 / 16 = split-K
-// sized for 1/2 / 1/4 of the CUs, 32 = generic (bounds-checked) epilogue, 64 = non-temporal
-// epilogue accesses, 128 = epilogue rows mod 256 (L2-resident output; diagnostic, wrong results),
-// 256*n (n < 64) = first-round stagger, 65536*g (g < 64) = grouped tile order, 1<<23 = split-K
-// weight gradients on the 256x256 engine (default: 256x128)
+// engine selection for A/B measurements in one process: 1 = 128x128 everywhere, 2 = production
+// (256x256, 1 WG/CU; split-K weight gradients on 256x128, 2 WG/CU), 4 = 256x128 everywhere;
+// anything else = 2.  Debug flag 2 = skip the epilogues (main-loop-only timing).
 void gemm_set_variant(int v);
 void gemm_set_debug(int flags);
 

@@ -315,53 +315,17 @@ __device__ __forceinline__ void wait_vm(int n) {
         default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     }
 }
-// vector-memory operations one wave issues in direct_epilogue<EPI> on an interior tile (16-B aux
-// loads, 16-B stores, colsum atomics); checked against the disassembly (global_load / _store /
-// _atomic between the persistent kernel's prologue issue and its loop back-edge)
-template <int EPI>
-__host__ __device__ constexpr int direct_vm_ops(bool colsum) {
-    return EPI == EPI_BF16_STORE ? 16
-         : (EPI == EPI_BF16_GELU || EPI == EPI_BF16_GELU_D || EPI == EPI_F32_STORE) ? 32
-         : (EPI == EPI_F32_RESID || EPI == EPI_F32_ACC) ? 64
-         : epi_aux16(EPI) ? 32 + (colsum ? 16 : 0)
-         : 64;
-}
-// s_waitcnt vmcnt(n), n <= 63 a runtime value from a small set (literal immediates)
-__device__ __forceinline__ void wait_vm_any(int n) {
-    switch (n) {
-#define VIT_W(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
-        VIT_W(20) VIT_W(36) VIT_W(52) VIT_W(63)
-#undef VIT_W
-        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    }
-}
 template <bool AK, bool BKC, int EPI, int DEPTH>
 __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
     constexpr int NS = DEPTH + 2;
     __shared__ __attribute__((aligned(1024))) char smem[smem_bytes<DEPTH>()];
-    // Epilogue de-phasing: every CU runs the same tile time, so the first round's start sets the
-    // phase of the whole launch and all CUs hit their epilogue HBM bursts together.  Delaying
-    // every other first-round workgroup (alternating within each XCD) puts half the CUs in their
-    // main loop while the other half stores.
-    if (p.stagger) {
-        const int lin = blockIdx.y * gridDim.x + blockIdx.x;
-        if (lin < 256 && ((lin >> 3) & 1))
-            for (int k = 0; k < p.stagger; k++) __builtin_amdgcn_s_sleep(127);
-    }
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
     const int ntm = cdiv(p.M, BM), ntn = cdiv(p.N, BN);
     int wg, split;
     split_remap(ntm * ntn, wg, split);
-    int tm0 = (wg / ntn) * BM, tn0 = (wg % ntn) * BN;
-    if (p.group_m > 0) {  // grouped order: GM M-rows x all N-columns, walked column-major
-        const int GM = p.group_m, per = GM * ntn, grp = wg / per, first = grp * GM;
-        const int gsz = min(GM, ntm - first), r = wg - grp * per;
-        tm0 = (first + r % gsz) * BM;
-        tn0 = (r / gsz) * BN;
-    }
-    if (p.debug_same_tile) { tm0 = 0; tn0 = 0; }  // diagnostic: every block streams one tile (L2)
+    const int tm0 = (wg / ntn) * BM, tn0 = (wg % ntn) * BN;
     const int kbeg = split * p.kchunk;
     const int kend = min(p.K, kbeg + p.kchunk);
     const int nk = (kend - kbeg) / BK;
@@ -470,497 +434,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
     staged_epilogue<EPI>(p, acc, smem + wave * STG_WAVE_BYTES, lane, tm0 + wm * 128, tn0 + wn * 64);
 }
 
-// Persistent form: one workgroup per CU walks the launch's tiles in the one-tile-per-workgroup
-// launch's XCD-aware order (tile v of workgroup b is v = b + k*gridDim.x, gridDim.x a multiple of
-// 8, so v % 8 is still b's XCD).  After a tile's main loop the NEXT tile's first DEPTH K-steps go
-// into the ring BEFORE this tile's epilogue, which runs LDS-free (direct_epilogue): the
-// prologue's DMA latency and the workgroup relaunch overlap the epilogue's stores.  The first
-// wait of the next tile is vmcnt(0) (vmcnt counts the epilogue's stores too).  Whole-K, N % 256
-// == 0, no split-K / bias-gradient launches.
-template <bool AK, bool BKC, int EPI>
-__global__ __launch_bounds__(NT, 1) void gemm_kernel_p(GemmParams p) {
-    constexpr int DEPTH = 2, NS = DEPTH + 2;
-    __shared__ __attribute__((aligned(1024))) char smem[NS * SLOT_BYTES];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 2, wn = wave & 3;
-    const int ntm = cdiv(p.M, BM), ntn = cdiv(p.N, BN), ntiles = ntm * ntn;
-    const int nk = p.K / BK;
-    const bf16_t* A = (const bf16_t*)p.A;
-    const bf16_t* B = (const bf16_t*)p.B;
-    const bool lagging = wave >= 4;
-    auto slot_of = [&](int st) { return smem + (st % NS) * SLOT_BYTES; };
-    auto tile_of = [&](int v, int& tm0, int& tn0) {
-        const int wg = xcd_remap(v, ntiles);
-        tm0 = (wg / ntn) * BM;
-        tn0 = (wg % ntn) * BN;
-    };
-    auto issue_a = [&](int tm0, int st) {
-        if (st < nk) stage<AK>(A, p.lda, tm0, p.M, st * BK, slot_of(st), wave, lane);
-    };
-    auto issue_b = [&](int tn0, int st) {
-        if (st < nk) stage<BKC>(B, p.ldb, tn0, p.N, st * BK, slot_of(st) + IMG_BYTES, wave, lane);
-    };
-    auto bar = [&]() {
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    f32x4_t acc[8][4];
-    auto mfma_half = [&](int half, const bf16x8_t (&fa)[4], const bf16x8_t (&fb)[4]) {
-#pragma unroll
-        for (int a = 0; a < 4; a++)
-#pragma unroll
-            for (int b = 0; b < 4; b++)
-                acc[half * 4 + a][b] =
-                    __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[b], fa[a], acc[half * 4 + a][b], 0, 0, 0);
-    };
-    int v = blockIdx.x;
-    if (v >= ntiles || nk <= 0) return;
-    int tm0, tn0;
-    tile_of(v, tm0, tn0);
-#pragma unroll
-    for (int st = 0; st < DEPTH; st++) { issue_a(tm0, st); issue_b(tn0, st); }
-    // memory operations a wave issued after the current tile's step-0 pieces that may stay in
-    // flight at its first wait: step 1's pieces (4), and after the first tile the previous tile's
-    // epilogue (vmcnt counts loads, stores, atomics and LDS-DMA together in issue order,
-    // MI355X_MICROARCH.md); -1 = wait for everything (a ragged previous tile skips stores)
-    int younger = 4 * (min(DEPTH, nk) - 1);
-    for (;;) {
-        if (younger == 0 || younger == 4) wait_vm(younger);
-        else if (younger > 0) wait_vm_any(younger);
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        bar();
-        if (lagging) {
-            __builtin_amdgcn_s_setprio(1);
-            bar();
-        }
-#pragma unroll
-        for (int a = 0; a < 8; a++)
-#pragma unroll
-            for (int b = 0; b < 4; b++) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        bf16x8_t fb[4], alo[4], ahi[4];
-        for (int kt = 0; kt < nk; kt++) {
-            const char* img = slot_of(kt);
-#pragma unroll
-            for (int b = 0; b < 4; b++) fb[b] = frag<BKC>(img + IMG_BYTES, wn * 64 + b * 16, lane);
-#pragma unroll
-            for (int a = 0; a < 4; a++) alo[a] = frag<AK>(img, wm * 128 + a * 16, lane);
-            issue_a(tm0, kt + DEPTH);
-            bar();
-            mfma_half(0, alo, fb);
-            bar();
-#pragma unroll
-            for (int a = 0; a < 4; a++) ahi[a] = frag<AK>(img, wm * 128 + (4 + a) * 16, lane);
-            wait_vm(4 * max(0, min(kt + DEPTH, nk) - (kt + 2)) + (kt + DEPTH < nk ? 2 : 0));
-            issue_b(tn0, kt + DEPTH);
-            bar();
-            mfma_half(1, ahi, fb);
-            bar();
-        }
-        if (!lagging) bar();  // balance the stagger barrier: every wave is past its last ring read
-        __builtin_amdgcn_s_setprio(0);
-        // this lane's bias columns (older than the next prologue's DMA)
-        float bv[2][8];
-        const int m0 = tm0 + wm * 128, n0 = tn0 + wn * 64;
-#pragma unroll
-        for (int pr = 0; pr < 2; pr++)
-#pragma unroll
-            for (int j = 0; j < 8; j++) bv[pr][j] = 0.f;
-        if constexpr (epi_bias(EPI)) {
-            if (p.bias) {
-#pragma unroll
-                for (int pr = 0; pr < 2; pr++) {
-                    const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n0 + pr * 32 + direct_col(lane));
-                    const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n0 + pr * 32 + direct_col(lane) + 4);
-                    bv[pr][0] = b0.x; bv[pr][1] = b0.y; bv[pr][2] = b0.z; bv[pr][3] = b0.w;
-                    bv[pr][4] = b1.x; bv[pr][5] = b1.y; bv[pr][6] = b1.z; bv[pr][7] = b1.w;
-                }
-            }
-        }
-        const int vn = v + gridDim.x;
-        int tm1 = 0, tn1 = 0;
-        __builtin_amdgcn_sched_barrier(0);  // bias loads stay older than the next prologue
-        if (vn < ntiles) {
-            tile_of(vn, tm1, tn1);
-#pragma unroll
-            for (int st = 0; st < DEPTH; st++) { issue_a(tm1, st); issue_b(tn1, st); }
-        }
-        __builtin_amdgcn_sched_barrier(0);  // and every epilogue access younger than it
-        const bool ragged = tm0 + BM > p.M;  // workgroup-uniform; rows >= M skip their stores
-        if (!skip_epilogue(p, acc)) direct_epilogue<EPI>(p, acc, bv, lane, m0, n0);
-        younger = (ragged || p.no_epi) ? -1 : min(63, 4 * (min(DEPTH, nk) - 1) + direct_vm_ops<EPI>(p.colsum_out != nullptr));
-        if (vn >= ntiles) break;
-        v = vn;
-        tm0 = tm1;
-        tn0 = tn1;
-    }
-}
 }  // namespace g2
-
-// ============================================================================ stream-K persistent
-// g3: the g2 tile / pipeline (256x256, 8 waves, LDS-DMA ring, staggered halves) run as ONE
-// persistent workgroup per CU over a contiguous range of the launch's (tile, K-step) space
-// ("stream-K").  Why: with one tile per workgroup every CU reached its epilogue at the same
-// moment, so the output stores (128-512 KiB per tile) went out as chip-wide HBM bursts with the
-// matrix pipes idle, and N = 768 launches (591 tiles) ran 2.31 tiles per CU in 3 rounds.  Here
-// each CU gets W/P K-steps; tile boundaries fall at a different point on every CU, so epilogues
-// are spread over the launch, and the ring keeps streaming across tile boundaries (the DMA for
-// the next tile's first steps is already in flight while a tile's epilogue runs).
-// A tile cut by a range boundary is computed in two parts: the CU whose range STARTS inside the
-// tile (it reaches that part first) writes its fp32 partial accumulators with write-through
-// (sc1) stores, each wave then adds 1 to the boundary's flag; the CU whose range ENDS inside the
-// tile (it reaches the tile's first K-steps last) polls the flag with sc1 loads, reads the
-// partial with sc1 loads (MI355X_MICROARCH.md, hand-off table row 3: no release/acquire fence),
-// adds it and runs the epilogue.  Every consumer wave adds 1 as well; the one that brings the
-// count to 16 resets it to 0 for the next launch.  W/P >= S (tiles >= CUs) so a tile is cut at
-// most once.  Epilogues go through a dedicated 32 KiB LDS staging area (4 KiB per wave: 16 rows
-// x 64 fp32, XOR-swizzled), so they never touch the ring.
-namespace g3 {
-using g2::BM;
-using g2::BN;
-using g2::BK;
-using g2::NT;
-constexpr int NSLOT = 4;  // g3 keeps the 4-slot ring (160 KiB with its 32 KiB staging area)
-using g2::IMG_BYTES;
-using g2::SLOT_BYTES;
-constexpr int RING_BYTES = NSLOT * SLOT_BYTES;        // 128 KiB
-constexpr int STG16_WAVE = 16 * 64 * 4;               // 4 KiB per wave
-constexpr int SMEM_BYTES = RING_BYTES + 8 * STG16_WAVE;  // 160 KiB
-constexpr int PART_BYTES = 8 * 32 * 64 * 16;          // fp32 partial tile, fragment-native: 256 KiB
-constexpr int FLAG_BYTES = 4096;                      // flags[1024] in front of the partials
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-// 16-row staged epilogue: pass a writes acc[a][0..3] (rows 16a..16a+15 of the wave tile) into the
-// wave's area (element (r, c) at r*256 + ((c/4 ^ r) * 16) + (c%4)*4: conflict-free for both the
-// fragment writes and the row reads); lane then owns row (lane>>3) + 8*it, columns 8*(lane&7)..+7.
-template <int EPI>
-__device__ __forceinline__ void staged_epilogue16(const GemmParams& p, f32x4_t (&acc)[8][4],
-                                                  char* stg, int lane, int m0, int n0) {
-    const int i = lane & 15, g = lane >> 4;
-    const int rr = lane >> 3, c8 = lane & 7;
-    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int a = 0; a < 8; a++) {
-        __builtin_amdgcn_sched_barrier(0);  // one pass at a time: no loads hoisted across passes
-#pragma unroll
-        for (int b = 0; b < 4; b++)
-            *reinterpret_cast<f32x4_t*>(stg + i * 256 + (((b * 4 + g) ^ i) << 4)) = acc[a][b];
-#pragma unroll
-        for (int it = 0; it < 2; it++) {
-            const int r = it * 8 + rr;
-            const f32x4_t lo = *reinterpret_cast<const f32x4_t*>(stg + r * 256 + (((2 * c8) ^ r) << 4));
-            const f32x4_t hi = *reinterpret_cast<const f32x4_t*>(stg + r * 256 + (((2 * c8 + 1) ^ r) << 4));
-            float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            const int m = m0 + a * 16 + r, n = n0 + c8 * 8;
-            if (m >= p.M) continue;
-            if (n + 8 <= p.N) {
-                epilogue8<EPI>(p, m, n, v, cs, lane);
-            } else if (n + 4 <= p.N) {
-                f32x4_t t = lo;
-                epilogue<EPI>(p, m, n, t);
-                if constexpr (EPI == EPI_BF16_DGELU) {
-                    const uint2 h = *reinterpret_cast<const uint2*>((const bf16_t*)p.aux + (long long)m * p.ldaux + n);
-                    cs[0] += lo[0] * gelu_grad_fast_f(__uint_as_float(h.x << 16));
-                    cs[1] += lo[1] * gelu_grad_fast_f(__uint_as_float(h.x & 0xffff0000u));
-                    cs[2] += lo[2] * gelu_grad_fast_f(__uint_as_float(h.y << 16));
-                    cs[3] += lo[3] * gelu_grad_fast_f(__uint_as_float(h.y & 0xffff0000u));
-                }
-            }
-        }
-    }
-    if constexpr (EPI == EPI_BF16_DGELU) {
-        if (p.colsum_out) {
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                float t = cs[j];
-                t += __shfl_xor(t, 8, 64);
-                t += __shfl_xor(t, 16, 64);
-                t += __shfl_xor(t, 32, 64);
-                cs[j] = t;
-            }
-            if (rr == 0) {
-#pragma unroll
-                for (int j = 0; j < 8; j++)
-                    if (n0 + c8 * 8 + j < p.N) atomicAdd(p.colsum_out + n0 + c8 * 8 + j, cs[j]);
-            }
-        }
-    }
-}
-
-// Interior wave tiles (all 128 rows < M, all 64 columns < N): the aux rows of the first D passes
-// are loaded before the first pass and pass a issues the loads of pass a + D, so the epilogue waits
-// for about one HBM round trip instead of one per 16-row pass (the loop above serialises eight).
-template <int EPI>
-__device__ __forceinline__ void staged_epilogue16_interior(const GemmParams& p, f32x4_t (&acc)[8][4],
-                                                           char* stg, int lane, int m0, int n0) {
-    constexpr bool AUX16 = EPI == EPI_BF16_DGELU;
-    constexpr bool AUX32 = EPI == EPI_F32_RESID || EPI == EPI_F32_ACC;
-    constexpr int NL = AUX16 ? 2 : (AUX32 ? 4 : 1);  // 16-B aux loads per lane and pass
-    constexpr int D = AUX16 ? 2 : 2;                 // passes whose aux loads are in flight (VGPR budget: no spills)
-    const int i = lane & 15, g = lane >> 4;
-    const int rr = lane >> 3, c8 = lane & 7;
-    const int n = n0 + c8 * 8;
-    u32x4 ax[8][NL];
-    auto load_pass = [&](int a) {
-        if constexpr (AUX16) {
-#pragma unroll
-            for (int it = 0; it < 2; it++)
-                ax[a & 7][it] = *reinterpret_cast<const u32x4*>(
-                    (const bf16_t*)p.aux + (long long)(m0 + a * 16 + it * 8 + rr) * p.ldaux + n);
-        } else if constexpr (AUX32) {
-            const float* src = EPI == EPI_F32_RESID ? (const float*)p.aux : (const float*)p.C;
-            const long long ld = EPI == EPI_F32_RESID ? p.ldaux : p.ldc;
-#pragma unroll
-            for (int it = 0; it < 2; it++) {
-                const u32x4* q = reinterpret_cast<const u32x4*>(src + (long long)(m0 + a * 16 + it * 8 + rr) * ld + n);
-                ax[a & 7][2 * it] = q[0];
-                ax[a & 7][2 * it + 1] = q[1];
-            }
-        }
-    };
-#pragma unroll
-    for (int a = 0; a < D; a++) load_pass(a);
-    float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if constexpr (EPI != EPI_F32_ATOMIC && EPI != EPI_BF16_DGELU && EPI != EPI_F32_SLAB) {
-        if (p.bias) {
-            const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
-            const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
-            bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w;
-            bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
-        }
-    }
-    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    auto pack8 = [](const float (&w)[8]) {
-        return u32x4{pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3]), pack_bf16x2(w[4], w[5]),
-                     pack_bf16x2(w[6], w[7])};
-    };
-#pragma unroll
-    for (int a = 0; a < 8; a++) {
-        __builtin_amdgcn_sched_barrier(0);  // pass a issues exactly the loads of pass a + D
-        if (a + D < 8) load_pass(a + D);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int b = 0; b < 4; b++)
-            *reinterpret_cast<f32x4_t*>(stg + i * 256 + (((b * 4 + g) ^ i) << 4)) = acc[a][b];
-#pragma unroll
-        for (int it = 0; it < 2; it++) {
-            if (it) __builtin_amdgcn_sched_barrier(0);  // one row at a time (VGPR budget)
-            const int r = it * 8 + rr;
-            const f32x4_t lo = *reinterpret_cast<const f32x4_t*>(stg + r * 256 + (((2 * c8) ^ r) << 4));
-            const f32x4_t hi = *reinterpret_cast<const f32x4_t*>(stg + r * 256 + (((2 * c8 + 1) ^ r) << 4));
-            float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-            for (int j = 0; j < 8; j++) v[j] += bv[j];
-            const long long off = (long long)(m0 + a * 16 + r) * p.ldc + n;
-            auto st_f32 = [&](float* q) {
-                reinterpret_cast<float4*>(q)[0] = make_float4(v[0], v[1], v[2], v[3]);
-                reinterpret_cast<float4*>(q)[1] = make_float4(v[4], v[5], v[6], v[7]);
-            };
-            if constexpr (EPI == EPI_F32_STORE) {
-                st_f32((float*)p.C + off);
-            } else if constexpr (AUX32) {
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    v[j] += __uint_as_float(ax[a][2 * it][j]);
-                    v[4 + j] += __uint_as_float(ax[a][2 * it + 1][j]);
-                }
-                st_f32((float*)p.C + off);
-            } else if constexpr (EPI == EPI_BF16_STORE) {
-                *reinterpret_cast<u32x4*>((bf16_t*)p.C + off) = pack8(v);
-            } else if constexpr (EPI == EPI_BF16_GELU) {
-                float gv[8];
-#pragma unroll
-                for (int j = 0; j < 8; j++) gv[j] = gelu_fast_f(v[j]);
-                *reinterpret_cast<u32x4*>((bf16_t*)p.C + off) = pack8(v);
-                *reinterpret_cast<u32x4*>((bf16_t*)p.C2 + off) = pack8(gv);
-            } else if constexpr (EPI == EPI_BF16_DGELU) {
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    v[2 * j] *= gelu_grad_fast_f(__uint_as_float(ax[a][it][j] << 16));
-                    v[2 * j + 1] *= gelu_grad_fast_f(__uint_as_float(ax[a][it][j] & 0xffff0000u));
-                }
-#pragma unroll
-                for (int j = 0; j < 8; j++) cs[j] += v[j];
-                *reinterpret_cast<u32x4*>((bf16_t*)p.C + off) = pack8(v);
-            }
-        }
-    }
-    if constexpr (EPI == EPI_BF16_DGELU) {
-        if (p.colsum_out) {
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                float t = cs[j];
-                t += __shfl_xor(t, 8, 64);
-                t += __shfl_xor(t, 16, 64);
-                t += __shfl_xor(t, 32, 64);
-                cs[j] = t;
-            }
-            if (rr == 0) {
-#pragma unroll
-                for (int j = 0; j < 8; j++) atomicAdd(p.colsum_out + n + j, cs[j]);
-            }
-        }
-    }
-}
-
-// whole != 0: persistent launch over whole tiles (workgroup w takes tiles [T*w/P, T*(w+1)/P)), so
-// no tile is cut and no workgroup waits on another: safe beside other streams' kernels, which a
-// stream-K hand-off is not (its partner may not be resident).
-template <bool AK, bool BKC, int EPI>
-__global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p, char* __restrict__ sk_ws, int S, int whole) {
-    __shared__ __attribute__((aligned(1024))) char smem[SMEM_BYTES];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 2, wn = wave & 3;
-    const int ntn = cdiv(p.N, BN);
-    const int P = gridDim.x;
-    const int w = xcd_remap(blockIdx.x, P);  // XCD-contiguous ranges: neighbouring tiles share L2
-    const int Wtot = p.tiles * S;  // host guarantees < 2^31
-    const int g_begin = whole ? (int)((long long)p.tiles * w / P) * S : (int)((long long)Wtot * w / P);
-    const int g_end = whole ? (int)((long long)p.tiles * (w + 1) / P) * S : (int)((long long)Wtot * (w + 1) / P);
-    const bf16_t* A = (const bf16_t*)p.A;
-    const bf16_t* B = (const bf16_t*)p.B;
-    int* flags = reinterpret_cast<int*>(sk_ws);
-    char* parts = sk_ws + FLAG_BYTES;
-    char* stg = smem + RING_BYTES + wave * STG16_WAVE;
-
-    f32x4_t acc[8][4];
-
-    // global step gs -> ring slot, tile origin and k offset (clamped to the range's last step:
-    // re-staging it keeps the per-step DMA count, and so every vmcnt literal, uniform)
-    auto slot_of = [&](int gs) { return smem + ((gs - g_begin) & (NSLOT - 1)) * SLOT_BYTES; };
-    auto coords = [&](int gs, int& m0, int& n0, int& k0) {
-        const int c = gs < g_end ? gs : g_end - 1;
-        const int t = c / S, ks = c - t * S;
-        m0 = (t / ntn) * BM;
-        n0 = (t % ntn) * BN;
-        k0 = ks * BK;
-    };
-    auto issue_a = [&](int gs) {
-        int m0, n0, k0;
-        coords(gs, m0, n0, k0);
-        g2::stage<AK>(A, p.lda, m0, p.M, k0, slot_of(gs), wave, lane);
-    };
-    auto issue_b = [&](int gs) {
-        int m0, n0, k0;
-        coords(gs, m0, n0, k0);
-        g2::stage<BKC>(B, p.ldb, n0, p.N, k0, slot_of(gs) + IMG_BYTES, wave, lane);
-    };
-    auto bar = [&]() {
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    auto mfma_half = [&](int half, const bf16x8_t (&fa)[4], const bf16x8_t (&fb)[4]) {
-#pragma unroll
-        for (int a = 0; a < 4; a++)
-#pragma unroll
-            for (int b = 0; b < 4; b++)
-                acc[half * 4 + a][b] =
-                    __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[b], fa[a], acc[half * 4 + a][b], 0, 0, 0);
-    };
-
-    const bool lagging = wave >= 4;
-    const bool any = g_end > g_begin;
-    if (any) {
-        issue_a(g_begin); issue_b(g_begin); issue_a(g_begin + 1); issue_b(g_begin + 1);
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        bar();
-        if (lagging) {
-            __builtin_amdgcn_s_setprio(1);
-            bar();
-        }
-    }
-    int gs = g_begin;
-    while (gs < g_end) {
-        // ---- one tile segment [gs, seg_end) of tile t
-        const int t = gs / S;
-        const int tbeg = t * S, tend = tbeg + S;
-        const int seg_end = min(g_end, tend);
-        const bool starts_in = tbeg < g_begin;  // range starts inside t: this part is a partial
-        const bool ends_in = seg_end < tend;     // range ends inside t: the partial comes in here
-        if (ends_in) {
-            // t's later K-steps were the FIRST work of the next range: its partial is (almost
-            // surely) published; it becomes the starting value of the accumulators
-            int spins = 0;
-            while (__hip_atomic_load(flags + w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 8 &&
-                   spins < (1 << 24)) {
-                __builtin_amdgcn_s_sleep(4);
-                spins++;
-            }
-            __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-                parts + (long long)(w + 1) * PART_BYTES, (short)0, PART_BYTES, 0x00020000);
-#pragma unroll
-            for (int a = 0; a < 8; a++)
-#pragma unroll
-                for (int b = 0; b < 4; b++)
-                    acc[a][b] = __builtin_bit_cast(
-                        f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
-                                     r, ((wave * 32 + a * 4 + b) * 64 + lane) * 16, 0, 16 /* sc1 */));
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0) {
-                const int old = __hip_atomic_fetch_add(flags + w + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (old == 15) __hip_atomic_store(flags + w + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        } else {
-#pragma unroll
-            for (int a = 0; a < 8; a++)
-#pragma unroll
-                for (int b = 0; b < 4; b++) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        }
-        for (; gs < seg_end; gs++) {
-            const char* img = slot_of(gs);
-            bf16x8_t fb[4], alo[4], ahi[4];
-            // ---- phase 0
-#pragma unroll
-            for (int b = 0; b < 4; b++) fb[b] = g2::frag<BKC>(img + IMG_BYTES, wn * 64 + b * 16, lane);
-#pragma unroll
-            for (int a = 0; a < 4; a++) alo[a] = g2::frag<AK>(img, wm * 128 + a * 16, lane);
-            issue_a(gs + 2);
-            bar();
-            mfma_half(0, alo, fb);
-            bar();
-            // ---- phase 1
-#pragma unroll
-            for (int a = 0; a < 4; a++) ahi[a] = g2::frag<AK>(img, wm * 128 + (4 + a) * 16, lane);
-            asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // own pieces of step gs+1 landed
-            issue_b(gs + 2);
-            bar();
-            mfma_half(1, ahi, fb);
-            bar();
-        }
-        if (starts_in) {
-            // fragment-native fp32 partial, write-through (sc1); then count this wave in
-            __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-                parts + (long long)w * PART_BYTES, (short)0, PART_BYTES, 0x00020000);
-#pragma unroll
-            for (int a = 0; a < 8; a++)
-#pragma unroll
-                for (int b = 0; b < 4; b++)
-                    __builtin_amdgcn_raw_buffer_store_b128(
-                        __builtin_bit_cast(u32x4, acc[a][b]), r,
-                        ((wave * 32 + a * 4 + b) * 64 + lane) * 16, 0, 16 /* sc1 */);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0) __hip_atomic_fetch_add(flags + w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else if (!skip_epilogue(p, acc)) {
-            const int m0 = (t / ntn) * BM + wm * 128, n0 = (t % ntn) * BN + wn * 64;
-            // DGELU keeps the generic loop: its interior form spills ~50 VGPRs in this kernel
-            if (EPI != EPI_BF16_DGELU && !p.epi_generic && m0 + 128 <= p.M && n0 + 64 <= p.N)
-                staged_epilogue16_interior<EPI>(p, acc, stg, lane, m0, n0);
-            else
-                staged_epilogue16<EPI>(p, acc, stg, lane, m0, n0);
-        }
-    }
-    if (any && !lagging) bar();  // balance the stagger barrier
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_setprio(0);
-}
-}  // namespace g3
 
 // ============================================================================ bf16 GEMM, 256x128
 // Two workgroups per CU.  A 256x128x32 block tile on 256 threads = 4 waves (2 M x 2 N), one
@@ -1055,14 +529,6 @@ __device__ __forceinline__ void group_order(int t, int ntm, int ntn, int& tm, in
 template <bool AK, bool BKC, int EPI>
 __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
     __shared__ __attribute__((aligned(1024))) char smem[NSLOT * SLOT_BYTES];
-    // phase offset (debug flag 256*n): the second resident workgroup of each CU (dispatch slots
-    // 256..511) starts n x s_sleep(127) later, so the two workgroups of a CU reach their epilogues
-    // at different times and one's stores overlap the other's main loop
-    if (p.stagger) {
-        const int lin = blockIdx.y * gridDim.x + blockIdx.x;
-        if (lin >= 256 && lin < 512)
-            for (int k = 0; k < p.stagger; k++) __builtin_amdgcn_s_sleep(127);
-    }
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 1, wn = wave & 1;
@@ -1254,13 +720,12 @@ __global__ __launch_bounds__(256) void slab_reduce_k(float* __restrict__ C, long
 }
 
 // engine selection (gemm_bf16_set_variant; default from VIT_GEMM, else 2):
-//   1 = 128x128 register-staged, 2 = 256x256 one workgroup per CU, 3 = 2 as stream-K persistent
-//   (launches with >= 1 tile per CU; the rest, e.g. split-K wgrad, take 2), 4 = 256x128 two per CU,
-//   5 = 2 as a persistent launch over whole tiles (no hand-offs; split-K wgrad takes 2),
-//   6 = 2 persistent with the next tile's prologue under an LDS-free epilogue (g2::gemm_kernel_p)
+//   1 = 128x128 register-staged everywhere, 2 = production (256x256 one workgroup per CU; split-K
+//   weight gradients on 256x128), 4 = 256x128 two per CU everywhere.  Debug flag 2 skips the
+//   epilogues (main-loop-only timing; results are garbage).
 static int g_variant = -1;
 static int g_debug_flags = 0;
-static bool known_variant(int v) { return v == 1 || v == 3 || v == 4 || v == 5 || v == 6; }
+static bool known_variant(int v) { return v == 1 || v == 2 || v == 4; }
 static int gemm_variant() {
     if (g_variant < 0) {
         const char* e = getenv("VIT_GEMM");
@@ -1277,14 +742,7 @@ GemmParams make_gemm_params(const GemmArgs& a, int kchunk) {
     p.A = a.A; p.B = a.B; p.C = a.C; p.C2 = a.C2; p.aux = a.aux; p.bias = a.bias; p.dbias = a.dbias; p.colsum_out = a.colsum_out;
     p.lda = a.lda; p.ldb = a.ldb; p.ldc = a.ldc; p.ldaux = a.ldaux;
     p.M = a.M; p.N = a.N; p.K = a.K; p.kchunk = kchunk;
-    static const int same = getenv("VIT_DEBUG_SAME_TILE") ? 1 : 0;
-    p.debug_same_tile = same;
     p.no_epi = (g_debug_flags & 2) ? 1 : 0;
-    p.epi_generic = (g_debug_flags & 32) ? 1 : 0;
-    p.stagger = (g_debug_flags >> 8) & 63;
-    p.group_m = (g_debug_flags >> 16) & 63;
-    p.nt = (g_debug_flags & 64) ? 1 : 0;
-    p.dbg_l2 = (g_debug_flags & 128) ? 1 : 0;
     p.mx_q = a.mx_q;
     p.mx_s = a.mx_s;
     p.mx_rg = (int)(mx_rows_padded(a.M) / 32);
@@ -1294,10 +752,8 @@ GemmParams make_gemm_params(const GemmArgs& a, int kchunk) {
 
 // split-K for one-block-per-CU kernels: the smallest split whose last wave of blocks fills
 // >= 90% of the 256 CUs (or the best fill up to 32), keeping >= 16 K-tiles per split
-// slots: the CUs the launch may fill (256; fewer when it shares the GPU with other streams, debug
-// flag 8 / 16: a half / a quarter)
 static int choose_split_waves(int tiles, int nk) {
-    const int slots = (g_debug_flags & 16) ? 64 : ((g_debug_flags & 8) ? 128 : 256);
+    const int slots = 256;
     int best = 1;
     double best_eff = 0.0;
     for (int s = 1; s <= 32 && nk / s >= 16; s++) {
@@ -1339,6 +795,7 @@ void gemm_f32(const GemmArgs& a, hipStream_t s) {
         default: set_error("gemm_f32: unsupported epilogue %d", a.epi); return;
     }
     after_launch("gemm_f32");
+    count_hit(VIT_HIT_GEMM_F32 + a.epi);
 }
 
 bool gemm_bf16_supported(const GemmArgs& a) {
@@ -1372,13 +829,9 @@ static void launch_bf16(const GemmArgs& a, const GemmParams& p, dim3 grid, hipSt
 
 template <bool AK, bool BKC>
 static void launch_g2(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStream_t s) {
-    const bool deep = (g_debug_flags & 4) != 0;  // debug flag 4: prefetch depth 3 (A/B)
     switch (a.epi) {
 #define VIT_CASE(E) \
-    case E:                                                                    \
-        if (deep) g2::gemm_kernel<AK, BKC, E, 3><<<grid, g2::NT, 0, s>>>(p);      \
-        else g2::gemm_kernel<AK, BKC, E, 2><<<grid, g2::NT, 0, s>>>(p);           \
-        break;
+    case E: g2::gemm_kernel<AK, BKC, E, 2><<<grid, g2::NT, 0, s>>>(p); break;
         VIT_CASE(EPI_F32_STORE)
         VIT_CASE(EPI_F32_ACC)
         VIT_CASE(EPI_F32_ATOMIC)
@@ -1387,24 +840,6 @@ static void launch_g2(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStre
         VIT_CASE(EPI_F32_RESID)
         VIT_CASE(EPI_BF16_DGELU)
         VIT_CASE(EPI_F32_SLAB)
-        VIT_CASE(EPI_BF16_GELU_D)
-        VIT_CASE(EPI_BF16_MUL)
-#undef VIT_CASE
-        default: set_error("gemm_bf16: unsupported epilogue %d", a.epi); return;
-    }
-}
-
-template <bool AK, bool BKC>
-static void launch_g2p(const GemmArgs& a, const GemmParams& p, int P, hipStream_t s) {
-    switch (a.epi) {
-#define VIT_CASE(E) \
-    case E: g2::gemm_kernel_p<AK, BKC, E><<<P, g2::NT, 0, s>>>(p); break;
-        VIT_CASE(EPI_F32_STORE)
-        VIT_CASE(EPI_F32_ACC)
-        VIT_CASE(EPI_BF16_STORE)
-        VIT_CASE(EPI_BF16_GELU)
-        VIT_CASE(EPI_F32_RESID)
-        VIT_CASE(EPI_BF16_DGELU)
         VIT_CASE(EPI_BF16_GELU_D)
         VIT_CASE(EPI_BF16_MUL)
 #undef VIT_CASE
@@ -1481,69 +916,15 @@ static void gemm_bf16_g4(const GemmArgs& a, hipStream_t s) {
     else if (!a.a_kcontig && !a.b_kcontig) launch_g4<false, false>(b, p, grid, s);
     else launch_g4<false, true>(b, p, grid, s);
     after_launch("gemm_bf16_256x128");
+    count_hit(VIT_HIT_GEMM_256x128 + b.epi);
     if (slab) {
         slab_reduce_k<<<grid_blocks((long long)a.M * a.N / 4), 256, 0, s>>>(
             (float*)a.C, a.ldc, slab, a.M, a.N, split);
         after_launch("gemm_slab_reduce");
+        count_hit(VIT_HIT_SPLITK_REDUCE);
     }
     // bias gradient of a wgrad (M-contig A = dout^T): column sums of dout over the K rows
     if (a.dbias && !a.a_kcontig) colsum_bf16(a.dbias, (const bf16_t*)a.A, a.K, a.M, a.lda, s);
-}
-
-static int num_cus() {
-    static int n = -1;
-    if (n < 0) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-            n = 256;
-        if (n > 1000) n = 1000;  // flags[] capacity
-    }
-    return n;
-}
-size_t gemm_sk_bytes() { return g3::FLAG_BYTES + (size_t)num_cus() * g3::PART_BYTES; }
-
-template <bool AK, bool BKC>
-static void launch_g3(int epi, const GemmParams& p, int P, char* ws, int S, int whole, hipStream_t s) {
-    switch (epi) {
-#define VIT_CASE(E) \
-    case E: g3::gemm_kernel<AK, BKC, E><<<P, g3::NT, 0, s>>>(p, ws, S, whole); break;
-        VIT_CASE(EPI_F32_STORE)
-        VIT_CASE(EPI_F32_ACC)
-        VIT_CASE(EPI_BF16_STORE)
-        VIT_CASE(EPI_BF16_GELU)
-        VIT_CASE(EPI_F32_RESID)
-        VIT_CASE(EPI_BF16_DGELU)
-#undef VIT_CASE
-        default: set_error("gemm_bf16: unsupported epilogue %d", epi); return;
-    }
-}
-
-// persistent launch (g3): stream-K when the launch has at least one tile per CU, or (whole) one
-// contiguous range of whole tiles per workgroup on min(tiles, CUs) workgroups; false = not taken
-static bool gemm_bf16_g3(const GemmArgs& a, hipStream_t s, bool whole) {
-    const int ncu = num_cus();
-    const long long tiles = (long long)cdiv(a.M, g3::BM) * cdiv(a.N, g3::BN);
-    const int S = a.K / g3::BK;
-    // the stream-K engine has its own epilogue copies for the original six epilogues only
-    if (a.epi == EPI_F32_ATOMIC || a.epi == EPI_F32_SLAB || a.epi == EPI_BF16_GELU_D || a.epi == EPI_BF16_MUL)
-        return false;
-    if ((!whole && tiles < ncu) || a.K % g3::BK || S < 2 || tiles * S >= (1LL << 31)) return false;
-    char* ws = nullptr;
-    if (!whole) {
-        ws = a.sk_ws ? a.sk_ws : (char*)sk_workspace(gemm_sk_bytes());
-        if (!ws) return true;  // error already set
-    }
-    const int P = whole ? (int)std::min<long long>(tiles, ncu) : ncu;
-    GemmParams p = make_gemm_params(a, a.K);
-    p.tiles = (int)tiles;
-    const int wh = whole ? 1 : 0;
-    if (a.a_kcontig && a.b_kcontig) launch_g3<true, true>(a.epi, p, P, ws, S, wh, s);
-    else if (a.a_kcontig && !a.b_kcontig) launch_g3<true, false>(a.epi, p, P, ws, S, wh, s);
-    else if (!a.a_kcontig && !a.b_kcontig) launch_g3<false, false>(a.epi, p, P, ws, S, wh, s);
-    else launch_g3<false, true>(a.epi, p, P, ws, S, wh, s);
-    after_launch(whole ? "gemm_bf16_persistent" : "gemm_bf16_streamk");
-    return true;
 }
 
 void gemm_bf16(const GemmArgs& a, hipStream_t s) {
@@ -1557,8 +938,6 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s) {
                   a.M, a.N, a.K, a.lda, a.ldb);
         return;
     }
-    if (gemm_variant() == 3 && a.M >= 256 && a.N >= 256 && gemm_bf16_g3(a, s, false)) return;
-    if (gemm_variant() == 5 && a.M >= 256 && a.N >= 256 && gemm_bf16_g3(a, s, true)) return;
     if (gemm_variant() == 4 && a.K % g4::KTILE == 0 && a.M >= 256 && a.N >= 128 &&
         (a.epi != EPI_F32_ATOMIC || a.N % 4 == 0)) {
         gemm_bf16_g4(a, s);
@@ -1567,16 +946,15 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s) {
     // split-K weight gradients (M/N-contiguous operands, K = the token count) run on the 256x128
     // two-per-CU engine: 3-9 % faster than 256x256 on every ViT-B/16 wgrad shape (r02,
     // tools/bench_gemm.py), the other GEMMs are faster on 256x256
-    if ((gemm_variant() == 2 || gemm_variant() == 6) && a.epi == EPI_F32_ATOMIC && !a.a_kcontig && !a.b_kcontig &&
-        a.K % g4::KTILE == 0 && a.M >= 256 && a.N >= 128 && a.N % 4 == 0 && !(g_debug_flags & (1 << 23)) &&
+    if (gemm_variant() == 2 && a.epi == EPI_F32_ATOMIC && !a.a_kcontig && !a.b_kcontig &&
+        a.K % g4::KTILE == 0 && a.M >= 256 && a.N >= 128 && a.N % 4 == 0 &&
         (a.splitk > 0 || !a.ws ||
          (size_t)choose_split_g4(cdiv(a.M, g4::BM) * cdiv(a.N, g4::BN), a.K / g4::KTILE) * a.M * a.N * sizeof(float) <=
              a.ws_bytes)) {
         gemm_bf16_g4(a, s);
         return;
     }
-    const bool big = a.K % g2::KTILE == 0 && a.M >= 256 && a.N >= 256 && gemm_variant() != 1 &&
-                     !getenv("VIT_G2_KK_ONLY");
+    const bool big = a.K % g2::KTILE == 0 && a.M >= 256 && a.N >= 256 && gemm_variant() != 1;
     if (big) {
         const int tiles = cdiv(a.M, g2::BM) * cdiv(a.N, g2::BN);
         int split = 1;
@@ -1597,28 +975,18 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s) {
         }
         GemmParams p = make_gemm_params(b, kchunk);
         p.tiles = tiles;
-        // persistent form (variant 6): whole-K launches with at least two tiles per CU
-        const int ncu = num_cus();
-        if (gemm_variant() == 6 && split == 1 && a.epi != EPI_F32_ATOMIC && !a.dbias && a.N % 256 == 0 &&
-            tiles >= 2 * ncu && ncu % 8 == 0) {
-            const int P = ncu;
-            if (a.a_kcontig && a.b_kcontig) launch_g2p<true, true>(b, p, P, s);
-            else if (a.a_kcontig && !a.b_kcontig) launch_g2p<true, false>(b, p, P, s);
-            else if (!a.a_kcontig && !a.b_kcontig) launch_g2p<false, false>(b, p, P, s);
-            else launch_g2p<false, true>(b, p, P, s);
-            after_launch("gemm_bf16_256_persistent");
-            return;
-        }
         dim3 grid(tiles, split);
         if (a.a_kcontig && a.b_kcontig) launch_g2<true, true>(b, p, grid, s);
         else if (a.a_kcontig && !a.b_kcontig) launch_g2<true, false>(b, p, grid, s);
         else if (!a.a_kcontig && !a.b_kcontig) launch_g2<false, false>(b, p, grid, s);
         else launch_g2<false, true>(b, p, grid, s);
         after_launch("gemm_bf16_256");
+        count_hit(VIT_HIT_GEMM_256x256 + b.epi);
         if (slab) {
             slab_reduce_k<<<grid_blocks((long long)a.M * a.N / 4), 256, 0, s>>>(
                 (float*)a.C, a.ldc, slab, a.M, a.N, split);
             after_launch("gemm_slab_reduce");
+        count_hit(VIT_HIT_SPLITK_REDUCE);
         }
         return;
     }
@@ -1635,6 +1003,7 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s) {
     else if (!a.a_kcontig && !a.b_kcontig) launch_bf16<false, false>(a, p, grid, s);
     else launch_bf16<false, true>(a, p, grid, s);
     after_launch("gemm_bf16");
+    count_hit(VIT_HIT_GEMM_128 + a.epi);
     if (a.colsum_out && epi_aux16(a.epi))  // the 128x128 kernel has no fused column sums
         colsum_bf16(a.colsum_out, (const bf16_t*)a.C, a.M, a.N, a.ldc, s);
 }

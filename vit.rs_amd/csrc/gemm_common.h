@@ -17,14 +17,8 @@ struct GemmParams {
     long long lda, ldb, ldc, ldaux;
     int M, N, K;
     int kchunk;  // K range per split (multiple of the K tile)
-    int debug_same_tile;
     int no_epi;  // diagnostic (gemm_bf16_set_debug): skip the epilogue, keep the accumulators live
-    int epi_generic;  // A/B (debug flag 32): the generic (bounds-checked) staged epilogue everywhere
     int tiles;   // output tiles of the launch (the grid is tiles x K-splits)
-    int stagger;  // first-round start delay of every other workgroup, in s_sleep(127) units
-    int group_m;  // > 0: tiles walk groups of group_m M-rows column by column (L2 reuse of B panels)
-    int dbg_l2;   // debug flag 128: epilogue rows taken mod 256 (its HBM traffic becomes L2 hits; output garbage)
-    int nt;       // debug flag 64: epilogue stores / aux loads non-temporal (streaming, L2 evict-first)
     uint8_t* mx_q;  // fused MX output (GemmArgs::mx_q / mx_s); mx_rg = padded rows / 32
     uint8_t* mx_s;
     int mx_rg;
@@ -84,15 +78,12 @@ __device__ __forceinline__ int split_index(int tiles) {
     return s;
 }
 
-// epilogue 16-B global access, optionally non-temporal (p.nt: the output / aux streams are touched
-// once, so they should not evict the operand panels the main loop re-reads from L2)
+// epilogue 16-B global access
 typedef unsigned int epi_u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void epi_st16(const GemmParams& p, void* q, epi_u32x4 v) {
-    if (p.nt) __builtin_nontemporal_store(v, reinterpret_cast<epi_u32x4*>(q));
-    else *reinterpret_cast<epi_u32x4*>(q) = v;
+__device__ __forceinline__ void epi_st16(const GemmParams&, void* q, epi_u32x4 v) {
+    *reinterpret_cast<epi_u32x4*>(q) = v;
 }
-__device__ __forceinline__ epi_u32x4 epi_ld16(const GemmParams& p, const void* q) {
-    if (p.nt) return __builtin_nontemporal_load(reinterpret_cast<const epi_u32x4*>(q));
+__device__ __forceinline__ epi_u32x4 epi_ld16(const GemmParams&, const void* q) {
     return *reinterpret_cast<const epi_u32x4*>(q);
 }
 
@@ -271,7 +262,6 @@ constexpr int STG_WAVE_BYTES = 64 * STG_LD * 4;  // 17,408 B per wave
 template <int EPI>
 __device__ __forceinline__ void staged_pass_interior(const GemmParams& p, const float* st, int rr,
                                                      int cc, int mrow, int n, float (&cs)[8]) {
-    if (p.dbg_l2) mrow &= 255;
     const int cc_lane = cc >> 3;  // the lane's column group (lane bits 0-2): mx_out8's block lanes
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -407,7 +397,7 @@ __device__ __forceinline__ void staged_pass(const GemmParams& p, const float* st
 }
 template <int EPI>
 __device__ __forceinline__ bool staged_interior(const GemmParams& p, int m0, int n0) {
-    return EPI != EPI_F32_ATOMIC && !p.epi_generic && m0 + 128 <= p.M && n0 + 64 <= p.N;
+    return EPI != EPI_F32_ATOMIC && m0 + 128 <= p.M && n0 + 64 <= p.N;
 }
 // fused bias gradient of the next GEMM: column sums of the DGELU output
 template <int EPI>
@@ -427,145 +417,6 @@ __device__ __forceinline__ void staged_colsum(const GemmParams& p, int lane, int
 #pragma unroll
                 for (int j = 0; j < 8; j++)
                     if (n0 + cc + j < p.N) atomicAdd(p.colsum_out + n0 + cc + j, cs[j]);
-            }
-        }
-    }
-}
-
-// ------------------------------------------------------------- LDS-free (direct) epilogue
-// For the persistent engine, whose ring holds the next tile's prologue while this epilogue runs.
-// The staged epilogue moves the accumulators through LDS so that a lane owns 8 consecutive
-// columns; here the same ownership comes from one v_permlane16_swap per accumulator dword: of the
-// 16x16 tiles b, b+1 of a row block (lane (i, g) holds row i, columns 4g..4g+3 of each), lane
-// groups g=1 <-> g=0 and g=3 <-> g=2 trade between the tiles, leaving lane (i, g) with 8
-// consecutive fp32 of row i: columns 16(b + (g & 1)) + 8(g >> 1) .. +7.  Every global access stays
-// 16 B per lane (a wave instruction covers 16 rows x 64 B).  Columns must be in range (the
-// persistent engine takes N % 256 == 0); rows >= M are skipped.  bias: this lane's 2 x 8 bias
-// values (loaded by the caller).
-__device__ __forceinline__ void pl16_swap(float& x, float& y) {
-    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
-    x = __uint_as_float(r[0]);
-    y = __uint_as_float(r[1]);
-}
-__device__ __forceinline__ int direct_col(int lane) { return ((lane >> 4) & 1) * 16 + (lane >> 5) * 8; }
-template <int EPI>
-__device__ __forceinline__ void direct_epilogue(const GemmParams& p, f32x4_t (&acc)[8][4], const float (&bv)[2][8],
-                                                int lane, int m0, int n0) {
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    const int i = lane & 15;
-    const int cq = direct_col(lane);
-    constexpr bool AUX16 = epi_aux16(EPI);
-    constexpr bool AUX32 = EPI == EPI_F32_RESID || EPI == EPI_F32_ACC;
-    float cs[2][8];
-#pragma unroll
-    for (int pr = 0; pr < 2; pr++)
-#pragma unroll
-        for (int j = 0; j < 8; j++) cs[pr][j] = 0.f;
-    // two halves of 4 row blocks: every aux load of a half is issued before its first use
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-        u32x4 ax[AUX16 ? 8 : (AUX32 ? 16 : 1)];
-        if constexpr (AUX16 || AUX32) {
-#pragma unroll
-            for (int aa = 0; aa < 4; aa++)
-#pragma unroll
-                for (int pr = 0; pr < 2; pr++) {
-                    const long long row = min(m0 + (4 * h + aa) * 16 + i, p.M - 1);
-                    const int col = n0 + pr * 32 + cq;
-                    if constexpr (AUX16) {
-                        ax[aa * 2 + pr] = epi_ld16(p, (const bf16_t*)p.aux + row * p.ldaux + col);
-                    } else {
-                        const float* src = EPI == EPI_F32_RESID ? (const float*)p.aux + row * p.ldaux + col
-                                                                : (const float*)p.C + row * p.ldc + col;
-                        ax[(aa * 2 + pr) * 2] = epi_ld16(p, src);
-                        ax[(aa * 2 + pr) * 2 + 1] = epi_ld16(p, src + 4);
-                    }
-                }
-        }
-#pragma unroll
-        for (int aa = 0; aa < 4; aa++) {
-            const int a = 4 * h + aa;
-            const int rowi = m0 + a * 16 + i;
-            const long long row = rowi;
-#pragma unroll
-            for (int pr = 0; pr < 2; pr++) {
-                const f32x4_t x = acc[a][2 * pr], y = acc[a][2 * pr + 1];
-                float v[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
-#pragma unroll
-                for (int e = 0; e < 4; e++) pl16_swap(v[e], v[4 + e]);
-#pragma unroll
-                for (int j = 0; j < 8; j++) v[j] += bv[pr][j];
-                if (rowi >= p.M) continue;
-                const int col = n0 + pr * 32 + cq;
-                const long long off = row * p.ldc + col;
-                auto pack8 = [](const float (&w)[8]) {
-                    return u32x4{pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3]), pack_bf16x2(w[4], w[5]),
-                                 pack_bf16x2(w[6], w[7])};
-                };
-                auto st_f32 = [&](float* q) {
-                    epi_st16(p, q, u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
-                                         __float_as_uint(v[3])});
-                    epi_st16(p, q + 4, u32x4{__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]),
-                                             __float_as_uint(v[7])});
-                };
-                if constexpr (EPI == EPI_F32_STORE) {
-                    st_f32((float*)p.C + off);
-                } else if constexpr (AUX32) {
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        v[j] += __uint_as_float(ax[(aa * 2 + pr) * 2][j]);
-                        v[4 + j] += __uint_as_float(ax[(aa * 2 + pr) * 2 + 1][j]);
-                    }
-                    st_f32((float*)p.C + off);
-                } else if constexpr (EPI == EPI_BF16_STORE) {
-                    epi_st16(p, (bf16_t*)p.C + off, pack8(v));
-                } else if constexpr (EPI == EPI_BF16_GELU || EPI == EPI_BF16_GELU_D) {
-                    float gv[8], dv[8];
-#pragma unroll
-                    for (int j = 0; j < 8; j++) {
-                        if constexpr (EPI == EPI_BF16_GELU) gv[j] = gelu_fast_f(v[j]);
-                        else gelu_pair_fast_f(v[j], gv[j], dv[j]);
-                    }
-                    epi_st16(p, (bf16_t*)p.C + off, EPI == EPI_BF16_GELU ? pack8(v) : pack8(dv));
-                    epi_st16(p, (bf16_t*)p.C2 + off, pack8(gv));
-                } else if constexpr (AUX16) {
-                    const u32x4 h8 = ax[aa * 2 + pr];
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        const float lo = __uint_as_float(h8[j] << 16), hi = __uint_as_float(h8[j] & 0xffff0000u);
-                        if constexpr (EPI == EPI_BF16_DGELU) {
-                            v[2 * j] *= gelu_grad_fast_f(lo);
-                            v[2 * j + 1] *= gelu_grad_fast_f(hi);
-                        } else {
-                            v[2 * j] *= lo;
-                            v[2 * j + 1] *= hi;
-                        }
-                    }
-#pragma unroll
-                    for (int j = 0; j < 8; j++) cs[pr][j] += v[j];
-                    epi_st16(p, (bf16_t*)p.C + off, pack8(v));
-                }
-            }
-        }
-    }
-    if constexpr (AUX16) {
-        if (p.colsum_out) {  // column sums over the wave's rows: reduce over the 16 row lanes
-#pragma unroll
-            for (int pr = 0; pr < 2; pr++)
-#pragma unroll
-                for (int j = 0; j < 8; j++) {
-                    float t = cs[pr][j];
-                    t += __shfl_xor(t, 1, 64);
-                    t += __shfl_xor(t, 2, 64);
-                    t += __shfl_xor(t, 4, 64);
-                    t += __shfl_xor(t, 8, 64);
-                    cs[pr][j] = t;
-                }
-            if (i == 0) {
-#pragma unroll
-                for (int pr = 0; pr < 2; pr++)
-#pragma unroll
-                    for (int j = 0; j < 8; j++) atomicAdd(p.colsum_out + n0 + pr * 32 + cq + j, cs[pr][j]);
             }
         }
     }

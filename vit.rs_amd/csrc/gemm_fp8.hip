@@ -340,6 +340,7 @@ void gemm_fp8(const GemmArgs& a, hipStream_t s) {
         default: set_error("gemm_fp8: unsupported epilogue %d", a.epi); return;
     }
     after_launch("gemm_fp8");
+    count_hit(VIT_HIT_GEMM_FP8 + a.epi);
 }
 
 template <typename TX>

@@ -147,6 +147,45 @@ __global__ void to_bf16_k(bf16_t* __restrict__ out, const float* __restrict__ in
         out[i] = f2bf(in[i]);
 }
 
+// Device arena layout (no GPU needed; vit_layout_query exposes it): layer-major in REVERSE layer
+// order [head | layer L-1 | ... | layer 0 | embed], each tensor 64-element aligned, so backward
+// finalises one contiguous range per layer.  off[ti*L + l] = element offset of tensor ti, layer l
+// (unlayered tensors: l = 0); chunk c = [chunk_off[c], chunk_off[c+1]): c = 0 head + final LN,
+// 1..L layers L-1..0 (backward's completion order), L+1 embedding.
+void compute_layout(int C, int L, int T, int KP, int NC, long long (&canon_size)[20], long long& n_params,
+                    std::vector<long long>& off, long long (&chunk_off)[66], int& n_chunks, long long& arena_elems) {
+    const long long C_ = C, K = KP;
+    const long long sz[20] = {C_ * K, C_, C_, (long long)T * C_,
+                              L * C_, L * C_, L * 3 * C_ * C_, L * 3 * C_, L * C_ * C_, L * C_,
+                              L * C_, L * C_, L * 4 * C_ * C_, L * 4 * C_, L * C_ * 4 * C_, L * C_,
+                              C_, C_, (long long)NC * C_, NC};
+    n_params = 0;
+    for (int i = 0; i < 20; i++) {
+        canon_size[i] = sz[i];
+        n_params += sz[i];
+    }
+    off.assign(20 * L, 0);
+    long long cur = 0;
+    auto place = [&](int ti, int l, long long n) {
+        off[ti * L + l] = cur;
+        cur += (n + 63) & ~63LL;
+    };
+    n_chunks = L + 2;
+    chunk_off[0] = 0;
+    const int head[4] = {P_HEADW, P_HEADB, P_LNFW, P_LNFB};
+    for (int ti : head) place(ti, 0, canon_size[ti]);
+    chunk_off[1] = cur;
+    for (int c = 1; c <= L; c++) {
+        const int l = L - c;
+        for (int ti = P_LN1W; ti <= P_FCPROJB; ti++) place(ti, l, canon_size[ti] / L);
+        chunk_off[c + 1] = cur;
+    }
+    const int emb[4] = {P_PATCH_W, P_PATCH_B, P_CLS, P_WPE};
+    for (int ti : emb) place(ti, 0, canon_size[ti]);
+    chunk_off[L + 2] = cur;
+    arena_elems = cur;
+}
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -251,6 +290,7 @@ struct Trainer {
     // snapshot arena (same layout as grads): snapshot == final grads bitwise proves every chunk
     // was final when the comm stream reduced it (at world 1 the sum itself is an identity)
     float* dp_snap = nullptr;
+    bool dp_probe_on = false;
 
     // ---- timing
     bool timing = false;
@@ -318,36 +358,7 @@ struct Trainer {
     }
 
     void build_layout() {
-        const long long C_ = C, K = KP;
-        long long sz[20] = {C_ * K, C_, C_, (long long)T * C_,
-                            L * C_, L * C_, L * 3 * C_ * C_, L * 3 * C_, L * C_ * C_, L * C_,
-                            L * C_, L * C_, L * 4 * C_ * C_, L * 4 * C_, L * C_ * 4 * C_, L * C_,
-                            C_, C_, (long long)NC * C_, NC};
-        n_params = 0;
-        for (int i = 0; i < 20; i++) {
-            canon_size[i] = sz[i];
-            n_params += sz[i];
-        }
-        off.assign(20 * L, 0);
-        long long cur = 0;
-        auto place = [&](int ti, int l, long long n) {
-            off[ti * L + l] = cur;
-            cur += (n + 63) & ~63LL;
-        };
-        n_chunks = L + 2;
-        chunk_off[0] = 0;
-        const int head[4] = {P_HEADW, P_HEADB, P_LNFW, P_LNFB};
-        for (int ti : head) place(ti, 0, canon_size[ti]);
-        chunk_off[1] = cur;
-        for (int c = 1; c <= L; c++) {
-            const int l = L - c;
-            for (int ti = P_LN1W; ti <= P_FCPROJB; ti++) place(ti, l, per_layer(ti));
-            chunk_off[c + 1] = cur;
-        }
-        const int emb[4] = {P_PATCH_W, P_PATCH_B, P_CLS, P_WPE};
-        for (int ti : emb) place(ti, 0, canon_size[ti]);
-        chunk_off[L + 2] = cur;
-        arena_elems = cur;
+        compute_layout(C, L, T, KP, NC, canon_size, n_params, off, chunk_off, n_chunks, arena_elems);
     }
 
     // canonical <-> device copies (host staging)
@@ -560,14 +571,18 @@ struct Trainer {
                     wtq[k].q = alloc<uint8_t>(L * ns[k] * ks[k]);
                     wtq[k].s = alloc<uint8_t>((long long)L * mx_scale_bytes(ks[k], (int)ns[k]));
                 }
-                // A-operand scratch per micro-batch stream: rows x (widest K = 4C) bytes + scales
+                // A-operand scratch per micro-batch stream: rows x (widest K = 4C) bytes + scales.
+                // Stream k runs only when there are > k micro-batches, so it holds at most
+                // B/(k+1) images' rows.
                 for (int k = 0; k < MAXMB; k++) {
-                    act_q[k] = alloc<uint8_t>(BT * 4 * C);
-                    act_s[k] = alloc<uint8_t>((long long)mx_scale_bytes(BT, 4 * C));
-                    act_q2[k] = alloc<uint8_t>(BT * 4 * C);
-                    act_s2[k] = alloc<uint8_t>((long long)mx_scale_bytes(BT, 4 * C));
+                    const long long rows = (long long)(B / (k + 1)) * T;
+                    if (rows <= 0) continue;
+                    act_q[k] = alloc<uint8_t>(rows * 4 * C);
+                    act_s[k] = alloc<uint8_t>((long long)mx_scale_bytes(rows, 4 * C));
+                    act_q2[k] = alloc<uint8_t>(rows * 4 * C);
+                    act_s2[k] = alloc<uint8_t>((long long)mx_scale_bytes(rows, 4 * C));
                     // the padding rows' scales (never written by the fused epilogues) stay 0
-                    VIT_HIP(hipMemset(act_s2[k], 0, mx_scale_bytes(BT, 4 * C)));
+                    VIT_HIP(hipMemset(act_s2[k], 0, mx_scale_bytes(rows, 4 * C)));
                 }
                 const char* fe = getenv("VIT_FP8_FUSE");
                 fuse_mx = !(fe && fe[0] == '0');
@@ -654,12 +669,14 @@ struct Trainer {
     void refresh_transposed() {
         const int kinds[4] = {P_QKVW, P_ATTPROJW, P_FCW, P_FCPROJW};
         const int rows[4] = {3 * C, C, 4 * C, C}, cols[4] = {C, C, C, 4 * C};
+        tbeg(TC_MISC, 0);
         for (int k = 0; k < 4; k++) {
             const long long stride = L > 1 ? off[kinds[k] * L + 1] - off[kinds[k] * L] : 0;
             // negative stride: pass the lowest-addressed layer (layers are stored in reverse)
             const int l0 = stride < 0 ? L - 1 : 0;
             transpose_bf16(WT(kinds[k], l0), W(kinds[k], l0), rows[k], cols[k], L, stride < 0 ? -stride : stride, s);
         }
+        tend();
         if (fp8()) refresh_fp8();
     }
     // MXFP8 weight copies: W [N][K] from the fp32 master, WT [Cin][OC] from the bf16 transpose;
@@ -1070,7 +1087,7 @@ struct Trainer {
         const long long o = chunk_off[c], n = chunk_off[c + 1] - chunk_off[c];
         ncclResult_t r = ncclAllReduce(grads + o, grads + o, (size_t)n, ncclFloat32, ncclSum, comm, s_comm);
         if (r != ncclSuccess) set_error("ncclAllReduce(chunk %d): %s", c, ncclGetErrorString(r));
-        if (dp_snap)
+        if (dp_probe_on)
             VIT_HIP(hipMemcpyAsync(dp_snap + o, grads + o, (size_t)n * 4, hipMemcpyDeviceToDevice, s_comm));
     }
     void finish_allreduce() {
@@ -1078,6 +1095,8 @@ struct Trainer {
         if (!overlap) {
             ncclResult_t r = ncclAllReduce(grads, grads, (size_t)arena_elems, ncclFloat32, ncclSum, comm, s);
             if (r != ncclSuccess) set_error("ncclAllReduce: %s", ncclGetErrorString(r));
+            if (dp_probe_on)
+                VIT_HIP(hipMemcpyAsync(dp_snap, grads, (size_t)arena_elems * 4, hipMemcpyDeviceToDevice, s));
             return;
         }
         VIT_HIP(hipEventRecord(comm_done, s_comm));
@@ -1406,6 +1425,23 @@ int vit_trainer_sync(vit_trainer_t* h) {
 }
 void* vit_trainer_stream(vit_trainer_t* h) { return (void*)h->t.s; }
 
+int vit_layout_query(const vit_config_t* cfg, long long* tensor_off, long long* chunk_off, long long* arena_elems) {
+    if (!cfg || cfg->num_layers < 1 || cfg->num_layers > 64 || cfg->patch < 1 || cfg->img < cfg->patch ||
+        cfg->channels < 1 || cfg->num_classes < 1) {
+        set_error("vit_layout_query: bad config");
+        return -1;
+    }
+    const int L = cfg->num_layers, np = (cfg->img / cfg->patch) * (cfg->img / cfg->patch);
+    long long canon[20], n_params = 0, co[66], arena = 0;
+    std::vector<long long> off;
+    int n_chunks = 0;
+    vit::compute_layout(cfg->channels, L, np + 1, cfg->in_ch * cfg->patch * cfg->patch, cfg->num_classes, canon,
+                        n_params, off, co, n_chunks, arena);
+    if (tensor_off) memcpy(tensor_off, off.data(), off.size() * sizeof(long long));
+    if (chunk_off) memcpy(chunk_off, co, (size_t)(n_chunks + 1) * sizeof(long long));
+    if (arena_elems) *arena_elems = arena;
+    return n_chunks;
+}
 int vit_dp_unique_id_size(void) { return (int)sizeof(ncclUniqueId); }
 int vit_dp_get_unique_id(char* out) {
     ncclUniqueId id;
@@ -1439,7 +1475,7 @@ int vit_trainer_dp_init(vit_trainer_t* h, int rank, int world, const char* uid, 
 }
 int vit_trainer_get_dp_snapshot(vit_trainer_t* h, float* host) {
     auto& t = h->t;
-    if (!t.dp_snap) {
+    if (!t.dp_probe_on) {
         set_error("vit_trainer_get_dp_snapshot: option dp_probe is off");
         return 1;
     }
@@ -1475,12 +1511,11 @@ int vit_trainer_set_option(vit_trainer_t* h, const char* name, int value) {
     } else if (n == "dgrad_transposed") {
         t.dgrad_wt = value != 0;
     } else if (n == "dp_probe") {
-        if (value && !t.dp_snap) {
+        if (value && !t.dp_snap) {  // allocated once, kept until destroy
             t.dp_snap = t.alloc<float>(t.arena_elems);
             if (t.dp_snap) VIT_HIP(hipMemset(t.dp_snap, 0, t.arena_elems * 4));
-        } else if (!value) {
-            t.dp_snap = nullptr;  // the arena stays allocated until destroy
         }
+        t.dp_probe_on = value != 0 && t.dp_snap != nullptr;
     } else {
         set_error("vit_trainer_set_option: unknown option '%s'", n.c_str());
         return 1;
