@@ -480,7 +480,7 @@ int fa::attn_bwd_variant() {  // read per launch (host-side, cheap) so tests can
     const char* e = getenv("VIT_ATTN_BWD");
     if (!e) return 0;
     const std::string v(e);
-    return v == "one" ? 1 : v == "pair" ? 2 : 0;
+    return v == "one" ? 1 : v == "pair" ? 2 : v == "p4" ? 4 : 0;
 }
 int fa::attn_cu_count() {
     static int n = [] {

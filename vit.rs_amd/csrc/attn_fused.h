@@ -135,6 +135,48 @@ __device__ __forceinline__ void store4(bf16_t* dst, f32x4_t v, float mul) {
         make_uint2(pack_bf16x2(v[0] * mul, v[1] * mul), pack_bf16x2(v[2] * mul, v[3] * mul));
 }
 
+// raw buffer loads: offsets past num_records (bytes) return 0, so zero-padded rows need no branch
+// (a "zero, then load if in range" pattern makes hipcc wait vmcnt(0) on the whole queue before the
+// zeroing, which turned the backward's one-slice-ahead prefetch into a blocking load)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 buf_ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ float buf_ldf(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+
+// Swizzled LDS images of the one-pass backward at head size 64 (rows of 128 B), conflict-free for
+// every access (tools/lds_banks.py model, MI355X_MICROARCH.md §LDS):
+//   Q / dO slices [32 q][64 d], stride 128 B, 16-B chunk index XOR gray(row): ds_read_b64 row
+//     fragments, ds_read_b64_tr_b16 transposed fragments and the ds_write_b128 staging;
+//   dS^T [key][32 q], stride 64 B, 8-B chunk index XOR gray(row): the ds_write_b64 of phase A and
+//     the transposed reads of phase B.
+// (the padded strides they replace cost 2x on the transposed slice reads and 4x on the dS^T writes)
+__device__ __forceinline__ int gray8(int r) { return (r ^ (r >> 1)) & 7; }
+__device__ __forceinline__ int sl_off(int row, int byte) { return row * 128 + ((((byte >> 4) ^ gray8(row)) << 4) | (byte & 15)); }
+__device__ __forceinline__ int ds_off(int row, int byte) { return row * 64 + ((((byte >> 3) ^ gray8(row)) << 3) | (byte & 7)); }
+__device__ __forceinline__ bf16x4_t lds4(const char* img, int off) { return *reinterpret_cast<const bf16x4_t*>(img + off); }
+__device__ __forceinline__ bf16x4_t lds4tr(const char* img, int off) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4_t, img + off));
+}
+// swizzled slice: row fragment (rows r0+i, k-step s) and transposed fragment (k rows kb.., cols c0+i)
+__device__ __forceinline__ bf16x8_t frag_row_sw(const char* img, int r0, int s, int lane) {
+    const int i = lane & 15, g = lane >> 4;
+    return __builtin_shufflevector(lds4(img, sl_off(r0 + i, 64 * s + 8 * g)), lds4(img, sl_off(r0 + i, 64 * s + 32 + 8 * g)),
+                                   0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ bf16x8_t frag_tr_sw(const char* img, int kb, int c0, int lane) {
+    const int i = lane & 15, g = lane >> 4, r = kb + 4 * g + (i >> 2), b = 2 * c0 + 8 * (i & 3);
+    return __builtin_shufflevector(lds4tr(img, sl_off(r, b)), lds4tr(img, sl_off(r + 16, b)), 0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ bf16x8_t frag_tr_ds(const char* img, int kb, int c0, int lane) {
+    const int i = lane & 15, g = lane >> 4, r = kb + 4 * g + (i >> 2), b = 2 * c0 + 8 * (i & 3);
+    return __builtin_shufflevector(lds4tr(img, ds_off(r, b)), lds4tr(img, ds_off(r + 16, b)), 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
 // ---------------------------------------------------------------------------------- forward
 template <int HS, int NKT>  // key tiles of 16 covering TP = 16*NKT (a multiple of 32)
 constexpr int fwd_lds_bytes() { return NKT * 16 * (Geo<HS>::SK + Geo<HS>::SV) * 2; }
@@ -604,6 +646,29 @@ __global__ __launch_bounds__(256, (bwd_occ<HS, NKT>())) void attn_bwd_pair_k(
 // attn_bwd1_k (one workgroup per item, blocking prologue) where the persistent LDS does not fit.
 constexpr int BWD_SDS = 48;          // dS^T [key][query] row stride: (SDS/2) = 8*odd dwords (tr reads)
 constexpr int ATTN_PART_ROWS = 16;   // column-sum partial rows per (b,h) a backward kernel may write
+// slice-image and dS^T row strides (elements): the swizzled images at head size 64 (sl_off, ds_off)
+// VIT_ATTN_SW_SLICE: swizzled 128-B slice rows (conflict-free transposed reads, more address
+// registers) vs the padded stride; the dS^T swizzle is always on at head size 64
+#ifndef VIT_ATTN_SW_SLICE
+#define VIT_ATTN_SW_SLICE 1
+#endif
+template <int HS>
+constexpr bool sw_slice() { return HS == 64 && VIT_ATTN_SW_SLICE; }
+#ifndef VIT_ATTN_SW_DS
+#define VIT_ATTN_SW_DS 1
+#endif
+template <int HS>
+constexpr bool sw_ds() { return HS == 64 && VIT_ATTN_SW_DS; }
+template <int HS>
+constexpr int slice_stride() { return sw_slice<HS>() ? 64 : Geo<HS>::SK; }
+template <int HS>
+constexpr int sds_stride() { return sw_ds<HS>() ? 32 : BWD_SDS; }
+// 16-B piece cc of slice row t into a slice image
+template <int HS>
+__device__ __forceinline__ void slice_put(bf16_t* img, int t, int cc, uint4 v) {
+    if constexpr (sw_slice<HS>()) *reinterpret_cast<uint4*>(reinterpret_cast<char*>(img) + sl_off(t, 16 * cc)) = v;
+    else *reinterpret_cast<uint4*>(img + t * Geo<HS>::SK + cc * 8) = v;
+}
 
 template <int HS, int KK = 2>
 struct BwdRegs {  // per-wave state of the one-pass backward: the wave owns KK 16-key tiles
@@ -633,6 +698,7 @@ __device__ __forceinline__ void bwd_slice_a(BwdRegs<HS, KK>& R, const bf16_t* Qc
                                             int nk = 0) {
     using G = Geo<HS>;
     constexpr int KS = G::KS, DT = G::DT, SK = G::SK;
+    constexpr bool SW = sw_slice<HS>(), SWD = sw_ds<HS>();  // swizzled slice / dS^T images (sl_off / ds_off)
     const int i = lane & 15, g = lane >> 4;
     f32x4_t P[KK][2], dS[KK][2];  // [kk][u]: lane (i,g) -> [q = 16u+4g+r][key = 16kk+i]
 #pragma unroll
@@ -640,8 +706,13 @@ __device__ __forceinline__ void bwd_slice_a(BwdRegs<HS, KK>& R, const bf16_t* Qc
         bf16x8_t qr[KS], dr[KS];
 #pragma unroll
         for (int s = 0; s < KS; s++) {
-            qr[s] = frag_row<HS>(Qc, SK, 16 * u, s, lane);
-            dr[s] = frag_row<HS>(Dc, SK, 16 * u, s, lane);
+            if constexpr (SW) {
+                qr[s] = frag_row_sw(reinterpret_cast<const char*>(Qc), 16 * u, s, lane);
+                dr[s] = frag_row_sw(reinterpret_cast<const char*>(Dc), 16 * u, s, lane);
+            } else {
+                qr[s] = frag_row<HS>(Qc, SK, 16 * u, s, lane);
+                dr[s] = frag_row<HS>(Dc, SK, 16 * u, s, lane);
+            }
         }
         float lq[4], dq[4];
 #pragma unroll
@@ -675,8 +746,14 @@ __device__ __forceinline__ void bwd_slice_a(BwdRegs<HS, KK>& R, const bf16_t* Qc
     }
 #pragma unroll
     for (int dt = 0; dt < DT; dt++) {
-        const bf16x8_t td = frag_tr(Dc, SK, 0, 16 * dt, lane);
-        const bf16x8_t tq = frag_tr(Qc, SK, 0, 16 * dt, lane);
+        bf16x8_t td, tq;
+        if constexpr (SW) {
+            td = frag_tr_sw(reinterpret_cast<const char*>(Dc), 0, 16 * dt, lane);
+            tq = frag_tr_sw(reinterpret_cast<const char*>(Qc), 0, 16 * dt, lane);
+        } else {
+            td = frag_tr(Dc, SK, 0, 16 * dt, lane);
+            tq = frag_tr(Qc, SK, 0, 16 * dt, lane);
+        }
 #pragma unroll
         for (int kk = 0; kk < KK; kk++) {
             R.dv[kk][dt] = mfma(td, pb[kk], R.dv[kk][dt]);
@@ -685,14 +762,17 @@ __device__ __forceinline__ void bwd_slice_a(BwdRegs<HS, KK>& R, const bf16_t* Qc
     }
     // dS^T -> LDS [key][query] (bf16, the MFMA operand's values): 4 consecutive queries per lane
     // and tile.  Without MASK, padded keys carry P != 0 (their K, V rows are zero): their dS is
-    // finite and multiplies the zero K rows in dQ.
+    // finite and multiplies the zero K rows in dQ.  dSk = the wave's first key row.
 #pragma unroll
     for (int kk = 0; kk < KK; kk++)
 #pragma unroll
         for (int u = 0; u < 2; u++) {
             const bf16x4_t h4 = u ? __builtin_shufflevector(db[kk], db[kk], 4, 5, 6, 7)
                                   : __builtin_shufflevector(db[kk], db[kk], 0, 1, 2, 3);
-            *reinterpret_cast<bf16x4_t*>(dSk + (16 * kk + i) * BWD_SDS + 16 * u + 4 * g) = h4;
+            if constexpr (SWD)
+                *reinterpret_cast<bf16x4_t*>(reinterpret_cast<char*>(dSk) + ds_off(16 * kk + i, 32 * u + 8 * g)) = h4;
+            else
+                *reinterpret_cast<bf16x4_t*>(dSk + (16 * kk + i) * BWD_SDS + 16 * u + 4 * g) = h4;
         }
 }
 
@@ -701,14 +781,20 @@ template <int HS, int NSL, int NW>
 __device__ __forceinline__ void bwd_slice_b(const bf16_t* Ks, const bf16_t* dSs, bf16_t* dq, long long C3, int q0,
                                             int T, float scale, int w, int lane) {
     constexpr int DT = Geo<HS>::DT, SV = Geo<HS>::SV;
+    constexpr bool SW = sw_ds<HS>();
     const int i = lane & 15, g = lane >> 4;
-    for (int j = w; j < 2 * DT; j += NW) {
-        const int dt = j >> 1, u = j & 1;
+    // 2*DT output tiles over the NW waves; waves w and w+4 share a SIMD, so with NW = 7 and 8 tiles
+    // the tile past the first seven goes to wave 3 (alone on its SIMD) rather than wave 0
+    auto tile = [&](int jj) {
+        const int dt = jj >> 1, u = jj & 1;
         // two accumulation chains (even / odd key blocks) halve the dependent-MFMA latency
         f32x4_t acc = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < NSL; ks++) {
-            const bf16x8_t a = frag_tr(Ks, SV, 32 * ks, 16 * dt, lane), b = frag_tr(dSs, BWD_SDS, 32 * ks, 16 * u, lane);
+            const bf16x8_t a = frag_tr(Ks, SV, 32 * ks, 16 * dt, lane);
+            bf16x8_t b;
+            if constexpr (SW) b = frag_tr_ds(reinterpret_cast<const char*>(dSs), 32 * ks, 16 * u, lane);
+            else b = frag_tr(dSs, BWD_SDS, 32 * ks, 16 * u, lane);
             if (ks & 1) acc1 = mfma(a, b, acc1);
             else acc = mfma(a, b, acc);
         }
@@ -716,7 +802,10 @@ __device__ __forceinline__ void bwd_slice_b(const bf16_t* Ks, const bf16_t* dSs,
         // lane (i,g): d = 16dt + 4g + r, q = q0 + 16u + i (padded queries: dS = 0)
         const int q = q0 + 16 * u + i;
         if (q < T) store4(dq + (long long)q * C3 + 16 * dt + 4 * g, acc, scale);
-    }
+    };
+    constexpr bool BAL = NW == 7 && 2 * DT == 8;  // one loop body (two inlined copies spill)
+    const int jlast = BAL ? (w == 3 ? 7 : w) : 2 * DT - 1, jstep = BAL ? 4 : NW;
+    for (int j = w; j <= jlast; j += jstep) tile(j);
 }
 
 // end of an item: dK, dV of the wave's keys; the wave's column sums of dQ | dK | dV into its own
@@ -783,13 +872,14 @@ __device__ __forceinline__ void bwd_item_end(BwdRegs<HS, KK>& R, bf16_t* dq, lon
 template <int HS, int NKT>
 struct Bwd1 {
     static constexpr int TP = NKT * 16, NW = NKT / 2, NT = NW * 64, NSL = TP / 32;
-    static constexpr int SK = Geo<HS>::SK;   // Q / dO slices: row and transposed reads
+    static constexpr int SK = slice_stride<HS>();  // Q / dO slices: row and transposed reads
     static constexpr int SV = Geo<HS>::SV;   // K image: transposed reads only
+    static constexpr int SDS = sds_stride<HS>();
     static constexpr int K_OFF = 0;
     static constexpr int Q_OFF = K_OFF + TP * SV * 2;
     static constexpr int D_OFF = Q_OFF + 2 * 32 * SK * 2;
     static constexpr int S_OFF = D_OFF + 2 * 32 * SK * 2;
-    static constexpr int L_OFF = S_OFF + TP * BWD_SDS * 2;
+    static constexpr int L_OFF = S_OFF + TP * SDS * 2;
     static constexpr int BYTES = L_OFF + 2 * TP * 4;
     static constexpr int PER = (32 * Geo<HS>::CH + NT - 1) / NT;  // 16-B pieces per thread per slice operand
 };
@@ -854,8 +944,8 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
         for (int j = 0; j < PER; j++) {
             const int idx = j * NT + tid, t = idx / CH, c = idx - t * CH;
             if (idx < 32 * CH) {
-                *reinterpret_cast<uint4*>(Qs + buf * 32 * SK + t * SK + c * 8) = pq[j];
-                *reinterpret_cast<uint4*>(Ds + buf * 32 * SK + t * SK + c * 8) = pd[j];
+                slice_put<HS>(Qs + buf * 32 * SK, t, c, pq[j]);
+                slice_put<HS>(Ds + buf * 32 * SK, t, c, pd[j]);
             }
         }
     };
@@ -889,7 +979,7 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
     for (int sl = 0; sl < NSL; sl++) {
         const int q0 = sl * 32, cur = sl & 1;
         if (sl + 1 < NSL) fetch_slice(q0 + 32);  // lands in registers during phase A
-        bwd_slice_a<HS>(R, Qs + cur * 32 * SK, Ds + cur * 32 * SK, lse_s + q0, del_s + q0, dSs + key0 * BWD_SDS, c, lane);
+        bwd_slice_a<HS>(R, Qs + cur * 32 * SK, Ds + cur * 32 * SK, lse_s + q0, del_s + q0, dSs + key0 * Z::SDS, c, lane);
         __syncthreads();
         if (sl + 1 < NSL) put_slice(cur ^ 1);  // its buffer was last read in the previous slice
         bwd_slice_b<HS, NSL, NW>(Ks, dSs, dq, C3, q0, T, scale, w, lane);
@@ -904,13 +994,13 @@ template <int HS, int NKT, int KK = 2>
 struct Bwdp {
     using G = Geo<HS>;
     static constexpr int TP = NKT * 16, NW = NKT / KK, NT = NW * 64, NSL = TP / 32, CH = G::CH;
-    static constexpr int SK = G::SK, SV = G::SV;
+    static constexpr int SK = G::SK, SV = G::SV, SL = slice_stride<HS>(), SDS = sds_stride<HS>();
     static constexpr int K_OFF = 0;                          // K images [2][TP][SV]: current / next item
     static constexpr int V_OFF = K_OFF + 2 * TP * SV * 2;    // next item's V rows [TP][SK]
-    static constexpr int Q_OFF = V_OFF + TP * SK * 2;        // Q slices [2][32][SK]
-    static constexpr int D_OFF = Q_OFF + 2 * 32 * SK * 2;    // dO slices [2][32][SK]
-    static constexpr int S_OFF = D_OFF + 2 * 32 * SK * 2;    // dS^T [TP][BWD_SDS]
-    static constexpr int L_OFF = S_OFF + TP * BWD_SDS * 2;   // lse [2][TP] (item parity)
+    static constexpr int Q_OFF = V_OFF + TP * SK * 2;        // Q slices [2][32][SL]
+    static constexpr int D_OFF = Q_OFF + 2 * 32 * SL * 2;    // dO slices [2][32][SL]
+    static constexpr int S_OFF = D_OFF + 2 * 32 * SL * 2;    // dS^T [TP][SDS]
+    static constexpr int L_OFF = S_OFF + TP * SDS * 2;       // lse [2][TP] (item parity)
     static constexpr int E_OFF = L_OFF + 2 * TP * 4;         // delta [2][32] (slice parity)
     static constexpr int BYTES = E_OFF + 2 * 32 * 4;
     static constexpr int PER = (32 * CH + NT - 1) / NT;      // 16-B pieces per thread, slice operand
@@ -923,7 +1013,7 @@ template <int HS, int NKT, int KK = 2>
 constexpr bool bwdp_fits() {
     using Z = Bwdp<HS, NKT, KK>;
     return Z::BYTES <= 160 * 1024 && (64 % Geo<HS>::CH) == 0 && HS <= 64 && Z::NW <= ATTN_PART_ROWS &&
-           (KK == 2 ? bwd1_fits<HS, NKT>() : Z::NW <= 16);
+           NKT % KK == 0 && (KK == 2 ? bwd1_fits<HS, NKT>() : KK == 4 ? (HS == 64 && Z::NW <= 4) : Z::NW <= 16);
 }
 
 template <int HS, int NKT, int KK>
@@ -935,7 +1025,8 @@ __global__ __launch_bounds__(NKT / KK * 64, 1) void attn_bwdp_k(bf16_t* __restri
                                                                int C, int NH, int BH, float* __restrict__ dsum) {
     using G = Geo<HS>;
     using Z = Bwdp<HS, NKT, KK>;
-    constexpr int TP = Z::TP, NW = Z::NW, NT = Z::NT, NSL = Z::NSL, SK = Z::SK, SV = Z::SV;
+    constexpr int TP = Z::TP, NW = Z::NW, NT = Z::NT, NSL = Z::NSL, SK = Z::SK, SV = Z::SV, SL = Z::SL;
+    static_assert((32 * G::CH) % 64 == 0 && NT % 64 == 0, "slice pieces are whole waves");
     constexpr int KS = G::KS, CH = G::CH, PER = Z::PER, PERS = Z::PERS;
     __shared__ __attribute__((aligned(16))) char lds[Z::BYTES];
     bf16_t* Kimg = reinterpret_cast<bf16_t*>(lds + Z::K_OFF);
@@ -946,7 +1037,8 @@ __global__ __launch_bounds__(NKT / KK * 64, 1) void attn_bwdp_k(bf16_t* __restri
     float* lse_s = reinterpret_cast<float*>(lds + Z::L_OFF);
     float* del_s = reinterpret_cast<float*>(lds + Z::E_OFF);
     const long long C3 = 3LL * C;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int key0 = w * 16 * KK;
     const float scale = 1.0f / sqrtf((float)HS);
     const float c = LOG2E * scale;
@@ -954,57 +1046,62 @@ __global__ __launch_bounds__(NKT / KK * 64, 1) void attn_bwdp_k(bf16_t* __restri
     auto row_of = [&](const bf16_t* p, int bh) { return p + (long long)(bh / NH) * T * C + (bh % NH) * HS; };
     // slice rows (Q, dO, O) of item bh at q0 -> registers; into LDS with delta = rowsum(dO * O)
     uint4 pq[PER], pd[PER], po[PER];
-    auto fetch_slice = [&](int bh, int q0) {
-        const bf16_t* qb = qkv_of(bh);
-        const bf16_t* db = row_of(dout, bh);
-        const bf16_t* ob = row_of(out, bh);
+    // Buffer loads: rows >= T read 0 without a branch.  No branch around any prefetch either: lanes
+    // past the last piece repeat a piece (same bytes to the same LDS address), so the compiler sees
+    // every prefetch register consumed on every path and never drains vmcnt to re-use one.
+    struct Src { __amdgpu_buffer_rsrc_t q, d, o, kv, l; };  // an item's buffer descriptors
+    auto src_of = [&](int bh) {
+        Src r;
+        r.q = buf_rsrc(qkv_of(bh), (uint32_t)(T * C3 * 2));
+        r.d = buf_rsrc(row_of(dout, bh), (uint32_t)(T * C * 2));
+        r.o = buf_rsrc(row_of(out, bh), (uint32_t)(T * C * 2));
+        // K | V columns from K's first column: every byte of rows >= T is past the end
+        r.kv = buf_rsrc(qkv_of(bh) + C, (uint32_t)(T * C3 * 2 - 2 * C));
+        r.l = buf_rsrc(lse + (long long)bh * T, (uint32_t)(T * 4));
+        return r;
+    };
+    auto fetch_slice = [&](const Src& sr, int q0) {
+        const auto rq = sr.q, rd = sr.d, ro = sr.o;
 #pragma unroll
         for (int j = 0; j < PER; j++) {
-            const int idx = j * NT + tid, t = idx / CH, cc = idx - t * CH;
-            pq[j] = pd[j] = po[j] = make_uint4(0, 0, 0, 0);
-            if (idx < 32 * CH && q0 + t < T) {
-                pq[j] = *reinterpret_cast<const uint4*>(qb + (long long)(q0 + t) * C3 + cc * 8);
-                pd[j] = *reinterpret_cast<const uint4*>(db + (long long)(q0 + t) * C + cc * 8);
-                po[j] = *reinterpret_cast<const uint4*>(ob + (long long)(q0 + t) * C + cc * 8);
-            }
+            const int idx = (j * NT + tid) % (32 * CH), t = idx / CH, cc = idx - t * CH;
+            const uint32_t r = (uint32_t)(q0 + t);
+            pq[j] = buf_ld16(rq, r * (uint32_t)(C3 * 2) + 16 * cc);
+            pd[j] = buf_ld16(rd, r * (uint32_t)(C * 2) + 16 * cc);
+            po[j] = buf_ld16(ro, r * (uint32_t)(C * 2) + 16 * cc);
         }
     };
     auto put_slice = [&](int buf) {
 #pragma unroll
         for (int j = 0; j < PER; j++) {
-            const int idx = j * NT + tid, t = idx / CH, cc = idx - t * CH;
+            const int idx = (j * NT + tid) % (32 * CH), t = idx / CH, cc = idx - t * CH;
             float dl = dot8_bf16(po[j], pd[j]);  // the CH lanes of row t are consecutive
 #pragma unroll
             for (int o = 1; o < CH; o <<= 1) dl += __shfl_xor(dl, o, 64);
-            if (idx < 32 * CH) {
-                *reinterpret_cast<uint4*>(Qs + buf * 32 * SK + t * SK + cc * 8) = pq[j];
-                *reinterpret_cast<uint4*>(Ds + buf * 32 * SK + t * SK + cc * 8) = pd[j];
-                if (cc == 0) del_s[buf * 32 + t] = dl;
-            }
+            slice_put<HS>(Qs + buf * 32 * SL, t, cc, pq[j]);
+            slice_put<HS>(Ds + buf * 32 * SL, t, cc, pd[j]);
+            if (cc == 0) del_s[buf * 32 + t] = dl;
         }
     };
     // next item's K and V rows [32 rb, 32 rb + 32) -> registers; into its K image / the V rows
     uint4 ps[PERS];
     float lse_n = INFINITY;
-    auto fetch_side = [&](int bh, int rb) {
-        const bf16_t* kb = qkv_of(bh) + C;
+    auto fetch_side = [&](const Src& sr, int rb) {
+        const auto rk = sr.kv;
 #pragma unroll
         for (int j = 0; j < PERS; j++) {
-            const int idx = j * NT + tid, op = idx >= 32 * CH, rem = idx - op * 32 * CH, t = rem / CH,
+            const int idx = (j * NT + tid) % (64 * CH), op = idx >= 32 * CH, rem = idx - op * 32 * CH, t = rem / CH,
                       cc = rem - t * CH, row = 32 * rb + t;
-            ps[j] = make_uint4(0, 0, 0, 0);
-            if (idx < 64 * CH && row < T) ps[j] = *reinterpret_cast<const uint4*>(kb + op * C + (long long)row * C3 + cc * 8);
+            ps[j] = buf_ld16(rk, (uint32_t)row * (uint32_t)(C3 * 2) + (uint32_t)(op * C * 2) + 16 * cc);
         }
     };
     auto put_side = [&](int kbuf, int rb) {
 #pragma unroll
         for (int j = 0; j < PERS; j++) {
-            const int idx = j * NT + tid, op = idx >= 32 * CH, rem = idx - op * 32 * CH, t = rem / CH,
+            const int idx = (j * NT + tid) % (64 * CH), op = idx >= 32 * CH, rem = idx - op * 32 * CH, t = rem / CH,
                       cc = rem - t * CH, row = 32 * rb + t;
-            if (idx < 64 * CH) {
-                bf16_t* dst = op ? Vst + row * SK : Kimg + kbuf * TP * SV + row * SV;
-                *reinterpret_cast<uint4*>(dst + cc * 8) = ps[j];
-            }
+            bf16_t* dst = op ? Vst + row * SK : Kimg + kbuf * TP * SV + row * SV;
+            *reinterpret_cast<uint4*>(dst + cc * 8) = ps[j];
         }
     };
     auto load_kv = [&](BwdRegs<HS, KK>& R, int kbuf) {  // the wave's fragments from the staged rows
@@ -1019,7 +1116,7 @@ __global__ __launch_bounds__(NKT / KK * 64, 1) void attn_bwdp_k(bf16_t* __restri
     int bh = blockIdx.x;
     if (bh >= BH) return;
     // prologue (first item): K image, V rows, lse, slice 0 — one blocking round trip
-    fetch_slice(bh, 0);
+    fetch_slice(src_of(bh), 0);
     {
         bf16_t* const img[2] = {Kimg, Vst};
         const int st[2] = {SV, SK};
@@ -1037,30 +1134,32 @@ __global__ __launch_bounds__(NKT / KK * 64, 1) void attn_bwdp_k(bf16_t* __restri
     for (int n = 0; bh < BH; n++, bh += gridDim.x) {
         const int bhn = bh + gridDim.x;
         const bool has_next = bhn < BH;
+        const int bhc = has_next ? bhn : bh;  // the next item, or this one again after the last
+        const Src s_cur = src_of(bh), s_nxt = src_of(bhc);
         bf16_t* dq = dqkv + (long long)(bh / NH) * T * C3 + (bh % NH) * HS;
         const float* lse_cur = lse_s + (n & 1) * TP;
         R.zero();
 #pragma unroll 1
         for (int sl = 0; sl < NSL; sl++, it++) {
             const int cur = it & 1, q0 = sl * 32;
-            const bool next_slice = sl + 1 < NSL || has_next;
             // one step ahead: the next slice (this item's or the next item's first), the next
             // item's K / V row block sl and, with its first block, its lse
-            if (next_slice) fetch_slice(sl + 1 < NSL ? bh : bhn, sl + 1 < NSL ? q0 + 32 : 0);
-            if (has_next) {
-                fetch_side(bhn, sl);
-                if (sl == 0 && tid < TP) lse_n = tid < T ? lse[(long long)bhn * T + tid] : INFINITY;
-            }
-            bwd_slice_a<HS, KK>(R, Qs + cur * 32 * SK, Ds + cur * 32 * SK, lse_cur + q0, del_s + cur * 32,
-                            dSs + key0 * BWD_SDS, c, lane);
+            // (unconditional: past the last item / slice a valid item is re-read into buffers no one
+            // reads again, so the compiler sees every prefetch register consumed on every path and
+            // does not drain vmcnt before re-using them)
+            if (sl + 1 < NSL) fetch_slice(s_cur, q0 + 32);
+            else fetch_slice(s_nxt, 0);
+            fetch_side(s_nxt, sl);
+            // unconditional load (past T: 0); padded keys get +inf when it is put
+            if (sl == 0) lse_n = buf_ldf(s_nxt.l, 4 * tid);
+            bwd_slice_a<HS, KK>(R, Qs + cur * 32 * SL, Ds + cur * 32 * SL, lse_cur + q0, del_s + cur * 32,
+                                dSs + key0 * Z::SDS, c, lane);
             __syncthreads();
             // buffers written here were last read before the barrier above (slice buffer cur^1 by
             // the previous slice, the idle K image by the previous item, the V rows by load_kv)
-            if (next_slice) put_slice(cur ^ 1);
-            if (has_next) {
-                put_side(kb ^ 1, sl);
-                if (sl == 0 && tid < TP) lse_s[((n + 1) & 1) * TP + tid] = lse_n;
-            }
+            put_slice(cur ^ 1);
+            put_side(kb ^ 1, sl);
+            if (sl == 0 && tid < TP) lse_s[((n + 1) & 1) * TP + tid] = tid < T ? lse_n : INFINITY;
             bwd_slice_b<HS, NSL, NW>(Kimg + kb * TP * SV, dSs, dq, C3, q0, T, scale, w, lane);
             __syncthreads();
         }
@@ -1096,6 +1195,18 @@ template <int HS, int NKT>
 int launch_bwd(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t* out, const float* lse, int B,
                int T, int C, int NH, float* part, hipStream_t s) {
     const int v = attn_bwd_variant(), BH = B * NH;
+    // "p4": the persistent one-pass kernel with 64 keys per wave (4 waves, one per SIMD, up to 512
+    // registers each; keys padded to a multiple of 64): measured slower than the default 32 keys per
+    // wave (338 vs 289 us at ViT-B/16 B=256: one wave per SIMD hides no latency)
+    constexpr int NK4 = (NKT + 7) / 8 * 8;
+    if constexpr (bwdp_fits<HS, NK4, 4>()) {
+        if (v == 4) {
+            attn_bwdp_k<HS, NK4, 4><<<std::min(BH, attn_cu_count()), NK4 / 4 * 64, 0, s>>>(dqkv, dout, qkv, out, lse,
+                                                                                          T, C, NH, BH, part);
+            count_hit(VIT_HIT_ATTN_BWD_PERSISTENT);
+            return NK4 / 4;
+        }
+    }
     if constexpr (bwdp_fits<HS, NKT, 2>()) {
         if (v == 0) {
             attn_bwdp_k<HS, NKT, 2><<<std::min(BH, attn_cu_count()), NKT / 2 * 64, 0, s>>>(dqkv, dout, qkv, out, lse,
