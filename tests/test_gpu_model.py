@@ -170,11 +170,10 @@ def test_vit_b16_fp32_and_bf16_vs_oracle_one_image(gpu, oracle32):
 @pytest.mark.parametrize("overlap", [True, False])
 def test_dp_single_rank_rccl_is_identity(gpu, prec_name, overlap):
     """The RCCL path on one GPU: world_size 1 all-reduce (per-layer chunks on the
-    side stream, or one whole-arena call) must leave the gradients equal to no DP and the SGD step
-    that waits on it must produce the same parameters (the tolerance only absorbs the float-atomic
-    summation order of the split-K / column-sum kernels between two runs).  At world 1 the sum is
-    an identity, so this does not see a chunk reduced too early: test_dp_overlap_chunks_are_final
-    does."""
+    side stream, or one whole-arena call) must leave the gradients BIT-IDENTICAL to no DP and the SGD
+    step that waits on it must produce the same parameters bit for bit (every gradient reduction
+    runs in a fixed order: no float atomics).  At world 1 the sum is an identity, so this does not
+    see a chunk reduced too early: test_dp_overlap_chunks_are_final does."""
     v = gpu
     prec = getattr(v, prec_name)
     cfg = v.data.CONFIGS["test_h64"]
@@ -192,8 +191,8 @@ def test_dp_single_rank_rccl_is_identity(gpu, prec_name, overlap):
         p = m.params()
         out.append((g, p))
         m.close()
-    assert rel_err(out[1][0], out[0][0]) <= 1e-6
-    assert rel_err(out[1][1], out[0][1]) <= 1e-6
+    assert np.array_equal(out[1][0], out[0][0])
+    assert np.array_equal(out[1][1], out[0][1])
 
 
 @pytest.mark.parametrize("prec_name", ["VIT_FP32", "VIT_BF16", "VIT_FP8"])
@@ -228,6 +227,38 @@ def test_dp_overlap_chunks_are_final(gpu, prec_name, nmb):
                if not np.array_equal(a, b)]
         assert not bad, bad
     m.close()
+
+
+@pytest.mark.parametrize("prec_name", ["VIT_FP32", "VIT_BF16", "VIT_FP8"])
+@pytest.mark.parametrize("nmb", [1, 2, 4])
+def test_trainer_step_is_bitwise_deterministic(gpu, prec_name, nmb):
+    """Every gradient reduction of the step runs in a fixed order: split-K
+    weight gradients through slabs + an ordered reduce, LayerNorm / bias column sums through
+    per-block partial rows reduced per layer after the micro-batch streams join, the head GEMMs
+    likewise; no float atomics anywhere.  Two trainers and two consecutive steps each, stream
+    concurrency on: gradients, loss and updated parameters bit-identical."""
+    v = gpu
+    prec = getattr(v, prec_name)
+    cfg = v.data.CONFIGS["test_h64"]
+    params = v.data.init_params(cfg, "parity", seed=23)
+    px, lab = v.data.synthetic_batch(cfg, 8, seed=24)
+    runs = []
+    for _ in range(2):
+        m = v.ViT.build(cfg, 8, prec, params=params)
+        m.set_concurrency(True)
+        m.set_option("microbatch", nmb)
+        m.set_batch(px, lab)
+        out = []
+        for _ in range(2):
+            m.train_step(0.05)
+            m.sync()
+            out.append((float(v.lib().vit_trainer_mean_loss(m.h)), m.grads(), m.params()))
+        runs.append(out)
+        m.close()
+    for (l0, g0, p0), (l1, g1, p1) in zip(*runs):
+        assert l0 == l1
+        assert np.array_equal(g0, g1)
+        assert np.array_equal(p0, p1)
 
 
 def test_vit_l16_full_size_step(gpu):
@@ -387,8 +418,8 @@ def test_fp8_trainer_vs_oracle(gpu, oracle32, name, B):
 def test_fp8_fused_mx_epilogues_bit_identical(gpu, monkeypatch):
     """fp8 mode's fused MX outputs (fc fwd's GELU output and fcproj dgrad's GELU' output written
     straight to e4m3 + scales by those GEMMs) against the separate quantize passes (VIT_FP8_FUSE=0):
-    the same loss, logits and gradients up to the wgrad atomics' summation order (1e-5; a wrong
-    block scale would show as ~1e-2), micro-batched (B=8 in 2) and not."""
+    bit-identical loss, logits and gradients (the same GEMM operands and deterministic reductions),
+    micro-batched (B=8 in 2) and not."""
     v = gpu
     cfg = v.data.CONFIGS["test_h64"]
     params = v.data.init_params(cfg, "parity", seed=3)
@@ -404,10 +435,9 @@ def test_fp8_fused_mx_epilogues_bit_identical(gpu, monkeypatch):
             m.backward()
             res[fuse] = (loss, m.logits(), m.grads())
             m.close()
-        # identical GEMM operands; only the split-K wgrad atomics' order may differ run to run
-        assert abs(res["1"][0] - res["0"][0]) <= 1e-6 * abs(res["0"][0])
-        assert rel_err(res["1"][1], res["0"][1]) < 1e-5
-        assert rel_err(res["1"][2], res["0"][2]) < 1e-5
+        assert res["1"][0] == res["0"][0]
+        assert np.array_equal(res["1"][1], res["0"][1])
+        assert np.array_equal(res["1"][2], res["0"][2])
 
 
 def test_fp8_training_reduces_loss(gpu):

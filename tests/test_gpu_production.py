@@ -90,7 +90,8 @@ def test_production_bf16_step_vs_oracle(gpu, ref, nmb):
     assert hits[G2 + 8] == L * nmb              # fc fwd (gelu' / gelu pair)
     assert hits[G2 + 9] == L * nmb              # fcproj dgrad (x stored gelu', fc-bias colsum)
     assert hits[G4 + 7] >= 4 * L                # split-K weight gradients into slabs
-    assert hits[v.HIT_SPLITK_REDUCE] == hits[G4 + 7] + hits[G2 + 7]
+    # every split-K launch reduces its slabs once (the head's fp32 GEMMs included); no atomics
+    assert hits[v.HIT_SPLITK_REDUCE] == hits[G4 + 7] + hits[G2 + 7] + hits[v.HIT_GEMM_F32 + 7]
     assert hits[v.HIT_ATTN_FWD_MFMA] == L * nmb
     assert hits[v.HIT_ATTN_BWD_PERSISTENT] == L * nmb
 
@@ -120,3 +121,14 @@ def test_production_fp8_step_vs_oracle(gpu, ref):
     lrel_f = abs(lf - ref["loss"]) / abs(ref["loss"])
     assert lrel_f <= parity.fp8_limit(lrel_b), (lrel_f, lrel_b)
     assert not bad, bad
+
+
+def test_production_bf16_step_is_bitwise_repeatable(gpu, ref):
+    """The production kernel set (2 micro-batch streams + the weight-gradient stream) reduces every
+    gradient in a fixed order: two steps on fresh trainers give bit-identical gradients."""
+    v = gpu
+    a = _run(v, ref, v.VIT_BF16, 2)
+    b = _run(v, ref, v.VIT_BF16, 2)
+    assert a[0] == b[0]
+    assert np.array_equal(a[1], b[1])
+    assert np.array_equal(a[2], b[2])

@@ -511,8 +511,8 @@ bool attn_fused_supported(int T, int C, int NH) {
 // Column sums of the fused backward's per-(row, h) partials, deterministic two-stage:
 //   part_k : block (s*NH + h, chunk) sums its chunk of the R = B x rows partial rows
 //            part[(r*NH + h)][s*HS + d] -> scratch[chunk][s*C + h*HS + d]
-//   final_k: out[j] += sum over chunks of scratch[chunk][j] (fixed order; one atomicAdd per j, as the
-//            micro-batches' launches add into one bias concurrently)
+//   final_k: out[j] (+)= sum over chunks of scratch[chunk][j] (fixed order; the trainer stores one
+//            row per micro-batch and reduces the rows after the layer)
 // stage 1 of the deterministic qkv-bias column sums: workgroup (section*head, chunk) sums its
 // chunk of the R partial rows for the head's HS columns.  16-B loads: HS/4 lanes cover a row
 // segment, 256/(HS/4) rows are in flight per iteration, four independent accumulators per lane.
@@ -549,18 +549,19 @@ __global__ __launch_bounds__(256) void attn_colsum_part_k(float* __restrict__ sc
     }
 }
 __global__ __launch_bounds__(256) void attn_colsum_final_k(float* __restrict__ out, const float* __restrict__ scratch,
-                                                           int nch, int C3) {
+                                                           int nch, int C3, int store) {
     const int j = blockIdx.x * 256 + threadIdx.x;
     if (j >= C3) return;
     float a = 0.f;
     for (int ch = 0; ch < nch; ch++) a += scratch[(long long)ch * C3 + j];
-    atomicAdd(out + j, a);
+    out[j] = store ? a : out[j] + a;
 }
 
 size_t attn_backward_ws_floats(int B, int T, int C, int NH) {
     // partial rows (up to ATTN_PART_ROWS per (b,h)) + the colsum chunk sums (<= B rows of 3C)
+    // (generic kernels: B*NH*T delta floats + the bias column sums' per-256-row partial rows)
     const size_t per_bh = std::max((size_t)T, (size_t)3 * (C / NH) * (fa::ATTN_PART_ROWS + 1));
-    return (size_t)B * NH * per_bh;
+    return (size_t)B * NH * per_bh + (size_t)cdiv((long long)B * T, 256) * 3 * C;
 }
 
 void attn_forward_fused(bf16_t* out, float* lse, const bf16_t* qkv, int B, int T, int C, int NH,
@@ -599,15 +600,14 @@ void attn_forward_fused(bf16_t* out, float* lse, const bf16_t* qkv, int B, int T
 
 void attn_backward_fused(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t* out,
                          const float* lse, int B, int T, int C, int NH, hipStream_t s,
-                         float* dqkv_colsum, float* ws) {
+                         float* dqkv_colsum, float* ws, bool colsum_store) {
     if (!attn_fused_supported(T, C, NH)) {
         if (!attn_generic_supported(T, C, NH)) {
             set_error("attention_backward_fused: unsupported shape (T=%d C=%d NH=%d)", T, C, NH);
             return;
         }
         // ws: [B*NH*T] delta = rowsum(dO*O)
-        const size_t need = (size_t)B * NH * T * sizeof(float);
-        if (!ws) ws = (float*)workspace(need);
+        if (!ws) ws = (float*)workspace(attn_backward_ws_floats(B, T, C, NH) * sizeof(float));
         if (!ws) return;
         const size_t lds = gen::lds_bytes(T, C / NH, gen::nw_bwd(C / NH));
         const dim3 g(B * NH, gen::CHUNKS);
@@ -628,7 +628,10 @@ void attn_backward_fused(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, co
         }
         after_launch("attention_backward_generic");
         count_hit(VIT_HIT_ATTN_GENERIC);
-        if (dqkv_colsum) colsum_bf16(dqkv_colsum, dqkv, B * T, 3 * C, 3LL * C, s);
+        if (dqkv_colsum) {
+            if (colsum_store) VIT_HIP(hipMemsetAsync(dqkv_colsum, 0, 3 * (size_t)C * sizeof(float), s));
+            colsum_bf16(dqkv_colsum, dqkv, B * T, 3 * C, 3LL * C, s, ws + (size_t)B * NH * T);
+        }
         return;
     }
     const int HS = C / NH;
@@ -650,7 +653,7 @@ void attn_backward_fused(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, co
         const int nch = std::min(8, B);
         float* scratch = part + (size_t)B * rows * NH * 3 * HS;
         attn_colsum_part_k<<<dim3(3 * NH, nch), 256, 0, s>>>(scratch, part, B * rows, NH, C, HS);
-        attn_colsum_final_k<<<cdiv(3 * C, 256), 256, 0, s>>>(dqkv_colsum, scratch, nch, 3 * C);
+        attn_colsum_final_k<<<cdiv(3 * C, 256), 256, 0, s>>>(dqkv_colsum, scratch, nch, 3 * C, colsum_store ? 1 : 0);
         after_launch("attention_colsum_reduce");
     }
 }

@@ -64,6 +64,24 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
     return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
 }
 
+// "bf16 + lo8": a value t kept as hi = bf16(t) plus one signed byte q = rint((t - hi) / (ulp(hi) / 256)),
+// t ~ hi + q * ulp(hi) / 256: a 16-bit significand in 3 bytes, with hi directly usable as a bf16
+// GEMM operand.  ulp(hi)/256 = 2^(E - 142) for hi's biased exponent E (hi of magnitude < 2^-111
+// keeps q = 0).
+__device__ __forceinline__ float lo8_step(float hf) {
+    const uint32_t e = (__float_as_uint(hf) >> 23) & 0xffu;
+    return e > 15u ? __uint_as_float((e - 15u) << 23) : 0.f;
+}
+__device__ __forceinline__ float lo8_decode(float hf, uint32_t q8) {
+    return hf + (float)(int)(int8_t)(uint8_t)q8 * lo8_step(hf);
+}
+__device__ __forceinline__ uint32_t lo8_encode(float t, float hf) {
+    const uint32_t e = (__float_as_uint(hf) >> 23) & 0xffu;
+    const float inv = (e > 15u && e < 255u) ? __uint_as_float((269u - e) << 23) : 0.f;
+    const float q = fminf(fmaxf(rintf((t - hf) * inv), -127.f), 127.f);
+    return (uint32_t)(uint8_t)(int8_t)(int)q;
+}
+
 __device__ __forceinline__ float warp_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -15,7 +15,7 @@ namespace vit {
 enum Epi {
     EPI_F32_STORE = 0,   // C_f32 = acc (+ bias[n])
     EPI_F32_ACC = 1,     // C_f32 += acc (+ bias[n])
-    EPI_F32_ATOMIC = 2,  // atomicAdd(C_f32, acc)   (split-K partials)
+    EPI_F32_ATOMIC = 2,  // C_f32 += acc, K split into fp32 slabs + one fixed-order reduce (no atomics)
     EPI_BF16_STORE = 3,  // C_bf16 = acc (+ bias)
     EPI_BF16_GELU = 4,   // C_bf16 = pre = acc + bias; C2_bf16 = gelu(pre)
     EPI_F32_RESID = 5,   // C_f32 = acc + bias + aux_f32[m*ldaux + n]
@@ -47,7 +47,12 @@ struct GemmArgs {
     long long ldaux = 0;
     const float* bias = nullptr;
     float* dbias = nullptr;  // bf16 wgrad with an M-contig A: dbias[m] += sum_k A(m,k) (fused colsum)
-    float* colsum_out = nullptr;  // EPI_BF16_DGELU / EPI_BF16_MUL: += column sums of the output
+    // EPI_BF16_DGELU / EPI_BF16_MUL column sums of the output, deterministic: the epilogue stores
+    // partial rows colsum_part[cdiv(M,128)][N] (row r = output rows 128r..128r+127; nullptr = thread
+    // workspace) and, with colsum_out set, the launcher adds them into colsum_out in a fixed order.
+    // colsum_part without colsum_out: the caller reduces the rows (the trainer, across micro-batches).
+    float* colsum_out = nullptr;
+    float* colsum_part = nullptr;
     int M = 0, N = 0, K = 0;
     int epi = EPI_F32_STORE;
     int splitk = 0;  // 0 = choose automatically (only EPI_F32_ATOMIC may split)
@@ -100,8 +105,21 @@ void quantize_mx_batched_f32(uint8_t* q, uint8_t* sl, const float* x, long long 
 long long mx_rows_padded(long long rows);
 size_t mx_scale_bytes(long long rows, int K);
 
-// column sums: dbias[n] += sum_m X[m*ld + n]   (X fp32 or bf16)
-void colsum_f32(float* dbias, const float* X, int M, int N, long long ld, hipStream_t s);
-void colsum_bf16(float* dbias, const bf16_t* X, int M, int N, long long ld, hipStream_t s);
+// column sums: dbias[n] += sum_m X[m*ld + n]   (X fp32 or bf16), in a fixed order: one pass when
+// M <= 256, else per-256-row partial rows in ws (nullptr = thread workspace; cdiv(M,256) * N
+// floats) + rows_reduce_add
+void colsum_f32(float* dbias, const float* X, int M, int N, long long ld, hipStream_t s, float* ws = nullptr);
+void colsum_bf16(float* dbias, const bf16_t* X, int M, int N, long long ld, hipStream_t s, float* ws = nullptr);
+// dst[c] += sum_{r < nrows} src[r * ld + c] for c < ncols, the rows added in a fixed order
+// (deterministic): the final step of every partial-row reduction (bias / LayerNorm gradients)
+struct RowsJob {
+    float* dst;
+    const float* src;
+    int nrows;
+    long long ld;
+    int ncols;
+};
+constexpr int ROWS_MAX_JOBS = 8;
+void rows_reduce_add(const RowsJob* jobs, int njobs, hipStream_t s);
 
 }  // namespace vit

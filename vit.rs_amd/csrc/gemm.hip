@@ -189,7 +189,13 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmParams p) {
         for (int b = 0; b < 4; b++) {
             const int n = tn0 + wn * 64 + b * 16 + 4 * g;
             if (n >= p.N) continue;
-            epilogue<EPI>(p, m, n, acc[a][b]);
+            if constexpr (EPI == EPI_F32_SLAB) {  // this K-split's slab (blockIdx.y; ldc = N)
+                const long long off = (long long)blockIdx.y * p.M * p.ldc + (long long)m * p.ldc + n;
+                *reinterpret_cast<float4*>((float*)p.C + off) =
+                    make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
+            } else {
+                epilogue<EPI>(p, m, n, acc[a][b]);
+            }
         }
     }
 }
@@ -672,21 +678,22 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(GemmParams p, int a_kc, in
                     *q = p.bias ? v + p.bias[n] : v;
                 } else if constexpr (EPI == EPI_F32_ACC) {
                     *q += p.bias ? v + p.bias[n] : v;
-                } else {
-                    atomicAdd(q, v);
+                } else {  // EPI_F32_SLAB: this K-split's slab (p.C = slab base, ldc = N)
+                    q[(long long)blockIdx.y * p.M * p.ldc] = v;
                 }
             }
 }
 }  // namespace f32
 
 // ============================================================================ column sums
+// part[blockIdx.y][n] = sum of rows blockIdx.y*rpb .. +rpb-1 of column n (ascending); with
+// add_direct the single row block adds straight into out (one add per column: deterministic)
 template <typename TX>
-__global__ __launch_bounds__(256) void colsum_kernel(float* __restrict__ dbias,
-                                                     const TX* __restrict__ X, int M, int N,
-                                                     long long ld, int rows_per_block) {
+__global__ __launch_bounds__(256) void colsum_part_k(float* __restrict__ out, const TX* __restrict__ X, int M, int N,
+                                                     long long ld, int rpb, int add_direct) {
     const int n = blockIdx.x * 256 + threadIdx.x;
-    const int r0 = blockIdx.y * rows_per_block;
-    const int r1 = min(M, r0 + rows_per_block);
+    const int r0 = blockIdx.y * rpb;
+    const int r1 = min(M, r0 + rpb);
     if (n >= N) return;
     float s = 0.f;
     for (int r = r0; r < r1; r++) {
@@ -695,9 +702,90 @@ __global__ __launch_bounds__(256) void colsum_kernel(float* __restrict__ dbias,
         else
             s += X[(long long)r * ld + n];
     }
-    atomicAdd(dbias + n, s);
+    if (add_direct) out[n] += s;
+    else out[(long long)blockIdx.y * N + n] = s;
 }
 
+// rows_reduce_add: workgroup = 64 columns x 4 row phases of one job; each thread sums the rows
+// r = phase (mod 4) in ascending order, the 4 phases are added in a fixed order
+struct RowsJobs {
+    RowsJob j[ROWS_MAX_JOBS];
+    int blk0[ROWS_MAX_JOBS + 1];
+};
+__global__ __launch_bounds__(256) void rows_reduce_k(RowsJobs jobs) {
+    __shared__ float red[4][64];
+    int jb = 0;
+#pragma unroll 1
+    while (jb + 1 < ROWS_MAX_JOBS && (int)blockIdx.x >= jobs.blk0[jb + 1]) jb++;
+    const RowsJob& J = jobs.j[jb];
+    const int c = (blockIdx.x - jobs.blk0[jb]) * 64 + (threadIdx.x & 63), ph = threadIdx.x >> 6;
+    float s0 = 0.f, s1 = 0.f;
+    if (c < J.ncols) {
+        int r = ph;
+        for (; r + 4 < J.nrows; r += 8) {  // two independent chains: rows ph+8i and ph+4+8i
+            s0 += J.src[(long long)r * J.ld + c];
+            s1 += J.src[(long long)(r + 4) * J.ld + c];
+        }
+        if (r < J.nrows) s0 += J.src[(long long)r * J.ld + c];
+    }
+    red[ph][threadIdx.x & 63] = s0 + s1;
+    __syncthreads();
+    if (ph == 0 && c < J.ncols) J.dst[c] += ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+}
+void rows_reduce_add(const RowsJob* jobs, int njobs, hipStream_t s) {
+    for (int b = 0; b < njobs; b += ROWS_MAX_JOBS) {
+        RowsJobs J{};
+        int nb = 0, k = 0;
+        for (; k < ROWS_MAX_JOBS && b + k < njobs; k++) {
+            J.j[k] = jobs[b + k];
+            J.blk0[k] = nb;
+            nb += J.j[k].nrows > 0 ? cdiv(J.j[k].ncols, 64) : 0;
+        }
+        for (; k <= ROWS_MAX_JOBS; k++) J.blk0[k] = nb;
+        if (nb == 0) continue;
+        rows_reduce_k<<<nb, 256, 0, s>>>(J);
+        after_launch("rows_reduce_add");
+    }
+}
+template <typename TX>
+static void colsum_any(float* dbias, const TX* X, int M, int N, long long ld, hipStream_t s, float* ws) {
+    if (M <= 0 || N <= 0) return;
+    const int rpb = 256, nch = cdiv(M, rpb);
+    if (nch == 1) {
+        colsum_part_k<TX><<<dim3(cdiv(N, 256), 1), 256, 0, s>>>(dbias, X, M, N, ld, rpb, 1);
+        after_launch("colsum");
+        return;
+    }
+    if (!ws) ws = (float*)workspace((size_t)nch * N * sizeof(float));
+    if (!ws) return;
+    colsum_part_k<TX><<<dim3(cdiv(N, 256), nch), 256, 0, s>>>(ws, X, M, N, ld, rpb, 0);
+    after_launch("colsum");
+    RowsJob j{dbias, ws, nch, N, N};
+    rows_reduce_add(&j, 1, s);
+}
+float* colsum_rows_begin(const GemmArgs& a) {
+    if (!epi_aux16(a.epi) || !(a.colsum_out || a.colsum_part)) return nullptr;
+    float* r = a.colsum_part ? a.colsum_part : (float*)workspace((size_t)cdiv(a.M, 128) * a.N * sizeof(float));
+    return r;
+}
+void colsum_rows_end(const GemmArgs& a, float* rows, hipStream_t s) {
+    if (!rows || !a.colsum_out) return;
+    RowsJob j{a.colsum_out, rows, cdiv(a.M, 128), a.N, a.N};
+    rows_reduce_add(&j, 1, s);
+}
+
+// C[m][n] += sum_z slab[z][m][n], any N (the fp32 engine's split-K)
+__global__ __launch_bounds__(256) void slab_reduce1_k(float* __restrict__ C, long long ldc,
+                                                      const float* __restrict__ slab, int M, int N,
+                                                      int splits) {
+    const long long n1 = (long long)M * N;
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n1; e += (long long)gridDim.x * 256) {
+        const int m = (int)(e / N), n = (int)(e - (long long)m * N);
+        float acc = slab[e];
+        for (int z = 1; z < splits; z++) acc += slab[z * n1 + e];
+        C[(long long)m * ldc + n] += acc;
+    }
+}
 // C[m][n] += sum_z slab[z][m][n]   (M x N fp32, ldc == N for the slabs)
 __global__ __launch_bounds__(256) void slab_reduce_k(float* __restrict__ C, long long ldc,
                                                      const float* __restrict__ slab, int M, int N,
@@ -739,7 +827,7 @@ void gemm_set_debug(int flags) { g_debug_flags = flags; }
 
 GemmParams make_gemm_params(const GemmArgs& a, int kchunk) {
     GemmParams p;
-    p.A = a.A; p.B = a.B; p.C = a.C; p.C2 = a.C2; p.aux = a.aux; p.bias = a.bias; p.dbias = a.dbias; p.colsum_out = a.colsum_out;
+    p.A = a.A; p.B = a.B; p.C = a.C; p.C2 = a.C2; p.aux = a.aux; p.bias = a.bias; p.dbias = a.dbias; p.colsum_out = nullptr;
     p.lda = a.lda; p.ldb = a.ldb; p.ldc = a.ldc; p.ldaux = a.ldaux;
     p.M = a.M; p.N = a.N; p.K = a.K; p.kchunk = kchunk;
     p.no_epi = (g_debug_flags & 2) ? 1 : 0;
@@ -773,6 +861,26 @@ static int choose_split(int tiles, int K, int ktile, int want_blocks) {
     return s;
 }
 
+static int grid_blocks(long long n) {
+    long long b = (n + 255) / 256;
+    return (int)(b < 1 ? 1 : (b > 4096 ? 4096 : b));
+}
+// split-K slabs: the caller's buffer (a.ws) or the thread workspace; error when neither fits
+static float* slab_buffer(const GemmArgs& a, int split) {
+    const size_t need = (size_t)split * a.M * a.N * sizeof(float);
+    float* slab = a.ws ? (a.ws_bytes >= need ? a.ws : nullptr) : (float*)workspace(need);
+    if (!slab) set_error("gemm: split-K workspace of %zu bytes unavailable", need);
+    return slab;
+}
+static void slab_reduce(const GemmArgs& a, float* slab, int split, hipStream_t s) {
+    if (a.N % 4 == 0)
+        slab_reduce_k<<<grid_blocks((long long)a.M * a.N / 4), 256, 0, s>>>((float*)a.C, a.ldc, slab, a.M, a.N, split);
+    else
+        slab_reduce1_k<<<grid_blocks((long long)a.M * a.N), 256, 0, s>>>((float*)a.C, a.ldc, slab, a.M, a.N, split);
+    after_launch("gemm_slab_reduce");
+    count_hit(VIT_HIT_SPLITK_REDUCE);
+}
+
 void gemm_f32(const GemmArgs& a, hipStream_t s) {
     if (a.M <= 0 || a.N <= 0) return;
     if (a.mx_q) {
@@ -785,17 +893,28 @@ void gemm_f32(const GemmArgs& a, hipStream_t s) {
     int kchunk = cdiv(cdiv(a.K, split), f32::BK) * f32::BK;
     if (kchunk <= 0) kchunk = f32::BK;
     split = cdiv(a.K > 0 ? a.K : 1, kchunk);
-    GemmParams p = make_gemm_params(a, kchunk);
+    GemmArgs b = a;
+    float* slab = nullptr;
+    if (a.epi == EPI_F32_ATOMIC) {  // one split accumulates in place; more go through slabs
+        if (split > 1) {
+            if (!(slab = slab_buffer(a, split))) return;
+            b.epi = EPI_F32_SLAB; b.C = slab; b.ldc = a.N;
+        } else {
+            b.epi = EPI_F32_ACC;
+        }
+    }
+    GemmParams p = make_gemm_params(b, kchunk);
     dim3 grid(tiles, split);
     int akc = a.a_kcontig, bkc = a.b_kcontig;
-    switch (a.epi) {
+    switch (b.epi) {
         case EPI_F32_STORE: f32::gemm_f32_kernel<EPI_F32_STORE><<<grid, f32::NT, 0, s>>>(p, akc, bkc); break;
         case EPI_F32_ACC: f32::gemm_f32_kernel<EPI_F32_ACC><<<grid, f32::NT, 0, s>>>(p, akc, bkc); break;
-        case EPI_F32_ATOMIC: f32::gemm_f32_kernel<EPI_F32_ATOMIC><<<grid, f32::NT, 0, s>>>(p, akc, bkc); break;
+        case EPI_F32_SLAB: f32::gemm_f32_kernel<EPI_F32_SLAB><<<grid, f32::NT, 0, s>>>(p, akc, bkc); break;
         default: set_error("gemm_f32: unsupported epilogue %d", a.epi); return;
     }
     after_launch("gemm_f32");
-    count_hit(VIT_HIT_GEMM_F32 + a.epi);
+    count_hit(VIT_HIT_GEMM_F32 + b.epi);
+    if (slab) slab_reduce(a, slab, split, s);
 }
 
 bool gemm_bf16_supported(const GemmArgs& a) {
@@ -815,7 +934,7 @@ static void launch_bf16(const GemmArgs& a, const GemmParams& p, dim3 grid, hipSt
     case E: bf::gemm_bf16_kernel<AK, BKC, E><<<grid, bf::NT, 0, s>>>(p); break;
         VIT_CASE(EPI_F32_STORE)
         VIT_CASE(EPI_F32_ACC)
-        VIT_CASE(EPI_F32_ATOMIC)
+        VIT_CASE(EPI_F32_SLAB)
         VIT_CASE(EPI_BF16_STORE)
         VIT_CASE(EPI_BF16_GELU)
         VIT_CASE(EPI_F32_RESID)
@@ -834,7 +953,6 @@ static void launch_g2(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStre
     case E: g2::gemm_kernel<AK, BKC, E, 2><<<grid, g2::NT, 0, s>>>(p); break;
         VIT_CASE(EPI_F32_STORE)
         VIT_CASE(EPI_F32_ACC)
-        VIT_CASE(EPI_F32_ATOMIC)
         VIT_CASE(EPI_BF16_STORE)
         VIT_CASE(EPI_BF16_GELU)
         VIT_CASE(EPI_F32_RESID)
@@ -847,10 +965,6 @@ static void launch_g2(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStre
     }
 }
 
-static int grid_blocks(long long n) {
-    long long b = (n + 255) / 256;
-    return (int)(b < 1 ? 1 : (b > 4096 ? 4096 : b));
-}
 
 template <bool AK, bool BKC>
 static void launch_g4(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStream_t s) {
@@ -898,9 +1012,7 @@ static void gemm_bf16_g4(const GemmArgs& a, hipStream_t s) {
         // split-K partials go to fp32 slabs + one reduce (no float atomics in the GEMM); a single
         // split accumulates in place
         if (split > 1) {
-            const size_t need = (size_t)split * a.M * a.N * sizeof(float);
-            slab = a.ws ? (a.ws_bytes >= need ? a.ws : nullptr) : (float*)workspace(need);
-            if (!slab) { set_error("gemm_bf16: split-K workspace of %zu bytes unavailable", need); return; }
+            if (!(slab = slab_buffer(a, split))) return;
             b.epi = EPI_F32_SLAB;
             b.C = slab;
             b.ldc = a.N;
@@ -910,6 +1022,9 @@ static void gemm_bf16_g4(const GemmArgs& a, hipStream_t s) {
     }
     GemmParams p = make_gemm_params(b, kchunk);
     p.tiles = tiles;
+    float* cs_rows = colsum_rows_begin(a);
+    if ((a.colsum_out || a.colsum_part) && epi_aux16(a.epi) && !cs_rows) return;
+    p.colsum_out = cs_rows;
     dim3 grid(tiles, split);
     if (a.a_kcontig && a.b_kcontig) launch_g4<true, true>(b, p, grid, s);
     else if (a.a_kcontig && !a.b_kcontig) launch_g4<true, false>(b, p, grid, s);
@@ -917,13 +1032,10 @@ static void gemm_bf16_g4(const GemmArgs& a, hipStream_t s) {
     else launch_g4<false, true>(b, p, grid, s);
     after_launch("gemm_bf16_256x128");
     count_hit(VIT_HIT_GEMM_256x128 + b.epi);
-    if (slab) {
-        slab_reduce_k<<<grid_blocks((long long)a.M * a.N / 4), 256, 0, s>>>(
-            (float*)a.C, a.ldc, slab, a.M, a.N, split);
-        after_launch("gemm_slab_reduce");
-        count_hit(VIT_HIT_SPLITK_REDUCE);
-    }
-    // bias gradient of a wgrad (M-contig A = dout^T): column sums of dout over the K rows
+    if (slab) slab_reduce(a, slab, split, s);
+    colsum_rows_end(a, cs_rows, s);
+    // bias gradient of a wgrad (M-contig A = dout^T): column sums of dout over the K rows (the
+    // thread workspace may be the slab just reduced: stream-ordered after the reduce)
     if (a.dbias && !a.a_kcontig) colsum_bf16(a.dbias, (const bf16_t*)a.A, a.K, a.M, a.lda, s);
 }
 
@@ -963,18 +1075,24 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s) {
         split = cdiv(a.K, kchunk);
         GemmArgs b = a;
         float* slab = nullptr;
-        if (a.epi == EPI_F32_ATOMIC && split > 1 && a.N % 4 == 0) {
-            // split-K partials to fp32 slabs + one reduce (no float atomics in the GEMM)
-            const size_t need = (size_t)split * a.M * a.N * sizeof(float);
-            slab = a.ws ? (a.ws_bytes >= need ? a.ws : nullptr) : (float*)workspace(need);
-            if (slab) {
+        if (a.epi == EPI_F32_ATOMIC) {  // split-K partials to fp32 slabs + one reduce (no atomics)
+            if (split > 1) {
+                if (!(slab = slab_buffer(a, split))) return;
                 b.epi = EPI_F32_SLAB;
                 b.C = slab;
                 b.ldc = a.N;
+            } else {
+                b.epi = EPI_F32_ACC;
             }
         }
         GemmParams p = make_gemm_params(b, kchunk);
         p.tiles = tiles;
+        float* cs_rows = colsum_rows_begin(a);
+        if ((a.colsum_out || a.colsum_part) && epi_aux16(a.epi) && !cs_rows) return;
+        p.colsum_out = cs_rows;
+        // fused bias gradient: one add per (column block, K-split), deterministic with one split
+        const bool late_db = a.dbias && !a.a_kcontig && split > 1;
+        if (late_db) p.dbias = nullptr;
         dim3 grid(tiles, split);
         if (a.a_kcontig && a.b_kcontig) launch_g2<true, true>(b, p, grid, s);
         else if (a.a_kcontig && !a.b_kcontig) launch_g2<true, false>(b, p, grid, s);
@@ -982,12 +1100,9 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s) {
         else launch_g2<false, true>(b, p, grid, s);
         after_launch("gemm_bf16_256");
         count_hit(VIT_HIT_GEMM_256x256 + b.epi);
-        if (slab) {
-            slab_reduce_k<<<grid_blocks((long long)a.M * a.N / 4), 256, 0, s>>>(
-                (float*)a.C, a.ldc, slab, a.M, a.N, split);
-            after_launch("gemm_slab_reduce");
-        count_hit(VIT_HIT_SPLITK_REDUCE);
-        }
+        if (slab) slab_reduce(a, slab, split, s);
+        colsum_rows_end(a, cs_rows, s);
+        if (late_db) colsum_bf16(a.dbias, (const bf16_t*)a.A, a.K, a.M, a.lda, s);
         return;
     }
     const int tiles = cdiv(a.M, bf::BM) * cdiv(a.N, bf::BN);
@@ -996,31 +1111,47 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s) {
     int kchunk = cdiv(cdiv(a.K, split), bf::BK) * bf::BK;
     if (kchunk <= 0) kchunk = bf::BK;
     split = cdiv(a.K > 0 ? a.K : 1, kchunk);
-    GemmParams p = make_gemm_params(a, kchunk);
+    GemmArgs b = a;
+    float* slab = nullptr;
+    if (a.epi == EPI_F32_ATOMIC) {  // split-K partials to fp32 slabs + one reduce (no atomics)
+        if (split > 1) {
+            if (!(slab = slab_buffer(a, split))) return;
+            b.epi = EPI_F32_SLAB; b.C = slab; b.ldc = a.N;
+        } else {
+            b.epi = EPI_F32_ACC;
+        }
+    }
+    GemmParams p = make_gemm_params(b, kchunk);
+    // the kernel's fused bias gradient adds once per (column block, K-split): deterministic with
+    // one split only; otherwise the column sums run after the GEMM
+    const bool late_db = a.dbias && !a.a_kcontig && split > 1;
+    if (late_db) p.dbias = nullptr;
     dim3 grid(tiles, split);
-    if (a.a_kcontig && a.b_kcontig) launch_bf16<true, true>(a, p, grid, s);
-    else if (a.a_kcontig && !a.b_kcontig) launch_bf16<true, false>(a, p, grid, s);
-    else if (!a.a_kcontig && !a.b_kcontig) launch_bf16<false, false>(a, p, grid, s);
-    else launch_bf16<false, true>(a, p, grid, s);
+    if (a.a_kcontig && a.b_kcontig) launch_bf16<true, true>(b, p, grid, s);
+    else if (a.a_kcontig && !a.b_kcontig) launch_bf16<true, false>(b, p, grid, s);
+    else if (!a.a_kcontig && !a.b_kcontig) launch_bf16<false, false>(b, p, grid, s);
+    else launch_bf16<false, true>(b, p, grid, s);
     after_launch("gemm_bf16");
-    count_hit(VIT_HIT_GEMM_128 + a.epi);
-    if (a.colsum_out && epi_aux16(a.epi))  // the 128x128 kernel has no fused column sums
-        colsum_bf16(a.colsum_out, (const bf16_t*)a.C, a.M, a.N, a.ldc, s);
+    count_hit(VIT_HIT_GEMM_128 + b.epi);
+    if (slab) slab_reduce(a, slab, split, s);
+    if (late_db) colsum_bf16(a.dbias, (const bf16_t*)a.A, a.K, a.M, a.lda, s);
+    // the 128x128 kernel has no fused column sums: partial rows of its output, then the same
+    // fixed-order reduce as the fused epilogues
+    if ((a.colsum_out || a.colsum_part) && epi_aux16(a.epi)) {
+        float* rows = colsum_rows_begin(a);
+        if (!rows) return;
+        colsum_part_k<bf16_t><<<dim3(cdiv(a.N, 256), cdiv(a.M, 128)), 256, 0, s>>>(
+            rows, (const bf16_t*)a.C, a.M, a.N, a.ldc, 128, 0);
+        after_launch("colsum_rows");
+        colsum_rows_end(a, rows, s);
+    }
 }
 
-void colsum_f32(float* dbias, const float* X, int M, int N, long long ld, hipStream_t s) {
-    if (M <= 0 || N <= 0) return;
-    const int rpb = 256;
-    dim3 grid(cdiv(N, 256), cdiv(M, rpb));
-    colsum_kernel<float><<<grid, 256, 0, s>>>(dbias, X, M, N, ld, rpb);
-    after_launch("colsum_f32");
+void colsum_f32(float* dbias, const float* X, int M, int N, long long ld, hipStream_t s, float* ws) {
+    colsum_any(dbias, X, M, N, ld, s, ws);
 }
-void colsum_bf16(float* dbias, const bf16_t* X, int M, int N, long long ld, hipStream_t s) {
-    if (M <= 0 || N <= 0) return;
-    const int rpb = 256;
-    dim3 grid(cdiv(N, 256), cdiv(M, rpb));
-    colsum_kernel<bf16_t><<<grid, 256, 0, s>>>(dbias, X, M, N, ld, rpb);
-    after_launch("colsum_bf16");
+void colsum_bf16(float* dbias, const bf16_t* X, int M, int N, long long ld, hipStream_t s, float* ws) {
+    colsum_any(dbias, X, M, N, ld, s, ws);
 }
 
 }  // namespace vit

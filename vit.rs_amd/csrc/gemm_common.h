@@ -13,7 +13,7 @@ struct GemmParams {
     const void* aux;
     const float* bias;
     float* dbias;
-    float* colsum_out;
+    float* colsum_out;  // partial rows [cdiv(M,128)][N] of the aux epilogues' column sums (stored)
     long long lda, ldb, ldc, ldaux;
     int M, N, K;
     int kchunk;  // K range per split (multiple of the K tile)
@@ -62,6 +62,11 @@ __device__ __forceinline__ void mx_out8(const GemmParams& p, int m, int n, uint3
     *reinterpret_cast<uint2*>(p.mx_q + (long long)m * p.N + n) = make_uint2((uint32_t)t0, (uint32_t)t1);
 }
 
+// host: the partial-row buffer of an aux epilogue's column sums (colsum_part or the thread
+// workspace; nullptr when the GEMM sums no columns) and the fixed-order add into colsum_out
+float* colsum_rows_begin(const GemmArgs& a);
+void colsum_rows_end(const GemmArgs& a, float* rows, hipStream_t s);
+
 // (tile, K-split) of this workgroup.  Workgroups are dealt round-robin over the 8 XCDs in
 // linear-id order (x fastest), so the XCD-aware remap runs over the whole (split, tile) grid: the
 // ~1/8 of the grid on one XCD is a contiguous range of the same K-split's tiles, which share
@@ -98,9 +103,11 @@ __device__ __forceinline__ bool skip_epilogue(const GemmParams& p, f32x4_t (&acc
     return true;
 }
 
-// epilogue for one lane's C[m][n..n+3] (n % 4 == 0, m < M, n < N)
+// epilogue for one lane's C[m][n..n+3] (n % 4 == 0, m < M, n < N).  EPI_F32_ATOMIC never reaches
+// a kernel: the launchers turn it into K-split slabs + a fixed-order reduce (or EPI_F32_ACC)
 template <int EPI>
 __device__ __forceinline__ void epilogue(const GemmParams& p, int m, int n, f32x4_t& v) {
+    static_assert(EPI != EPI_F32_ATOMIC, "split-K partials go through slabs");
     if constexpr (epi_bias(EPI)) {
         if (p.bias) {
             const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
@@ -115,12 +122,6 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, int m, int n, f32x
         float4 o = *q;
         o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
         *q = o;
-    } else if constexpr (EPI == EPI_F32_ATOMIC) {
-        float* q = (float*)p.C + off;
-        atomicAdd(q + 0, v[0]);
-        atomicAdd(q + 1, v[1]);
-        atomicAdd(q + 2, v[2]);
-        atomicAdd(q + 3, v[3]);
     } else if constexpr (EPI == EPI_BF16_STORE) {
         *reinterpret_cast<uint2*>((bf16_t*)p.C + off) =
             make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
@@ -193,10 +194,6 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, flo
         v[0] += o0.x; v[1] += o0.y; v[2] += o0.z; v[3] += o0.w;
         v[4] += o1.x; v[5] += o1.y; v[6] += o1.z; v[7] += o1.w;
         st_f32(q);
-    } else if constexpr (EPI == EPI_F32_ATOMIC) {
-        float* q = (float*)p.C + off;
-#pragma unroll
-        for (int j = 0; j < 8; j++) atomicAdd(q + j, v[j]);
     } else if constexpr (EPI == EPI_F32_SLAB) {
         st_f32((float*)p.C + (long long)split_index(p.tiles) * p.M * p.ldc + off);
     } else if constexpr (EPI == EPI_BF16_STORE) {
@@ -399,9 +396,11 @@ template <int EPI>
 __device__ __forceinline__ bool staged_interior(const GemmParams& p, int m0, int n0) {
     return EPI != EPI_F32_ATOMIC && m0 + 128 <= p.M && n0 + 64 <= p.N;
 }
-// fused bias gradient of the next GEMM: column sums of the DGELU output
+// fused bias gradient of the next GEMM: column sums of the DGELU / MUL output.  The wave's 128 x 64
+// tile reduces its 8 row groups by shuffles and stores its 64 column sums as partial row m0/128
+// (each (row, column) of the partial matrix has exactly one writer: no atomics, fixed order)
 template <int EPI>
-__device__ __forceinline__ void staged_colsum(const GemmParams& p, int lane, int n0, float (&cs)[8]) {
+__device__ __forceinline__ void staged_colsum(const GemmParams& p, int lane, int m0, int n0, float (&cs)[8]) {
     if constexpr (epi_aux16(EPI)) {
         if (p.colsum_out) {
             const int rr = lane >> 3, cc = (lane & 7) * 8;
@@ -416,7 +415,7 @@ __device__ __forceinline__ void staged_colsum(const GemmParams& p, int lane, int
             if (rr == 0) {
 #pragma unroll
                 for (int j = 0; j < 8; j++)
-                    if (n0 + cc + j < p.N) atomicAdd(p.colsum_out + n0 + cc + j, cs[j]);
+                    if (n0 + cc + j < p.N) p.colsum_out[(long long)(m0 >> 7) * p.N + n0 + cc + j] = cs[j];
             }
         }
     }
@@ -438,7 +437,7 @@ __device__ __forceinline__ void staged_epilogue(const GemmParams& p, f32x4_t (&a
                 *reinterpret_cast<f32x4_t*>(st + (a * 16 + i) * STG_LD + b * 16 + 4 * g) = acc[pass * 4 + a][b];
         staged_pass<EPI>(p, st, lane, m0, n0, pass, interior, cs);
     }
-    staged_colsum<EPI>(p, lane, n0, cs);
+    staged_colsum<EPI>(p, lane, m0, n0, cs);
 }
 
 }  // namespace vit

@@ -233,7 +233,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(F8Params fp) {
                 }
         staged_pass<EPI>(p, st, lane, m0, n0, pass, interior, cs);
     }
-    staged_colsum<EPI>(p, lane, n0, cs);
+    staged_colsum<EPI>(p, lane, m0, n0, cs);
 }
 
 // ------------------------------------------------------------------------------- quantizer
@@ -319,6 +319,9 @@ void gemm_fp8(const GemmArgs& a, hipStream_t s) {
     }
     f8::F8Params fp;
     fp.p = make_gemm_params(a, a.K);
+    float* cs_rows = colsum_rows_begin(a);
+    if ((a.colsum_out || a.colsum_part) && !cs_rows) return;
+    fp.p.colsum_out = cs_rows;
     const int tiles = cdiv(a.M, f8::BM) * cdiv(a.N, f8::BN);
     fp.p.tiles = tiles;
     fp.sa = (const uint8_t*)a.a_scale;
@@ -341,6 +344,7 @@ void gemm_fp8(const GemmArgs& a, hipStream_t s) {
     }
     after_launch("gemm_fp8");
     count_hit(VIT_HIT_GEMM_FP8 + a.epi);
+    colsum_rows_end(a, cs_rows, s);
 }
 
 template <typename TX>

@@ -103,35 +103,54 @@ __global__ __launch_bounds__(256) void ln_fwd_k(TO* __restrict__ out, float* __r
     }
 }
 
-// train_vit.rs:603-637 (D5).  dinp += ...; dweight/dbias accumulate through per-block LDS
-// partials and one global atomic per column per block.  TD: dout type (fp32 or bf16).
-// If dres_in != nullptr:  dinp = dres_in + ln_dinp   (fused residual_backward, bf16 path),
-// and a bf16 copy of dinp is written to dinp_bf (if non-null).
-template <typename TD>
-__global__ __launch_bounds__(256) void ln_bwd_k(float* __restrict__ dinp, bf16_t* __restrict__ dinp_bf,
-                                                const float* __restrict__ dres_in,
-                                                float* __restrict__ dweight, float* __restrict__ dbias,
-                                                const TD* __restrict__ dout,
+// train_vit.rs:603-637 (D5).  Two modes (compile time, so every load is unconditional):
+//   ST = false: dinp (fp32) += LN_dinp(dout)                       (layernorm_backward, fp32 trainer)
+//   ST = true : the trainer's residual-gradient stream in "bf16 + lo8" form (common.h lo8_*):
+//               out = in + LN_dinp(dout), in/out as (bf16 plane, byte plane); dsum (nullable) gets the
+//               column sums of out taken in fp32 (the next bias gradient)
+// dweight / dbias (/ dsum) accumulate in per-wave LDS rows (each lane owns its columns: no atomics),
+// are summed across the 4 waves in a fixed order and leave the block as its partial row
+// part[blockIdx.x][2C or 3C] (dw | db | dsum), summed in a fixed order by rows_reduce_add — by the
+// launcher, or by the trainer across micro-batches: deterministic.  TD: dout type (fp32 or bf16).
+struct LnbIo {
+    float* dinp;            // ST = false: accumulated in place
+    bf16_t* hi_out;         // ST = true
+    uint8_t* lo_out;
+    const bf16_t* hi_in;
+    const uint8_t* lo_in;
+    float *dweight, *dbias, *dsum, *part;
+};
+__device__ __forceinline__ float to_f32(float v) { return v; }
+__device__ __forceinline__ float to_f32(bf16_t v) { return bf2f(v); }
+__device__ __forceinline__ void lnb_flush(const LnbIo& io, const float* sm, int C) {
+    __syncthreads();
+    const int nsum = io.dsum ? 3 * C : 2 * C;
+    for (int i = threadIdx.x; i < nsum; i += 256) {
+        const float t = sm[i] + sm[3 * C + i] + sm[6 * C + i] + sm[9 * C + i];
+        io.part[(long long)blockIdx.x * nsum + i] = t;
+    }
+}
+// any C (the vectorised kernel below needs C % 256 == 0)
+template <typename TD, bool ST>
+__global__ __launch_bounds__(256) void ln_bwd_k(LnbIo io, const TD* __restrict__ dout,
                                                 const float* __restrict__ inp,
                                                 const float* __restrict__ weight,
                                                 const float* __restrict__ mean,
-                                                const float* __restrict__ rstd, long long rows,
-                                                int C) {
-    extern __shared__ float sm[];  // [2][C]
-    float* sdw = sm;
-    float* sdb = sm + C;
-    for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) sm[i] = 0.f;
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
+                                                const float* __restrict__ rstd, long long rows, int C) {
+    extern __shared__ float sm[];  // [4 waves][3][C]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float* pw = sm + wave * 3 * C;
+    float* pb = pw + C;
+    float* ps = pw + 2 * C;
+    for (int i = lane; i < C; i += 64) pw[i] = pb[i] = ps[i] = 0.f;
     const long long nwaves = (long long)gridDim.x * 4;
-    for (long long row = blockIdx.x * 4LL + (threadIdx.x >> 6); row < rows; row += nwaves) {
+    for (long long row = blockIdx.x * 4LL + wave; row < rows; row += nwaves) {
         const TD* dy = dout + row * C;
         const float* x = inp + row * C;
         const float mu = mean[row], rs = rstd[row];
         float a = 0.f, bsum = 0.f;
         for (int i = lane; i < C; i += 64) {
-            float d;
-            if constexpr (sizeof(TD) == 2) d = bf2f(dy[i]); else d = dy[i];
+            const float d = to_f32(dy[i]);
             const float nrm = (x[i] - mu) * rs;
             const float dn = weight[i] * d;
             a += dn;
@@ -140,31 +159,28 @@ __global__ __launch_bounds__(256) void ln_bwd_k(float* __restrict__ dinp, bf16_t
         const float dnorm_mean = warp_sum(a) / (float)C;
         const float dnorm_norm_mean = warp_sum(bsum) / (float)C;
         for (int i = lane; i < C; i += 64) {
-            float d;
-            if constexpr (sizeof(TD) == 2) d = bf2f(dy[i]); else d = dy[i];
+            const float d = to_f32(dy[i]);
             const float nrm = (x[i] - mu) * rs;
             const float dn = weight[i] * d;
-            atomicAdd(&sdb[i], d);
-            atomicAdd(&sdw[i], nrm * d);
+            pb[i] += d;
+            pw[i] += nrm * d;
             float dval = dn;
             dval -= dnorm_mean;
             dval -= nrm * dnorm_norm_mean;
             dval *= rs;
             const long long o = row * C + i;
-            if (dres_in) {
-                const float t = dres_in[o] + dval;
-                dinp[o] = t;
-                if (dinp_bf) dinp_bf[o] = f2bf(t);
+            if constexpr (ST) {
+                const float t = lo8_decode(bf2f(io.hi_in[o]), io.lo_in[o]) + dval;
+                const bf16_t h = f2bf(t);
+                io.hi_out[o] = h;
+                io.lo_out[o] = (uint8_t)lo8_encode(t, bf2f(h));
+                ps[i] += t;
             } else {
-                dinp[o] += dval;
+                io.dinp[o] += dval;
             }
         }
     }
-    __syncthreads();
-    for (int i = threadIdx.x; i < C; i += blockDim.x) {
-        atomicAdd(dweight + i, sdw[i]);
-        atomicAdd(dbias + i, sdb[i]);
-    }
+    lnb_flush(io, sm, C);
 }
 
 // Vectorised LayerNorm for C % 256 == 0: one wave per row, NV float4 per lane held in registers
@@ -221,14 +237,12 @@ __device__ __forceinline__ float4 ld4(const bf16_t* p, int k) {
                        __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
 }
 
-template <int NV, typename TD>
-__global__ __launch_bounds__(256) void ln_bwd_vec_k(float* __restrict__ dinp, bf16_t* __restrict__ dinp_bf,
-                                                    const float* __restrict__ dres_in,
-                                                    float* __restrict__ dweight,
-                                                    float* __restrict__ dbias,
-                                                    float* __restrict__ dsum,
-                                                    const TD* __restrict__ dout,
-                                                    const float* __restrict__ inp,
+// C % 256 == 0: one wave per row, NV float4 per lane in registers, the next row's loads in flight
+// while this row reduces and stores (every load unconditional — the last row re-fetches itself — so
+// the compiler never drains the prefetch with a vmcnt(0))
+template <int NV, typename TD, bool ST>
+__global__ __launch_bounds__(256) void ln_bwd_vec_k(LnbIo io, const TD* __restrict__ dout,
+                                                    const float* inp,  // not restrict: keeps its prefetch above the row's stores
                                                     const float* __restrict__ weight,
                                                     const float* __restrict__ mean,
                                                     const float* __restrict__ rstd, long long rows,
@@ -236,7 +250,7 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_k(float* __restrict__ dinp, bf
     extern __shared__ float sm[];  // [4 waves][3][C]: this wave's dweight / dbias / dsum partials
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     // the column partials live in the wave's LDS rows (each lane owns its 4*NV columns, so the
-    // read-modify-writes need no synchronisation): 36 VGPRs freed for the row prefetch below
+    // read-modify-writes need no synchronisation)
     float4* pw = reinterpret_cast<float4*>(sm + wave * 3 * C);
     float4* pb = reinterpret_cast<float4*>(sm + wave * 3 * C + C);
     float4* ps = reinterpret_cast<float4*>(sm + wave * 3 * C + 2 * C);
@@ -247,10 +261,8 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_k(float* __restrict__ dinp, bf
         pw[lane + 64 * j] = pb[lane + 64 * j] = ps[lane + 64 * j] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     const long long nwaves = (long long)gridDim.x * 4;
-    // software pipeline over the wave's rows: the next row's dout / inp / dres_in / mean / rstd
-    // loads are in flight while this row reduces and stores (one HBM round trip per row
-    // otherwise: the row loop was latency-bound at ~85 % of the achievable bandwidth)
     float4 pdy[NV], px[NV], pri[NV];
+    uint32_t plo[NV];
     float pmu = 0.f, prs = 0.f;
     auto fetch = [&](long long r) {
         const TD* dyr = dout + r * C;
@@ -259,8 +271,12 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_k(float* __restrict__ dinp, bf
         for (int j = 0; j < NV; j++) {
             pdy[j] = ld4(dyr, lane + 64 * j);
             px[j] = x4[lane + 64 * j];
-            pri[j] = dres_in ? reinterpret_cast<const float4*>(dres_in + r * C)[lane + 64 * j]
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
+            if constexpr (ST) {
+                pri[j] = ld4(io.hi_in + r * C, lane + 64 * j);
+                plo[j] = reinterpret_cast<const uint32_t*>(io.lo_in + r * C)[lane + 64 * j];
+            } else {
+                pri[j] = reinterpret_cast<const float4*>(io.dinp + r * C)[lane + 64 * j];
+            }
         }
         pmu = mean[r];
         prs = rstd[r];
@@ -274,9 +290,17 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_k(float* __restrict__ dinp, bf
             dy[j] = pdy[j];
             xr[j] = px[j];
             ri[j] = pri[j];
+            if constexpr (ST) {
+                const uint32_t q = plo[j];
+                ri[j] = make_float4(lo8_decode(ri[j].x, q), lo8_decode(ri[j].y, q >> 8), lo8_decode(ri[j].z, q >> 16),
+                                    lo8_decode(ri[j].w, q >> 24));
+            }
         }
         const float mu = pmu, rs = prs;
-        if (row + nwaves < rows) fetch(row + nwaves);
+        fetch(row + nwaves < rows ? row + nwaves : row);
+        // keep the prefetch at the top: the scheduler otherwise sinks it to the end of the row to
+        // reuse this row's registers, and the next iteration waits a full HBM round trip
+        __builtin_amdgcn_sched_barrier(0);
         float a = 0.f, bs = 0.f;
 #pragma unroll
         for (int j = 0; j < NV; j++) {
@@ -303,29 +327,24 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_k(float* __restrict__ dinp, bf
             dv.y = ((w4[j].y * dy[j].y - dm) - nr[j].y * dnm) * rs;
             dv.z = ((w4[j].z * dy[j].z - dm) - nr[j].z * dnm) * rs;
             dv.w = ((w4[j].w * dy[j].w - dm) - nr[j].w * dnm) * rs;
-            float4* o = reinterpret_cast<float4*>(dinp + row * C) + k;
-            if (dres_in) {
-                const float4 t = make_float4(ri[j].x + dv.x, ri[j].y + dv.y, ri[j].z + dv.z, ri[j].w + dv.w);
-                *o = t;
+            const float4 t = make_float4(ri[j].x + dv.x, ri[j].y + dv.y, ri[j].z + dv.z, ri[j].w + dv.w);
+            if constexpr (ST) {
                 float4 u = ps[k];
                 u.x += t.x; u.y += t.y; u.z += t.z; u.w += t.w;
                 ps[k] = u;
-                if (dinp_bf)
-                    reinterpret_cast<uint2*>(dinp_bf + row * C)[k] =
-                        make_uint2(pack_bf16x2(t.x, t.y), pack_bf16x2(t.z, t.w));
+                const uint2 h = make_uint2(pack_bf16x2(t.x, t.y), pack_bf16x2(t.z, t.w));
+                reinterpret_cast<uint2*>(io.hi_out + row * C)[k] = h;
+                reinterpret_cast<uint32_t*>(io.lo_out + row * C)[k] =
+                    lo8_encode(t.x, __uint_as_float(h.x << 16)) |
+                    (lo8_encode(t.y, __uint_as_float(h.x & 0xffff0000u)) << 8) |
+                    (lo8_encode(t.z, __uint_as_float(h.y << 16)) << 16) |
+                    (lo8_encode(t.w, __uint_as_float(h.y & 0xffff0000u)) << 24);
             } else {
-                float4 t = *o;
-                t.x += dv.x; t.y += dv.y; t.z += dv.z; t.w += dv.w;
-                *o = t;
+                reinterpret_cast<float4*>(io.dinp + row * C)[k] = t;
             }
         }
     }
-    __syncthreads();
-    const int nsum = dsum ? 3 * C : 2 * C;
-    for (int i = threadIdx.x; i < nsum; i += 256) {
-        const float t = sm[i] + sm[3 * C + i] + sm[6 * C + i] + sm[9 * C + i];
-        atomicAdd(i < C ? dweight + i : (i < 2 * C ? dbias + (i - C) : dsum + (i - 2 * C)), t);
-    }
+    lnb_flush(io, sm, C);
 }
 
 // ------------------------------------------------------------------ softmax / cross-entropy
@@ -409,10 +428,10 @@ __global__ void patch_assemble_k(float* __restrict__ enc, const float* __restric
         enc[idx] = base + wpe[(long long)t * C + c];
     }
 }
-// gather the patch rows of dencoded into [B*NP, C] (TO = float or bf16)
-template <typename TO>
-__global__ void patch_gather_k(TO* __restrict__ out, const float* __restrict__ denc, int B, int NP,
-                               int C) {
+// gather the patch rows of dencoded into [B*NP, C] (TO = float or bf16; TI likewise)
+template <typename TO, typename TI>
+__global__ void patch_gather_k(TO* __restrict__ out, const TI* __restrict__ denc, const uint8_t* __restrict__ lo,
+                               int B, int NP, int C) {
     const int T = NP + 1;
     const long long n = (long long)B * NP * C;
     for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < n;
@@ -420,24 +439,40 @@ __global__ void patch_gather_k(TO* __restrict__ out, const float* __restrict__ d
         const long long r = idx / C;
         const int c = (int)(idx - r * C);
         const int b = (int)(r / NP), p = (int)(r - (long long)b * NP);
-        const float v = denc[((long long)b * T + 1 + p) * C + c];
-        if constexpr (sizeof(TO) == 2) out[idx] = f2bf(v); else out[idx] = v;
+        const long long src = ((long long)b * T + 1 + p) * C + c;
+        const TI v = denc[src];
+        if constexpr (sizeof(TO) == sizeof(TI)) out[idx] = v;
+        else if constexpr (sizeof(TO) == 2) out[idx] = f2bf(v);
+        else out[idx] = lo ? lo8_decode(bf2f(v), lo[src]) : bf2f(v);
     }
 }
-// dcls[c] += sum_b denc[b,0,c];  dwpe[t,c] += sum_b denc[b,t,c];  dpatch_b[c] += sum_{b,t>0} denc
-__global__ void patch_small_grads_k(float* __restrict__ dcls, float* __restrict__ dwpe,
-                                    float* __restrict__ dpb, const float* __restrict__ denc, int B,
-                                    int T, int C) {
+// dwpe[t,c] += colsum_t[c] = sum_b denc[b,t,c] (b ascending); colsum_t -> tsum[t][c]
+template <typename TI>
+__global__ void patch_small_grads_k(float* __restrict__ dwpe, float* __restrict__ tsum,
+                                    const TI* __restrict__ denc, const uint8_t* __restrict__ lo, int B, int T,
+                                    int C) {
     const long long n = (long long)T * C;
     for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < n;
          idx += (long long)gridDim.x * blockDim.x) {
         const int t = (int)(idx / C), c = (int)(idx - (long long)t * C);
         float s = 0.f;
-        for (int b = 0; b < B; b++) s += denc[((long long)b * T + t) * C + c];
+        for (int b = 0; b < B; b++) {
+            const long long e = ((long long)b * T + t) * C + c;
+            s += lo ? lo8_decode(to_f32(denc[e]), lo[e]) : to_f32(denc[e]);
+        }
         dwpe[idx] += s;
-        if (t == 0) dcls[c] += s;
-        else atomicAdd(dpb + c, s);
+        tsum[idx] = s;
     }
+}
+// dcls[c] += tsum[0][c];  dpatch_b[c] += sum_{t>0} tsum[t][c] (t ascending: no atomics)
+__global__ void patch_small_grads_fin_k(float* __restrict__ dcls, float* __restrict__ dpb,
+                                        const float* __restrict__ tsum, int T, int C) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    float s = 0.f;
+    for (int t = 1; t < T; t++) s += tsum[(long long)t * C + c];
+    dcls[c] += tsum[c];
+    dpb[c] += s;
 }
 
 // ------------------------------------------------------------------ launch helpers (internal)
@@ -467,63 +502,76 @@ void ln_forward_bf16(bf16_t* out, float* mean, float* rstd, const float* inp, co
                      const float* b, long long rows, int C, hipStream_t s) {
     ln_forward_any<bf16_t>(out, mean, rstd, inp, w, b, rows, C, s);
 }
-static int ln_bwd_grid(long long rows) {
-    long long g = (rows + 31) / 32;  // ~8 rows per wave
-    return (int)(g < 1 ? 1 : (g > 2048 ? 2048 : g));
-}
-template <typename TD>
-static void ln_backward_any(float* dinp, bf16_t* dinp_bf, const float* dres_in, float* dw,
-                            float* db, float* dsum, const TD* dout, const float* inp,
-                            const float* w, const float* mean, const float* rstd, long long rows,
-                            int C, hipStream_t s) {
+int ln_bwd_blocks(long long rows);
+template <typename TD, bool ST>
+static void ln_backward_any(LnbIo io, const TD* dout, const float* inp, const float* w,
+                            const float* mean, const float* rstd, long long rows, int C, hipStream_t s,
+                            float* ws = nullptr) {
     if (rows <= 0) return;
+    // io.part set: the caller reduces the partial rows; else they go to ws (nullptr = thread
+    // workspace) and are added into dweight / dbias / dsum here
+    const bool reduce = io.part == nullptr;
+    const int nsum = io.dsum ? 3 * C : 2 * C;
+    if (reduce) {
+        io.part = ws ? ws : (float*)workspace((size_t)ln_bwd_blocks(rows) * nsum * sizeof(float));
+        if (!io.part) return;
+    }
     const bool vec = C % 256 == 0 && C <= 2048 &&
-                     (((uintptr_t)dinp | (uintptr_t)dout | (uintptr_t)inp | (uintptr_t)w |
-                       (uintptr_t)dres_in | (uintptr_t)dinp_bf) & 15) == 0;
-    if (!vec) {
-        ln_bwd_k<TD><<<ln_bwd_grid(rows), 256, 2 * C * sizeof(float), s>>>(
-            dinp, dinp_bf, dres_in, dw, db, dout, inp, w, mean, rstd, rows, C);
-        after_launch("layernorm_backward");
-        if (dsum) colsum_f32(dsum, dinp, (int)rows, C, C, s);
-        return;
-    }
-    long long g = (rows + 15) / 16;  // ~4 rows per wave
-    // at most one round of resident blocks (3 per CU at 142-144 VGPRs; 256 CUs)
-    const int grid = (int)(g < 1 ? 1 : (g > 768 ? 768 : g));
+                     (((uintptr_t)io.dinp | (uintptr_t)dout | (uintptr_t)inp | (uintptr_t)w |
+                       (uintptr_t)io.hi_in | (uintptr_t)io.hi_out | (uintptr_t)io.lo_in | (uintptr_t)io.lo_out) & 15) == 0;
+    const int grid = ln_bwd_blocks(rows);
     const size_t lds = 12 * (size_t)C * sizeof(float);
-    if (dsum && !dres_in) { set_error("layernorm_backward: output column sum needs dres_in"); return; }
-#define VIT_LNB(NV) ln_bwd_vec_k<NV, TD><<<grid, 256, lds, s>>>(dinp, dinp_bf, dres_in, dw, db, dsum, dout, inp, w, mean, rstd, rows, C)
-    switch (C / 256) {
-        case 1: VIT_LNB(1); break;
-        case 2: VIT_LNB(2); break;
-        case 3: VIT_LNB(3); break;
-        case 4: VIT_LNB(4); break;
-        case 5: VIT_LNB(5); break;
-        case 6: VIT_LNB(6); break;
-        case 7: VIT_LNB(7); break;
-        default: VIT_LNB(8); break;
-    }
+    if (lds > 160 * 1024) { set_error("layernorm_backward: C=%d exceeds the LDS column partials", C); return; }
+    if (!vec) {
+        if (lds > 64 * 1024) VIT_HIP(hipFuncSetAttribute((const void*)ln_bwd_k<TD, ST>,
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        ln_bwd_k<TD, ST><<<grid, 256, lds, s>>>(io, dout, inp, w, mean, rstd, rows, C);
+    } else {
+#define VIT_LNB(NV)                                                                                        \
+    if (lds > 64 * 1024) VIT_HIP(hipFuncSetAttribute((const void*)ln_bwd_vec_k<NV, TD, ST>,                 \
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+    ln_bwd_vec_k<NV, TD, ST><<<grid, 256, lds, s>>>(io, dout, inp, w, mean, rstd, rows, C)
+        switch (C / 256) {
+            case 1: VIT_LNB(1); break;
+            case 2: VIT_LNB(2); break;
+            case 3: VIT_LNB(3); break;
+            case 4: VIT_LNB(4); break;
+            case 5: VIT_LNB(5); break;
+            case 6: VIT_LNB(6); break;
+            case 7: VIT_LNB(7); break;
+            default: VIT_LNB(8); break;
+        }
 #undef VIT_LNB
+    }
     after_launch("layernorm_backward");
+    if (reduce) {
+        const RowsJob jobs[3] = {{io.dweight, io.part, grid, nsum, C}, {io.dbias, io.part + C, grid, nsum, C},
+                                 {io.dsum, io.part + 2 * C, grid, nsum, C}};
+        rows_reduce_add(jobs, io.dsum ? 3 : 2, s);
+    }
+}
+int ln_bwd_blocks(long long rows) {
+    const long long g = (rows + 15) / 16;  // ~4 rows per wave
+    // at most one round of resident blocks (3 per CU at 142-144 VGPRs; 256 CUs)
+    return (int)(g < 1 ? 1 : (g > 768 ? 768 : g));
 }
 void ln_backward_f32(float* dinp, float* dw, float* db, const float* dout, const float* inp,
                      const float* w, const float* mean, const float* rstd, long long rows, int C,
-                     hipStream_t s) {
-    ln_backward_any(dinp, nullptr, nullptr, dw, db, nullptr, dout, inp, w, mean, rstd, rows, C, s);
+                     hipStream_t s, float* ws) {
+    LnbIo io{};
+    io.dinp = dinp; io.dweight = dw; io.dbias = db;
+    ln_backward_any<float, false>(io, dout, inp, w, mean, rstd, rows, C, s, ws);
 }
-void ln_backward_fused(float* dres_out, bf16_t* dres_out_bf, const float* dres_in, float* dw,
-                       float* db, float* dres_colsum, const float* dout, const float* inp,
-                       const float* w, const float* mean, const float* rstd, long long rows, int C,
-                       hipStream_t s) {
-    ln_backward_any(dres_out, dres_out_bf, dres_in, dw, db, dres_colsum, dout, inp, w, mean, rstd,
-                    rows, C, s);
-}
-void ln_backward_fused_bf16(float* dres_out, bf16_t* dres_out_bf, const float* dres_in, float* dw,
-                            float* db, float* dres_colsum, const bf16_t* dout, const float* inp,
-                            const float* w, const float* mean, const float* rstd, long long rows,
-                            int C, hipStream_t s) {
-    ln_backward_any(dres_out, dres_out_bf, dres_in, dw, db, dres_colsum, dout, inp, w, mean, rstd,
-                    rows, C, s);
+void ln_backward_bf16_stream(bf16_t* dres_out, uint8_t* lo_out, const bf16_t* dres_in, const uint8_t* lo_in,
+                             float* dw, float* db, float* dres_colsum, const bf16_t* dout, const float* inp,
+                             const float* w, const float* mean, const float* rstd, long long rows, int C,
+                             hipStream_t s, float* part) {
+    if (!dres_out || !lo_out || !dres_in || !lo_in) { set_error("layernorm_backward: the bf16 stream needs its 4 planes"); return; }
+    if (((uintptr_t)lo_in | (uintptr_t)lo_out) & 3) { set_error("layernorm_backward: lo8 planes need 4-B alignment"); return; }
+    LnbIo io{};
+    io.hi_out = dres_out; io.lo_out = lo_out; io.hi_in = dres_in; io.lo_in = lo_in;
+    io.dweight = dw; io.dbias = db; io.dsum = dres_colsum; io.part = part;
+    ln_backward_any<bf16_t, true>(io, dout, inp, w, mean, rstd, rows, C, s);
 }
 // out[c][r] = in[r][c] for `count` matrices of R x Cc bf16 spaced `stride` elements apart
 // (in and out use the same stride); 64 x 64 tiles through LDS, 16-B global accesses.
@@ -607,18 +655,41 @@ void patch_assemble(float* enc, const float* emb, const float* cls, const float*
 }
 void patch_gather_f32(float* out, const float* denc, int B, int NP, int C, hipStream_t s) {
     const long long n = (long long)B * NP * C;
-    patch_gather_k<float><<<grid_for(n, 256), 256, 0, s>>>(out, denc, B, NP, C);
+    patch_gather_k<float, float><<<grid_for(n, 256), 256, 0, s>>>(out, denc, nullptr, B, NP, C);
     after_launch("patch_gather");
 }
 void patch_gather_bf16(bf16_t* out, const float* denc, int B, int NP, int C, hipStream_t s) {
     const long long n = (long long)B * NP * C;
-    patch_gather_k<bf16_t><<<grid_for(n, 256), 256, 0, s>>>(out, denc, B, NP, C);
+    patch_gather_k<bf16_t, float><<<grid_for(n, 256), 256, 0, s>>>(out, denc, nullptr, B, NP, C);
     after_launch("patch_gather_bf16");
 }
-void patch_small_grads(float* dcls, float* dwpe, float* dpb, const float* denc, int B, int T,
-                       int C, hipStream_t s) {
+void patch_gather_f32(float* out, const bf16_t* denc, const uint8_t* lo, int B, int NP, int C, hipStream_t s) {
+    const long long n = (long long)B * NP * C;
+    patch_gather_k<float, bf16_t><<<grid_for(n, 256), 256, 0, s>>>(out, denc, lo, B, NP, C);
+    after_launch("patch_gather");
+}
+void patch_gather_bf16(bf16_t* out, const bf16_t* denc, int B, int NP, int C, hipStream_t s) {
+    const long long n = (long long)B * NP * C;
+    patch_gather_k<bf16_t, bf16_t><<<grid_for(n, 256), 256, 0, s>>>(out, denc, nullptr, B, NP, C);
+    after_launch("patch_gather_bf16");
+}
+template <typename TI>
+static void patch_small_grads_any(float* dcls, float* dwpe, float* dpb, const TI* denc, const uint8_t* lo, int B,
+                                  int T, int C, hipStream_t s, float* ws) {
     const long long n = (long long)T * C;
-    patch_small_grads_k<<<grid_for(n, 256), 256, 0, s>>>(dcls, dwpe, dpb, denc, B, T, C);
+    if (!ws) ws = (float*)workspace(n * sizeof(float));
+    if (!ws) return;
+    patch_small_grads_k<TI><<<grid_for(n, 256), 256, 0, s>>>(dwpe, ws, denc, lo, B, T, C);
+    patch_small_grads_fin_k<<<cdiv(C, 256), 256, 0, s>>>(dcls, dpb, ws, T, C);
+}
+void patch_small_grads(float* dcls, float* dwpe, float* dpb, const float* denc, int B, int T,
+                       int C, hipStream_t s, float* ws) {
+    patch_small_grads_any(dcls, dwpe, dpb, denc, nullptr, B, T, C, s, ws);
+    after_launch("patch_small_grads");
+}
+void patch_small_grads(float* dcls, float* dwpe, float* dpb, const bf16_t* denc, const uint8_t* lo, int B, int T,
+                       int C, hipStream_t s, float* ws) {
+    patch_small_grads_any(dcls, dwpe, dpb, denc, lo, B, T, C, s, ws);
     after_launch("patch_small_grads");
 }
 
@@ -723,10 +794,11 @@ void patch_embed_backward(float* dpatch_w, float* dpatch_b, float* dcls, float* 
                           const float* dencoded, const float* pixels, int B, int IMG, int P, int C) {
     const int NP = (IMG / P) * (IMG / P), K = 3 * P * P, T = NP + 1;
     const size_t n_patch = (size_t)B * NP * K, n_g = (size_t)B * NP * C;
-    float* ws = (float*)workspace((n_patch + n_g) * sizeof(float) + 256);
+    const size_t o_g = (n_patch + 63) & ~(size_t)63, o_t = (o_g + n_g + 63) & ~(size_t)63;
+    float* ws = (float*)workspace((o_t + (size_t)T * C) * sizeof(float));
     if (!ws) return;
     float* patches = ws;
-    float* g = ws + ((n_patch + 63) & ~(size_t)63);
+    float* g = ws + o_g;
     hipStream_t s = stream();
     im2col_f32(patches, pixels, B, IMG, P, s);
     patch_gather_f32(g, dencoded, B, NP, C, s);
@@ -737,7 +809,7 @@ void patch_embed_backward(float* dpatch_w, float* dpatch_b, float* dcls, float* 
     a.M = C; a.N = K; a.K = B * NP;
     a.epi = (long long)B * NP > 4096 ? EPI_F32_ATOMIC : EPI_F32_ACC;
     gemm_f32(a, s);
-    patch_small_grads(dcls, dwpe, dpatch_b, dencoded, B, T, C, s);
+    patch_small_grads(dcls, dwpe, dpatch_b, dencoded, B, T, C, s, ws + o_t);
 }
 void sgd_step(float* params, const float* grads, long long n, float lr) {
     sgd(params, grads, n, lr, stream());
@@ -777,7 +849,9 @@ void matmul_backward_bf16(float* dinp, float* dweight, float* dbias, const uint1
 void layernorm_backward_bf16(float* dinp, float* dweight, float* dbias, const uint16_t* dout,
                              const float* inp, const float* weight, const float* mean,
                              const float* rstd, int B, int T, int C) {
-    ln_backward_any(dinp, nullptr, nullptr, dweight, dbias, nullptr, (const bf16_t*)dout, inp, weight,
+    LnbIo io{};
+    io.dinp = dinp; io.dweight = dweight; io.dbias = dbias;
+    ln_backward_any<bf16_t, false>(io, (const bf16_t*)dout, inp, weight,
                     mean, rstd, (long long)B * T, C, stream());
 }
 void gelu_forward_bf16(uint16_t* out, const uint16_t* inp, int N) {

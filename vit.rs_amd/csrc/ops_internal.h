@@ -10,20 +10,21 @@ void ln_forward_f32(float* out, float* mean, float* rstd, const float* inp, cons
                     const float* b, long long rows, int C, hipStream_t s);
 void ln_forward_bf16(bf16_t* out, float* mean, float* rstd, const float* inp, const float* w,
                      const float* b, long long rows, int C, hipStream_t s);
+// dinp += LN_dinp(dout); dw / db += the column sums, in a fixed order through per-block partial
+// rows in ws (nullptr = thread workspace; ln_bwd_blocks(rows) * 2C floats)
 void ln_backward_f32(float* dinp, float* dw, float* db, const float* dout, const float* inp,
                      const float* w, const float* mean, const float* rstd, long long rows, int C,
-                     hipStream_t s);
-// dres_out = dres_in + LN_dinp(dout);  dres_out_bf = bf16(dres_out) (nullable);
-// dres_colsum += column sums of dres_out (nullable: the next bias gradient, fused)
-void ln_backward_fused(float* dres_out, bf16_t* dres_out_bf, const float* dres_in, float* dw,
-                       float* db, float* dres_colsum, const float* dout, const float* inp,
-                       const float* w, const float* mean, const float* rstd, long long rows, int C,
-                       hipStream_t s);
-// the same with the LN-output gradient in bf16 (the dgrad GEMM writes it as bf16)
-void ln_backward_fused_bf16(float* dres_out, bf16_t* dres_out_bf, const float* dres_in, float* dw,
-                            float* db, float* dres_colsum, const bf16_t* dout, const float* inp,
-                            const float* w, const float* mean, const float* rstd, long long rows,
-                            int C, hipStream_t s);
+                     hipStream_t s, float* ws = nullptr);
+// the trainer's residual-gradient stream in "bf16 + lo8" form (common.h lo8_*: a bf16 plane, the
+// GEMM operand, and a byte plane of the rounding residual; lo planes nullable = plain bf16):
+// dres_out = dres_in + LN_dinp(dout); dres_colsum / dw / db as above, taken in fp32 before the
+// rounding; part != null: per-block partial rows [ln_bwd_blocks(rows)][2C or 3C] (dw | db |
+// dres_colsum) instead of atomics, summed later in a fixed order
+void ln_backward_bf16_stream(bf16_t* dres_out, uint8_t* lo_out, const bf16_t* dres_in, const uint8_t* lo_in,
+                             float* dw, float* db, float* dres_colsum, const bf16_t* dout, const float* inp,
+                             const float* w, const float* mean, const float* rstd, long long rows, int C,
+                             hipStream_t s, float* part = nullptr);
+int ln_bwd_blocks(long long rows);
 void convert_f2bf(bf16_t* out, const float* inp, long long n, hipStream_t s);
 void sgd(float* p, const float* g, long long n, float lr, hipStream_t s);
 void softmax_rows(float* probs, const float* logits, long long rows, int V, hipStream_t s);
@@ -40,8 +41,15 @@ void transpose_bf16(bf16_t* out, const bf16_t* in, int R, int Cc, int count, lon
                     hipStream_t s);
 void patch_gather_f32(float* out, const float* denc, int B, int NP, int C, hipStream_t s);
 void patch_gather_bf16(bf16_t* out, const float* denc, int B, int NP, int C, hipStream_t s);
+// (bf16 + lo8 input: lo nullable)
+void patch_gather_f32(float* out, const bf16_t* denc, const uint8_t* lo, int B, int NP, int C, hipStream_t s);
+void patch_gather_bf16(bf16_t* out, const bf16_t* denc, int B, int NP, int C, hipStream_t s);
+// dcls += sum_b denc[b,0];  dwpe[t] += sum_b denc[b,t];  dpb += sum_{b,t>0} denc[b,t] — fixed order
+// (no atomics); ws (nullable = thread workspace): T*C floats of per-position sums
 void patch_small_grads(float* dcls, float* dwpe, float* dpb, const float* denc, int B, int T,
-                       int C, hipStream_t s);
+                       int C, hipStream_t s, float* ws = nullptr);
+void patch_small_grads(float* dcls, float* dwpe, float* dpb, const bf16_t* denc, const uint8_t* lo, int B, int T,
+                       int C, hipStream_t s, float* ws = nullptr);
 // attention.hip
 void attn_forward_f32(float* out, float* preatt, float* att, const float* inp, int B, int T, int C,
                       int NH, hipStream_t s);
@@ -52,11 +60,12 @@ bool attn_fused_supported(int T, int C, int NH);
 bool attn_generic_supported(int T, int C, int NH);  // VALU bf16 kernels (other head sizes, T > 256)
 void attn_forward_fused(bf16_t* out, float* lse, const bf16_t* qkv, int B, int T, int C, int NH,
                         hipStream_t s);
-// dqkv_colsum (nullable, [3C]) += column sums of dqkv (the qkv bias gradient, fused)
+// dqkv_colsum (nullable, [3C]) += column sums of dqkv (the qkv bias gradient, fused, fixed order);
+// colsum_store: dqkv_colsum = the sums instead (a per-micro-batch partial row the trainer reduces)
 // floats of the workspace attn_backward_fused needs (generic delta rows / fused column-sum partials)
 size_t attn_backward_ws_floats(int B, int T, int C, int NH);
 void attn_backward_fused(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t* out,
                          const float* lse, int B, int T, int C, int NH, hipStream_t s,
-                         float* dqkv_colsum = nullptr, float* ws = nullptr);
+                         float* dqkv_colsum = nullptr, float* ws = nullptr, bool colsum_store = false);
 // ws (nullable = thread workspace): B*NH*192 floats — per-(b,h) bias partial sums
 }  // namespace vit

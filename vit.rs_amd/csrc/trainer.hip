@@ -48,6 +48,16 @@ __global__ void bcast_rows_k(float* __restrict__ out, const float* __restrict__ 
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < (long long)rows * n) out[i] = vec[i % n];
 }
+// the CLS rows of a "bf16 + lo8" [B, T, C] tensor (common.h lo8_*) from fp32 rows in[b][c]
+__global__ void rows_to_bf16_k(bf16_t* __restrict__ out, uint8_t* __restrict__ lo, long long ldo,
+                               const float* __restrict__ in, int rows, int C) {
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= (long long)rows * C) return;
+    const long long b = i / C, o = b * ldo + (i - b * C);
+    const bf16_t h = f2bf(in[i]);
+    out[o] = h;
+    lo[o] = (uint8_t)lo8_encode(in[i], bf2f(h));
+}
 __global__ void fill_k(float* p, float v, int n) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) p[i] = v;
@@ -210,7 +220,7 @@ struct Trainer {
     // attention kernels of the main stream (they only read activations and write grads)
     hipStream_t s2 = nullptr;
     bool two_streams = true;
-    enum BwdEv { EV_RESA, EV_RESB, EV_DFCH, EV_DQKV, EV_W1, EV_W2, EV_W3, EV_W4, EV_JOIN, EV_COUNT };
+    enum BwdEv { EV_RESA, EV_RESB, EV_DFCH, EV_DQKV, EV_W1, EV_W2, EV_W3, EV_W4, EV_JOIN, EV_SG, EV_COUNT };
     hipEvent_t bev[EV_COUNT]{};
     // micro-batches: the batch is processed as NMB row ranges on NMB streams (ms[0] = s), so the
     // kernels of one half (GEMM epilogue bursts, LayerNorm, attention) overlap the other's GEMM
@@ -274,6 +284,15 @@ struct Trainer {
     // grads scratch
     float *dlosses = nullptr, *dlogits = nullptr, *dlnf = nullptr, *dcls_x = nullptr;
     float *dres_a = nullptr, *dres_b = nullptr, *dln = nullptr;
+    float* pos_sums = nullptr;  // [T][C] per-position column sums of the patch-embedding backward
+    uint8_t *dres_lo = nullptr, *dres_lo2 = nullptr;  // lo8 planes of the bf16 residual-gradient stream
+    // deterministic small gradients (no float atomics): stream-s scratch for the fixed-order column
+    // sums of the head / fp32 path, and in bf16 / fp8 mode the per-layer partial rows of the
+    // micro-batches' LayerNorm (dw | db | next bias), fc-bias and qkv-bias sums, double-buffered by
+    // layer parity and reduced once per layer on the weight-gradient stream (sg_finalize)
+    float* red_ws = nullptr;
+    float* sg_part[2]{};
+    long long sg_ln2 = 0, sg_ln1 = 0, sg_fcb = 0, sg_qkv = 0;  // offsets (floats) in sg_part[p]
     bf16_t* dln_bf = nullptr;  // bf16 mode: LN-output gradient from the fc / qkv dgrad GEMMs
     bf16_t *dres_bf = nullptr, *dres_bf2 = nullptr, *dfch = nullptr, *datty = nullptr, *dqkv = nullptr, *dpatch_bf = nullptr;
     float* dpatch_f = nullptr;
@@ -513,10 +532,22 @@ struct Trainer {
         dlogits = alloc<float>((long long)B * NC);
         dlnf = alloc<float>((long long)B * C);
         dcls_x = alloc<float>((long long)B * C);
-        dres_a = alloc<float>(BT * C);
-        dres_b = alloc<float>(BT * C);
+        if (!lowp()) {  // the bf16 / fp8 residual-gradient stream is bf16 (dres_bf / dres_bf2)
+            dres_a = alloc<float>(BT * C);
+            dres_b = alloc<float>(BT * C);
+        }
+        pos_sums = alloc<float>((long long)T * C);
+        {  // column-sum / LayerNorm partial rows on s (head, fp32 path)
+            const long long a1 = (long long)ln_bwd_blocks(BT) * 2 * C;
+            const long long a2 = (long long)cdiv(BT, 256) * std::max(4 * C, NC);
+            red_ws = alloc<float>(std::max(a1, a2));
+        }
         emb_tmp = alloc<float>((long long)B * NP * C);
         la.resize(L);
+        if (!lowp()) {  // the fp32 engine's split-K slabs (<= ~16 MB: splits x tiles <= 1024 tiles of 64 x 64)
+            gemm_ws_bytes = (size_t)32 << 20;
+            gemm_ws = alloc<float>((long long)(gemm_ws_bytes / sizeof(float)));
+        }
         if (lowp()) {
             if (!(attn_fused_supported(T, C, NH) || attn_generic_supported(T, C, NH)) || C % 8) {
                 set_error("trainer: bf16 / fp8 path needs head size 32, 64, 80, 96 or 128 and C %% 8 == 0 (T=%d C=%d NH=%d)", T, C, NH);
@@ -553,6 +584,8 @@ struct Trainer {
             dln_bf = alloc<bf16_t>(BT * C);
             dres_bf = alloc<bf16_t>(BT * C);
             dres_bf2 = alloc<bf16_t>(BT * C);
+            dres_lo = alloc<uint8_t>(BT * C);
+            dres_lo2 = alloc<uint8_t>(BT * C);
             dfch = alloc<bf16_t>(BT * 4 * C);
             datty = alloc<bf16_t>(BT * C);
             dqkv = alloc<bf16_t>(BT * 3 * C);
@@ -560,7 +593,17 @@ struct Trainer {
             // slabs: <= 32 splits of the largest weight gradient (4C x C)
             gemm_ws_bytes = (size_t)32 * 4 * C * (size_t)std::max(C, KP) * sizeof(float);
             gemm_ws = alloc<float>((long long)(gemm_ws_bytes / sizeof(float)));
-            attn_part = alloc<float>((long long)attn_backward_ws_floats(B, T, C, NH));  // bias partials | delta
+            attn_part = alloc<float>((long long)attn_backward_ws_floats(B, T, C, NH) + MAXMB * 3LL * C);  // bias partials | delta
+            {  // per-layer small-gradient partial rows for up to MAXMB micro-batches
+                const long long lnr = (long long)MAXMB * ln_bwd_blocks(BT), fcr = cdiv(BT, 128) + MAXMB;
+                sg_ln2 = 0;
+                sg_ln1 = sg_ln2 + lnr * 3 * C;
+                sg_fcb = sg_ln1 + lnr * 3 * C;
+                sg_qkv = sg_fcb + fcr * 4 * C;
+                const long long n = sg_qkv + (long long)MAXMB * 3 * C;
+                sg_part[0] = alloc<float>(n);
+                sg_part[1] = alloc<float>(n);
+            }
             if (fp8()) {
                 const long long ns[NWK] = {3LL * C, C, 4LL * C, C}, ks[NWK] = {C, C, C, 4LL * C};
                 for (int k = 0; k < NWK; k++) {
@@ -747,13 +790,14 @@ struct Trainer {
             a.bias = nullptr;
             a.epi = EPI_F32_ATOMIC;
         }
+        a.ws = gemm_ws; a.ws_bytes = gemm_ws_bytes;
         gemm_f32(a, s);
         softmax_rows(probs, logits, B, NC, s);
         if (has_targets) ce_forward(losses, probs, labels, B, NC, s);
         tend();
     }
-    // dres_cur (zeroed) <- lnf backward on CLS rows
-    void head_backward(float* dres) {
+    // dres_cur (zeroed) <- lnf backward on CLS rows (fp32 dres, or the bf16 stream dres_bf)
+    void head_backward(float* dres, bf16_t* dres_bf = nullptr, uint8_t* dres_lo = nullptr) {
         tbeg(TC_HEAD, 4.0 * B * C * NC);
         fill_k<<<cdiv(B, 256), 256, 0, s>>>(dlosses, 1.0f / (float)b_global, B);
         VIT_HIP(hipMemsetAsync(dlogits, 0, (size_t)B * NC * 4, s));
@@ -763,17 +807,25 @@ struct Trainer {
         a.A = dlogits; a.lda = NC; a.a_kcontig = true;
         a.B = P(P_HEADW); a.ldb = C; a.b_kcontig = false;
         a.C = dlnf; a.ldc = C; a.M = B; a.N = C; a.K = NC; a.epi = lowp() ? EPI_F32_ATOMIC : EPI_F32_ACC;
+        a.ws = gemm_ws; a.ws_bytes = gemm_ws_bytes;
         gemm_f32(a, s);
         GemmArgs w;  // dhead_w += dlogits^T . lnf
         w.A = dlogits; w.lda = NC; w.a_kcontig = false;
         w.B = lnf; w.ldb = C; w.b_kcontig = false;
         w.C = G(P_HEADW); w.ldc = C; w.M = NC; w.N = C; w.K = B; w.epi = lowp() ? EPI_F32_ATOMIC : EPI_F32_ACC;
+        w.ws = gemm_ws; w.ws_bytes = gemm_ws_bytes;
         gemm_f32(w, s);
-        colsum_f32(G(P_HEADB), dlogits, B, NC, NC, s);
+        colsum_f32(G(P_HEADB), dlogits, B, NC, NC, s, red_ws);
         VIT_HIP(hipMemsetAsync(dcls_x, 0, (size_t)B * C * 4, s));
-        ln_backward_f32(dcls_x, G(P_LNFW), G(P_LNFB), dlnf, cls_x, P(P_LNFW), lnf_mean, lnf_rstd, B, C, s);
-        VIT_HIP(hipMemsetAsync(dres, 0, (size_t)BT * C * 4, s));
-        VIT_HIP(hipMemcpy2DAsync(dres, (size_t)T * C * 4, dcls_x, C * 4, C * 4, B, hipMemcpyDeviceToDevice, s));
+        ln_backward_f32(dcls_x, G(P_LNFW), G(P_LNFB), dlnf, cls_x, P(P_LNFW), lnf_mean, lnf_rstd, B, C, s, red_ws);
+        if (dres_bf) {
+            VIT_HIP(hipMemsetAsync(dres_bf, 0, (size_t)BT * C * 2, s));
+            VIT_HIP(hipMemsetAsync(dres_lo, 0, (size_t)BT * C, s));
+            rows_to_bf16_k<<<cdiv((long long)B * C, 256), 256, 0, s>>>(dres_bf, dres_lo, (long long)T * C, dcls_x, B, C);
+        } else {
+            VIT_HIP(hipMemsetAsync(dres, 0, (size_t)BT * C * 4, s));
+            VIT_HIP(hipMemcpy2DAsync(dres, (size_t)T * C * 4, dcls_x, C * 4, C * 4, B, hipMemcpyDeviceToDevice, s));
+        }
         tend();
     }
 
@@ -874,20 +926,54 @@ struct Trainer {
         if (two_streams) VIT_HIP(hipStreamWaitEvent(st, bev[done], 0));
     }
 
+    float* sg_rows(int l, long long off) { return sg_part[l & 1] + off; }
+    // the layer's small gradients from the micro-batches' partial rows, in a fixed order, on the
+    // weight-gradient stream once every micro-batch stream has finished the layer (LN1 backward).
+    // Layer l-2 reuses this parity's rows only after waits on wgrad events recorded after this
+    // reduce (after_wgrad in layer l-1 / l-2), so one pair of buffers suffices.
+    void sg_finalize(int l, long long R) {
+        hipStream_t st = two_streams ? s2 : s;
+        if (two_streams) {
+            for (int mb = 0; mb < nmb; mb++) {
+                VIT_HIP(hipEventRecord(mev[mb][EV_SG], ms[mb]));
+                VIT_HIP(hipStreamWaitEvent(s2, mev[mb][EV_SG], 0));
+            }
+        }
+        const int nb = nmb * ln_bwd_blocks(R), w1 = l > 0 ? 3 * C : 2 * C;
+        const float* p2 = sg_rows(l, sg_ln2);
+        const float* p1 = sg_rows(l, sg_ln1);
+        RowsJob jobs[8] = {
+            {G(P_LN2W, l), p2, nb, 3 * C, C},
+            {G(P_LN2B, l), p2 + C, nb, 3 * C, C},
+            {G(P_ATTPROJB, l), p2 + 2 * C, nb, 3 * C, C},
+            {G(P_LN1W, l), p1, nb, w1, C},
+            {G(P_LN1B, l), p1 + C, nb, w1, C},
+            {G(P_FCB, l), sg_rows(l, sg_fcb), nmb * cdiv(R, 128), 4 * C, 4 * C},
+            {G(P_QKVB, l), sg_rows(l, sg_qkv), nmb, 3 * C, 3 * C},
+            {l > 0 ? G(P_FCPROJB, l - 1) : nullptr, p1 + 2 * C, nb, w1, C},
+        };
+        tbeg(TC_COLSUM, 0, st);
+        rows_reduce_add(jobs, l > 0 ? 8 : 7, st);
+        tend();
+    }
+
     void backward_bf16() {
-        float* dcur = dres_a;
-        float* dnxt = dres_b;
-        bf16_t* rbA = dres_bf;   // bf16 copy of dres3 (read by fcproj dgrad / wgrad)
-        bf16_t* rbB = dres_bf2;  // bf16 copy of dres2 (read by attproj dgrad / wgrad)
-        head_backward(dcur);
+        // the residual-gradient stream is "bf16 + lo8" (common.h: a bf16 plane, the GEMM operand,
+        // plus a byte plane of its rounding residual; a 16-bit significand in 3 bytes): dres3 (the
+        // layer output's gradient) in rbA/loA, dres2 in rbB/loB; each LayerNorm backward reads one
+        // and writes the other (its column sum, the next bias gradient, is taken in fp32)
+        bf16_t* rbA = dres_bf;   // dres3 (read by the fcproj dgrad / wgrad and LN2 backward)
+        bf16_t* rbB = dres_bf2;  // dres2 (read by the attproj dgrad / wgrad and LN1 backward)
+        uint8_t* loA = dres_lo;
+        uint8_t* loB = dres_lo2;
+        head_backward(nullptr, rbA, loA);
         chunk_done(0);
-        convert_f2bf(rbA, dcur, BT * C, s);
         // bias gradients are fused into the kernels that produce each gradient tensor:
         //   fcproj_b += colsum(dres3): LN1-backward of layer l+1 (head rows for the last layer)
         //   fc_b     += colsum(dfch):  fcproj dgrad epilogue
         //   attproj_b+= colsum(dres2): LN2-backward
         //   qkv_b    += colsum(dqkv):  attention backward
-        colsum_f32(G(P_FCPROJB, L - 1), dcls_x, B, C, C, s);
+        colsum_f32(G(P_FCPROJB, L - 1), dcls_x, B, C, C, s, red_ws);
         mb_fork();
         const int Bm = B / nmb;
         const long long R = (long long)Bm * T;
@@ -903,7 +989,7 @@ struct Trainer {
                 d1.A = rbA + r0 * C; d1.lda = C; dgrad_b(d1, P_FCPROJW, l, C, 4 * C);
                 d1.C = dfch + r0 * 4 * C; d1.ldc = 4 * C; d1.aux = a.fchd + r0 * 4 * C; d1.ldaux = 4 * C;
                 d1.M = (int)R; d1.N = 4 * C; d1.K = C; d1.epi = EPI_BF16_MUL;
-                d1.colsum_out = G(P_FCB, l);
+                d1.colsum_part = sg_rows(l, sg_fcb) + (long long)mb * cdiv(R, 128) * 4 * C;
                 gemm_w(TC_FCPROJ_DGRAD, d1, P_FCPROJW, l, true, mb, ms[mb], false, fuse_mx);
             }
             // fc: dln2 = dfch . fcw;  fcw += dfch^T . ln2
@@ -917,12 +1003,12 @@ struct Trainer {
                 // ln2 backward + residual: dres2 = dres3 + LN2'(dln2); attproj_b += colsum(dres2)
                 after_wgrad(EV_W3, ms[mb]);  // the previous layer's attproj wgrad has read rbB
                 tbeg(TC_LN_BWD, 0, ms[mb]);
-                ln_backward_fused_bf16(dnxt + r0 * C, rbB + r0 * C, dcur + r0 * C, G(P_LN2W, l), G(P_LN2B, l),
-                                  G(P_ATTPROJB, l), dln_bf + r0 * C, a.res2 + r0 * C, P(P_LN2W, l),
-                                  a.ln2_mean + r0, a.ln2_rstd + r0, R, C, ms[mb]);
+                ln_backward_bf16_stream(rbB + r0 * C, loB + r0 * C, rbA + r0 * C, loA + r0 * C, G(P_LN2W, l), G(P_LN2B, l),
+                                        G(P_ATTPROJB, l), dln_bf + r0 * C, a.res2 + r0 * C, P(P_LN2W, l),
+                                        a.ln2_mean + r0, a.ln2_rstd + r0, R, C, ms[mb],
+                                        sg_rows(l, sg_ln2) + (long long)mb * ln_bwd_blocks(R) * 3 * C);
                 tend();
             }
-            std::swap(dcur, dnxt);
             // attproj
             wgrad(TC_PROJ_WGRAD, rbB, C, a.atty, C, G(P_ATTPROJW, l), EV_RESB, EV_W3);
             for (int mb = 0; mb < nmb; mb++) {
@@ -935,8 +1021,9 @@ struct Trainer {
                 after_wgrad(EV_W4, ms[mb]);  // the previous layer's qkv wgrad has read dqkv
                 tbeg(TC_ATTN_BWD, 8.0 * Bm * (double)T * T * C, ms[mb]);
                 attn_backward_fused(dqkv + r0 * 3 * C, datty + r0 * C, a.qkv + r0 * 3 * C, a.atty + r0 * C,
-                                    a.lse + (long long)mb * Bm * NH * T, Bm, T, C, NH, ms[mb], G(P_QKVB, l),
-                                    attn_part + (long long)attn_backward_ws_floats(mb * Bm, T, C, NH));
+                                    a.lse + (long long)mb * Bm * NH * T, Bm, T, C, NH, ms[mb],
+                                    sg_rows(l, sg_qkv) + (long long)mb * 3 * C,
+                                    attn_part + (long long)attn_backward_ws_floats(mb * Bm, T, C, NH), true);
                 tend();
             }
             // qkv
@@ -950,12 +1037,13 @@ struct Trainer {
                 // ln1 backward: dres = dres2 + LN1'(dln1); fcproj_b of layer l-1 += colsum(dres)
                 after_wgrad(EV_W1, ms[mb]);  // this layer's fcproj wgrad has read rbA
                 tbeg(TC_LN_BWD, 0, ms[mb]);
-                ln_backward_fused_bf16(dnxt + r0 * C, rbA + r0 * C, dcur + r0 * C, G(P_LN1W, l), G(P_LN1B, l),
-                                  l > 0 ? G(P_FCPROJB, l - 1) : nullptr, dln_bf + r0 * C, xl + r0 * C,
-                                  P(P_LN1W, l), a.ln1_mean + r0, a.ln1_rstd + r0, R, C, ms[mb]);
+                ln_backward_bf16_stream(rbA + r0 * C, loA + r0 * C, rbB + r0 * C, loB + r0 * C, G(P_LN1W, l), G(P_LN1B, l),
+                                        l > 0 ? G(P_FCPROJB, l - 1) : nullptr, dln_bf + r0 * C, xl + r0 * C,
+                                        P(P_LN1W, l), a.ln1_mean + r0, a.ln1_rstd + r0, R, C, ms[mb],
+                                        sg_rows(l, sg_ln1) + (long long)mb * ln_bwd_blocks(R) * (l > 0 ? 3 : 2) * C);
                 tend();
             }
-            std::swap(dcur, dnxt);
+            sg_finalize(l, R);
             chunk_done(L - l);
         }
         mb_join();
@@ -966,13 +1054,13 @@ struct Trainer {
         // patch embedding backward (encoder_backward, train_vit.rs:371 -> ViT)
         tbeg(TC_PATCH_BWD, 2.0 * B * NP * (double)KP * C);
         if (patch_f32) {
-            patch_gather_f32(dpatch_f, dcur, B, NP, C, s);
+            patch_gather_f32(dpatch_f, rbA, loA, B, NP, C, s);
             GemmArgs w;
             w.A = dpatch_f; w.lda = C; w.a_kcontig = false; w.B = patches_f; w.ldb = KP; w.b_kcontig = false;
             w.C = G(P_PATCH_W); w.ldc = KP; w.M = C; w.N = KP; w.K = B * NP; w.epi = EPI_F32_ATOMIC;
             gemm_f32(w, s);
         } else {
-            patch_gather_bf16(dpatch_bf, dcur, B, NP, C, s);
+            patch_gather_bf16(dpatch_bf, rbA, B, NP, C, s);
             GemmArgs w;
             w.A = dpatch_bf; w.lda = C; w.a_kcontig = false;
             w.B = patches_bf; w.ldb = KP; w.b_kcontig = false;
@@ -980,7 +1068,7 @@ struct Trainer {
             w.ws = gemm_ws; w.ws_bytes = gemm_ws_bytes;
             gemm_bf16(w, s);
         }
-        patch_small_grads(G(P_CLS), G(P_WPE), G(P_PATCH_B), dcur, B, T, C, s);
+        patch_small_grads(G(P_CLS), G(P_WPE), G(P_PATCH_B), rbA, loA, B, T, C, s, pos_sums);
         tend();
         chunk_done(L + 1);
     }
@@ -1026,8 +1114,9 @@ struct Trainer {
         GemmArgs g;
         g.A = dout; g.lda = OC; g.a_kcontig = false; g.B = inp; g.ldb = Cin; g.b_kcontig = false;
         g.C = dw; g.ldc = Cin; g.M = OC; g.N = Cin; g.K = (int)BT; g.epi = EPI_F32_ATOMIC;
+        g.ws = gemm_ws; g.ws_bytes = gemm_ws_bytes;
         gemm_f32(g, s);
-        colsum_f32(db, dout, (int)BT, OC, OC, s);
+        colsum_f32(db, dout, (int)BT, OC, OC, s, red_ws);
     }
     void add(float* out, const float* a, const float* b, long long n);
     void gelu(float* out, const float* in, long long n);
@@ -1050,13 +1139,13 @@ struct Trainer {
             gelu_bwd(g_dfch, a.fchf, g_dfchg, BT * 4 * C);
             mm_bwd(g_dln2, G(P_FCW, l), G(P_FCB, l), g_dfch, a.ln2f, P(P_FCW, l), C, 4 * C);
             ln_backward_f32(g_dres2, G(P_LN2W, l), G(P_LN2B, l), g_dln2, a.res2, P(P_LN2W, l),
-                            a.ln2_mean, a.ln2_rstd, BT, C, s);
+                            a.ln2_mean, a.ln2_rstd, BT, C, s, red_ws);
             res_bwd(dnxt, g_dattproj, g_dres2, BT * C);
             mm_bwd(g_datty, G(P_ATTPROJW, l), G(P_ATTPROJB, l), g_dattproj, a.attyf, P(P_ATTPROJW, l), C, C);
             attn_backward_f32(g_dqkv, g_dpreatt, g_datt, g_datty, a.qkvf, a.att, B, T, C, NH, s);
             mm_bwd(g_dln1, G(P_QKVW, l), G(P_QKVB, l), g_dqkv, a.ln1f, P(P_QKVW, l), C, 3 * C);
             ln_backward_f32(dnxt, G(P_LN1W, l), G(P_LN1B, l), g_dln1, x, P(P_LN1W, l), a.ln1_mean,
-                            a.ln1_rstd, BT, C, s);
+                            a.ln1_rstd, BT, C, s, red_ws);
             std::swap(dcur, dnxt);
             chunk_done(L - l);
         }
@@ -1065,8 +1154,9 @@ struct Trainer {
         GemmArgs w;
         w.A = dpatch_f; w.lda = C; w.a_kcontig = false; w.B = patches_f; w.ldb = KP; w.b_kcontig = false;
         w.C = G(P_PATCH_W); w.ldc = KP; w.M = C; w.N = KP; w.K = B * NP; w.epi = EPI_F32_ATOMIC;
+        w.ws = gemm_ws; w.ws_bytes = gemm_ws_bytes;
         gemm_f32(w, s);
-        patch_small_grads(G(P_CLS), G(P_WPE), G(P_PATCH_B), dcur, B, T, C, s);
+        patch_small_grads(G(P_CLS), G(P_WPE), G(P_PATCH_B), dcur, B, T, C, s, pos_sums);
         chunk_done(L + 1);
     }
 
