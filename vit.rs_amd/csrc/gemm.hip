@@ -706,40 +706,77 @@ __global__ __launch_bounds__(256) void colsum_part_k(float* __restrict__ out, co
     else out[(long long)blockIdx.y * N + n] = s;
 }
 
-// rows_reduce_add: workgroup = 64 columns x 4 row phases of one job; each thread sums the rows
-// r = phase (mod 4) in ascending order, the 4 phases are added in a fixed order
+// rows_reduce_add.  Vector form (ncols, ld % 4 == 0, 16-B aligned src): a workgroup takes 64
+// columns of one job as 16 float4 lanes x 16 row phases; phase p sums rows p, p+16, ... in two
+// interleaved chains (rows p+32i and p+16+32i), then the 16 phases are added in ascending order.
+// Scalar form otherwise: 64 columns x 4 phases.  Both orders are fixed: deterministic.
 struct RowsJobs {
     RowsJob j[ROWS_MAX_JOBS];
     int blk0[ROWS_MAX_JOBS + 1];
+    int vec;
 };
 __global__ __launch_bounds__(256) void rows_reduce_k(RowsJobs jobs) {
-    __shared__ float red[4][64];
+    __shared__ float4 red[16][17];
     int jb = 0;
 #pragma unroll 1
     while (jb + 1 < ROWS_MAX_JOBS && (int)blockIdx.x >= jobs.blk0[jb + 1]) jb++;
     const RowsJob& J = jobs.j[jb];
-    const int c = (blockIdx.x - jobs.blk0[jb]) * 64 + (threadIdx.x & 63), ph = threadIdx.x >> 6;
+    const int c0 = (blockIdx.x - jobs.blk0[jb]) * 64;
+    if (jobs.vec) {
+        const int q = threadIdx.x & 15, ph = threadIdx.x >> 4, c = c0 + 4 * q;
+        float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
+        if (c < J.ncols) {
+            const float* base = J.src + c;
+            int r = ph;
+            for (; r + 16 < J.nrows; r += 32) {
+                const float4 a = *reinterpret_cast<const float4*>(base + (long long)r * J.ld);
+                const float4 b = *reinterpret_cast<const float4*>(base + (long long)(r + 16) * J.ld);
+                s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
+                s1.x += b.x; s1.y += b.y; s1.z += b.z; s1.w += b.w;
+            }
+            if (r < J.nrows) {
+                const float4 a = *reinterpret_cast<const float4*>(base + (long long)r * J.ld);
+                s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
+            }
+        }
+        red[ph][q] = make_float4(s0.x + s1.x, s0.y + s1.y, s0.z + s1.z, s0.w + s1.w);
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            const int qq = threadIdx.x >> 2, e = threadIdx.x & 3, cc = c0 + threadIdx.x;
+            float t = 0.f;
+#pragma unroll
+            for (int p = 0; p < 16; p++) t += reinterpret_cast<const float*>(&red[p][qq])[e];
+            if (cc < J.ncols) J.dst[cc] += t;
+        }
+        return;
+    }
+    float* reds = reinterpret_cast<float*>(red);  // [4][64]
+    const int c = c0 + (threadIdx.x & 63), ph = threadIdx.x >> 6;
     float s0 = 0.f, s1 = 0.f;
     if (c < J.ncols) {
         int r = ph;
-        for (; r + 4 < J.nrows; r += 8) {  // two independent chains: rows ph+8i and ph+4+8i
+        for (; r + 4 < J.nrows; r += 8) {  // two chains: rows ph+8i and ph+4+8i
             s0 += J.src[(long long)r * J.ld + c];
             s1 += J.src[(long long)(r + 4) * J.ld + c];
         }
         if (r < J.nrows) s0 += J.src[(long long)r * J.ld + c];
     }
-    red[ph][threadIdx.x & 63] = s0 + s1;
+    reds[ph * 64 + (threadIdx.x & 63)] = s0 + s1;
     __syncthreads();
-    if (ph == 0 && c < J.ncols) J.dst[c] += ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+    if (ph == 0 && c < J.ncols)
+        J.dst[c] += ((reds[threadIdx.x] + reds[64 + threadIdx.x]) + reds[128 + threadIdx.x]) + reds[192 + threadIdx.x];
 }
 void rows_reduce_add(const RowsJob* jobs, int njobs, hipStream_t s) {
     for (int b = 0; b < njobs; b += ROWS_MAX_JOBS) {
         RowsJobs J{};
+        J.vec = 1;
         int nb = 0, k = 0;
         for (; k < ROWS_MAX_JOBS && b + k < njobs; k++) {
-            J.j[k] = jobs[b + k];
+            const RowsJob& x = jobs[b + k];
+            J.j[k] = x;
             J.blk0[k] = nb;
-            nb += J.j[k].nrows > 0 ? cdiv(J.j[k].ncols, 64) : 0;
+            nb += x.nrows > 0 ? cdiv(x.ncols, 64) : 0;
+            if (x.nrows > 0 && ((x.ncols | x.ld) % 4 || ((uintptr_t)x.src & 15))) J.vec = 0;
         }
         for (; k <= ROWS_MAX_JOBS; k++) J.blk0[k] = nb;
         if (nb == 0) continue;

@@ -412,7 +412,7 @@ __device__ __forceinline__ void staged_colsum(const GemmParams& p, int lane, int
                 t += __shfl_xor(t, 32, 64);
                 cs[j] = t;
             }
-            if (rr == 0) {
+            if (rr == 0 && m0 < p.M) {  // (a wave tile wholly past M has no partial row)
 #pragma unroll
                 for (int j = 0; j < 8; j++)
                     if (n0 + cc + j < p.N) p.colsum_out[(long long)(m0 >> 7) * p.N + n0 + cc + j] = cs[j];
