@@ -991,6 +991,12 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
 }
 
 template <int HS, int NKT, int KK = 2>
+// VIT_ATTN_SKEW: the persistent backward runs phase B of slice s-1 right after phase A of slice s
+// (dS^T double-buffered), one barrier per slice instead of two, so the two phases' MFMA, VALU and
+// LDS work share one barrier interval
+#ifndef VIT_ATTN_SKEW
+#define VIT_ATTN_SKEW 1
+#endif
 struct Bwdp {
     using G = Geo<HS>;
     static constexpr int TP = NKT * 16, NW = NKT / KK, NT = NW * 64, NSL = TP / 32, CH = G::CH;
@@ -999,8 +1005,9 @@ struct Bwdp {
     static constexpr int V_OFF = K_OFF + 2 * TP * SV * 2;    // next item's V rows [TP][SK]
     static constexpr int Q_OFF = V_OFF + TP * SK * 2;        // Q slices [2][32][SL]
     static constexpr int D_OFF = Q_OFF + 2 * 32 * SL * 2;    // dO slices [2][32][SL]
-    static constexpr int S_OFF = D_OFF + 2 * 32 * SL * 2;    // dS^T [TP][SDS]
-    static constexpr int L_OFF = S_OFF + TP * SDS * 2;       // lse [2][TP] (item parity)
+    static constexpr int NDS = VIT_ATTN_SKEW ? 2 : 1;       // dS^T buffers
+    static constexpr int S_OFF = D_OFF + 2 * 32 * SL * 2;    // dS^T [NDS][TP][SDS]
+    static constexpr int L_OFF = S_OFF + NDS * TP * SDS * 2; // lse [2][TP] (item parity)
     static constexpr int E_OFF = L_OFF + 2 * TP * 4;         // delta [2][32] (slice parity)
     static constexpr int BYTES = E_OFF + 2 * 32 * 4;
     static constexpr int PER = (32 * CH + NT - 1) / NT;      // 16-B pieces per thread, slice operand
@@ -1152,15 +1159,37 @@ __global__ __launch_bounds__(NKT / KK * 64, 1) void attn_bwdp_k(bf16_t* __restri
             fetch_side(s_nxt, sl);
             // unconditional load (past T: 0); padded keys get +inf when it is put
             if (sl == 0) lse_n = buf_ldf(s_nxt.l, 4 * tid);
-            bwd_slice_a<HS, KK>(R, Qs + cur * 32 * SL, Ds + cur * 32 * SL, lse_cur + q0, del_s + cur * 32,
-                                dSs + key0 * Z::SDS, c, lane);
-            __syncthreads();
-            // buffers written here were last read before the barrier above (slice buffer cur^1 by
-            // the previous slice, the idle K image by the previous item, the V rows by load_kv)
-            put_slice(cur ^ 1);
-            put_side(kb ^ 1, sl);
-            if (sl == 0 && tid < TP) lse_s[((n + 1) & 1) * TP + tid] = tid < T ? lse_n : INFINITY;
-            bwd_slice_b<HS, NSL, NW>(Kimg + kb * TP * SV, dSs, dq, C3, q0, T, scale, w, lane);
+            if constexpr (VIT_ATTN_SKEW) {
+                // A(sl) -> dS^T buffer sl&1; B(sl-1) from buffer (sl-1)&1 (complete since the last
+                // barrier); the slice buffers cur^1 were last read by A(sl-1), before that barrier
+                bf16_t* dS_a = dSs + (sl & 1) * TP * Z::SDS;
+                bwd_slice_a<HS, KK>(R, Qs + cur * 32 * SL, Ds + cur * 32 * SL, lse_cur + q0, del_s + cur * 32,
+                                    dS_a + key0 * Z::SDS, c, lane);
+                if (sl > 0)
+                    bwd_slice_b<HS, NSL, NW>(Kimg + kb * TP * SV, dSs + ((sl - 1) & 1) * TP * Z::SDS, dq, C3,
+                                             q0 - 32, T, scale, w, lane);
+                put_slice(cur ^ 1);
+                if (sl == 0 && tid < TP) lse_s[((n + 1) & 1) * TP + tid] = tid < T ? lse_n : INFINITY;
+                __syncthreads();
+                // the next item's K image / V rows: after the barrier, so every wave has finished
+                // this item's load_kv reads of the V rows (item start) before any block is replaced
+                put_side(kb ^ 1, sl);
+            } else {
+                bwd_slice_a<HS, KK>(R, Qs + cur * 32 * SL, Ds + cur * 32 * SL, lse_cur + q0, del_s + cur * 32,
+                                    dSs + key0 * Z::SDS, c, lane);
+                __syncthreads();
+                // buffers written here were last read before the barrier above (slice buffer cur^1 by
+                // the previous slice, the idle K image by the previous item, the V rows by load_kv)
+                put_slice(cur ^ 1);
+                put_side(kb ^ 1, sl);
+                if (sl == 0 && tid < TP) lse_s[((n + 1) & 1) * TP + tid] = tid < T ? lse_n : INFINITY;
+                bwd_slice_b<HS, NSL, NW>(Kimg + kb * TP * SV, dSs, dq, C3, q0, T, scale, w, lane);
+                __syncthreads();
+            }
+        }
+        if constexpr (VIT_ATTN_SKEW) {  // the item's last phase B; the barrier also publishes the last put_side
+            bwd_slice_b<HS, NSL, NW>(Kimg + kb * TP * SV, dSs + ((NSL - 1) & 1) * TP * Z::SDS, dq, C3,
+                                     (NSL - 1) * 32, T, scale, w, lane);
             __syncthreads();
         }
         bwd_item_end<HS, KK>(R, dq, C, key0, T, scale,

@@ -419,6 +419,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
         bar();
     }
     if (nk > 0 && !lagging) bar();  // balance the stagger barrier
+    float bpre[8];  // the epilogue's bias columns, loaded under the trailing DMA wait
+    staged_bias_prefetch<EPI>(p, lane, tn0 + wn * 64, bpre);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // retire the trailing re-staged pieces
     __builtin_amdgcn_s_setprio(0);
     if constexpr (!AK) {
@@ -437,7 +439,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    staged_epilogue<EPI>(p, acc, smem + wave * STG_WAVE_BYTES, lane, tm0 + wm * 128, tn0 + wn * 64);
+    staged_epilogue<EPI>(p, acc, smem + wave * STG_WAVE_BYTES, lane, tm0 + wm * 128, tn0 + wn * 64, bpre);
 }
 
 }  // namespace g2

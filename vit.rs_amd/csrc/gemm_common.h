@@ -95,7 +95,7 @@ __device__ __forceinline__ epi_u32x4 epi_ld16(const GemmParams&, const void* q) 
 // diagnostic: time the main loop alone (the accumulators stay live so nothing is eliminated)
 template <int NA, int NB>
 __device__ __forceinline__ bool skip_epilogue(const GemmParams& p, f32x4_t (&acc)[NA][NB]) {
-    if (!p.no_epi) return false;
+    if (!(p.no_epi & 1)) return false;
 #pragma unroll
     for (int a = 0; a < NA; a++)
 #pragma unroll
@@ -256,14 +256,43 @@ constexpr int STG_WAVE_BYTES = 64 * STG_LD * 4;  // 17,408 B per wave
 // between loads and stores.  The generic loop below serialised load -> s_waitcnt vmcnt(0) ->
 // compute -> store per 8-row step (the wait also drained the previous step's stores), so the
 // DGELU / RESID epilogues ran one HBM round trip per step.
+typedef unsigned int epi_u32x4v __attribute__((ext_vector_type(4)));
+// the aux operand rows of one interior 64-row pass (bf16: 8 x 16 B per lane, fp32: 16 x 16 B)
+template <int EPI>
+struct EpiAux {
+    static constexpr bool AUX16 = epi_aux16(EPI);
+    static constexpr bool AUX32 = EPI == EPI_F32_RESID || EPI == EPI_F32_ACC;
+    static constexpr int N = AUX16 ? 8 : (AUX32 ? 16 : 0);
+    epi_u32x4v ax[N > 0 ? N : 1];
+    __device__ __forceinline__ void load(const GemmParams& p, int rr, int mrow, int n) {
+        if constexpr (AUX16) {
+#pragma unroll
+            for (int it = 0; it < 8; it++)
+                ax[it] = epi_ld16(p, (const bf16_t*)p.aux + (long long)(mrow + it * 8 + rr) * p.ldaux + n);
+        } else if constexpr (AUX32) {
+            const float* src = EPI == EPI_F32_RESID ? (const float*)p.aux : (const float*)p.C;
+            const long long ld = EPI == EPI_F32_RESID ? p.ldaux : p.ldc;
+#pragma unroll
+            for (int it = 0; it < 8; it++) {
+                const float* q = src + (long long)(mrow + it * 8 + rr) * ld + n;
+                ax[2 * it] = epi_ld16(p, q);
+                ax[2 * it + 1] = epi_ld16(p, q + 4);
+            }
+        }
+    }
+};
 template <int EPI>
 __device__ __forceinline__ void staged_pass_interior(const GemmParams& p, const float* st, int rr,
-                                                     int cc, int mrow, int n, float (&cs)[8]) {
+                                                     int cc, int mrow, int n, float (&cs)[8],
+                                                     const float* bpre, const EpiAux<EPI>* pre = nullptr) {
     const int cc_lane = cc >> 3;  // the lane's column group (lane bits 0-2): mx_out8's block lanes
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if constexpr (epi_bias(EPI)) {
-        if (p.bias) {
+        if (bpre) {  // the lane's 8 bias values, loaded by the caller under the main loop's tail
+#pragma unroll
+            for (int j = 0; j < 8; j++) bv[j] = bpre[j];
+        } else if (p.bias) {
             const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
             const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
             bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w;
@@ -272,21 +301,9 @@ __device__ __forceinline__ void staged_pass_interior(const GemmParams& p, const 
     }
     constexpr bool AUX16 = epi_aux16(EPI);
     constexpr bool AUX32 = EPI == EPI_F32_RESID || EPI == EPI_F32_ACC;
-    u32x4 ax[AUX16 ? 8 : (AUX32 ? 16 : 1)];
-    if constexpr (AUX16) {
-#pragma unroll
-        for (int it = 0; it < 8; it++)
-            ax[it] = epi_ld16(p, (const bf16_t*)p.aux + (long long)(mrow + it * 8 + rr) * p.ldaux + n);
-    } else if constexpr (AUX32) {
-        const float* src = EPI == EPI_F32_RESID ? (const float*)p.aux : (const float*)p.C;
-        const long long ld = EPI == EPI_F32_RESID ? p.ldaux : p.ldc;
-#pragma unroll
-        for (int it = 0; it < 8; it++) {
-            const float* q = src + (long long)(mrow + it * 8 + rr) * ld + n;
-            ax[2 * it] = epi_ld16(p, q);
-            ax[2 * it + 1] = epi_ld16(p, q + 4);
-        }
-    }
+    EpiAux<EPI> own;
+    if (!pre) own.load(p, rr, mrow, n);
+    const u32x4* ax = pre ? pre->ax : own.ax;
     float* slab = nullptr;
     if constexpr (EPI == EPI_F32_SLAB) slab = (float*)p.C + (long long)split_index(p.tiles) * p.M * p.ldc;
 #pragma unroll
@@ -362,10 +379,11 @@ GemmParams make_gemm_params(const GemmArgs& a, int kchunk);  // gemm.hip
 // 64*pass + r): every lane owns 8 consecutive columns of a row per access
 template <int EPI>
 __device__ __forceinline__ void staged_pass(const GemmParams& p, const float* st, int lane, int m0,
-                                            int n0, int pass, bool interior, float (&cs)[8]) {
+                                            int n0, int pass, bool interior, float (&cs)[8],
+                                            const float* bpre = nullptr, const EpiAux<EPI>* pre = nullptr) {
     const int rr = lane >> 3, cc = (lane & 7) * 8;
     if (interior) {
-        staged_pass_interior<EPI>(p, st, rr, cc, m0 + pass * 64, n0 + cc, cs);
+        staged_pass_interior<EPI>(p, st, rr, cc, m0 + pass * 64, n0 + cc, cs, bpre, pre);
         return;
     }
 #pragma unroll
@@ -421,21 +439,55 @@ __device__ __forceinline__ void staged_colsum(const GemmParams& p, int lane, int
     }
 }
 
+// the lane's 8 bias columns of the staged epilogue (n0 + 8 (lane & 7) ..), loaded ahead of it so
+// the epilogue's first pass does not wait a memory round trip for them (zeros past N / no bias)
+template <int EPI>
+__device__ __forceinline__ void staged_bias_prefetch(const GemmParams& p, int lane, int n0, float (&bv)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) bv[j] = 0.f;
+    if constexpr (epi_bias(EPI)) {
+        const int n = n0 + (lane & 7) * 8;
+        if (p.bias && n + 8 <= p.N) {
+            const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
+            const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
+            bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w;
+            bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+        }
+    }
+}
 template <int EPI>
 __device__ __forceinline__ void staged_epilogue(const GemmParams& p, f32x4_t (&acc)[8][4],
-                                                char* stage, int lane, int m0, int n0) {
+                                                char* stage, int lane, int m0, int n0,
+                                                const float* bpre = nullptr) {
     float* st = reinterpret_cast<float*>(stage);
     const int i = lane & 15, g = lane >> 4;
     float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const bool interior = staged_interior<EPI>(p, m0, n0);
-#pragma unroll
-    for (int pass = 0; pass < 2; pass++) {
+    auto stage_pass = [&](int pass) {
 #pragma unroll
         for (int a = 0; a < 4; a++)
 #pragma unroll
             for (int b = 0; b < 4; b++)
                 *reinterpret_cast<f32x4_t*>(st + (a * 16 + i) * STG_LD + b * 16 + 4 * g) = acc[pass * 4 + a][b];
-        staged_pass<EPI>(p, st, lane, m0, n0, pass, interior, cs);
+    };
+    if (interior && EpiAux<EPI>::N > 0) {
+        // aux-reading epilogues: both passes' aux rows are loaded up front, so the second pass
+        // waits for its own loads only (vmcnt counts in issue order: loads issued after the first
+        // pass's stores would wait for those stores too)
+        const int rr = lane >> 3, n = n0 + (lane & 7) * 8;
+        EpiAux<EPI> a0, a1;
+        a0.load(p, rr, m0, n);
+        a1.load(p, rr, m0 + 64, n);
+        stage_pass(0);
+        staged_pass_interior<EPI>(p, st, rr, (lane & 7) * 8, m0, n, cs, bpre, &a0);
+        stage_pass(1);
+        staged_pass_interior<EPI>(p, st, rr, (lane & 7) * 8, m0 + 64, n, cs, bpre, &a1);
+    } else {
+#pragma unroll
+        for (int pass = 0; pass < 2; pass++) {
+            stage_pass(pass);
+            staged_pass<EPI>(p, st, lane, m0, n0, pass, interior, cs, bpre);
+        }
     }
     staged_colsum<EPI>(p, lane, m0, n0, cs);
 }

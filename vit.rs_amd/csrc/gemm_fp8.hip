@@ -197,7 +197,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(F8Params fp) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_setprio(0);
 
-    if (p.no_epi) {  // diagnostic: main loop only; keep the accumulators live (in 16-B pieces: a
+    if (p.no_epi & 1) {  // diagnostic: main loop only; keep the accumulators live (in 16-B pieces: a
                      // 64-B "v" asm operand makes hipcc drop the host stubs of the other instances)
 #pragma unroll
         for (int a = 0; a < 4; a++)
