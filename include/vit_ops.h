@@ -183,12 +183,21 @@ void gemm_bf16_fused(void* C, void* C2, long long ldc, const void* aux, long lon
  * bytes per operand.  quantize_mx_*: x [R][K] (row stride ldx elements, K % 64 == 0) -> q [R][K]
  * e4m3 (row stride ldq bytes) + scales; scale 2^X with X = ceil(log2(amax / 448)) per block,
  * x * 2^-X rounded to nearest even.  gemm_fp8_fused: C = A . B^T with A [M][K], B [N][K]
- * (K-contiguous bytes) and the epilogues of gemm_bf16_fused (epi 0, 1, 3, 4, 5, 6, 8, 9). */
+ * (K-contiguous bytes) and the epilogues of gemm_bf16_fused (epi 0, 1, 2, 3, 4, 5, 6, 8, 9; epi 2 =
+ * C += A . B^T through K-split fp32 slabs and a fixed-order reduce: the fp8 weight gradient of
+ * matmul_backward, train_vit.rs:543-555, with A / B from quantize_mx_cols_bf16_ex). */
 long long mx_scale_size(long long rows, int K);
 void quantize_mx_bf16_ex(uint8_t* q, uint8_t* scales, const uint16_t* x, long long R, int K,
                          long long ldx, long long ldq);
 void quantize_mx_f32_ex(uint8_t* q, uint8_t* scales, const float* x, long long R, int K,
                         long long ldx, long long ldq);
+/* column-wise MX (blocks of 32 consecutive ROWS of x: the token axis a weight gradient reduces
+ * over): x [R][C] bf16 (row stride ldx, C % 64 == 0) -> q [C][Kp] e4m3, Kp = mx_cols_padded(R)
+ * (R rounded up to 64, padding tokens zero) + scales (mx_scale_size(C, Kp) bytes); equal, byte for
+ * byte, to quantize_mx_bf16_ex of the zero-padded transpose. */
+long long mx_cols_padded(long long R);
+void quantize_mx_cols_bf16_ex(uint8_t* q, uint8_t* scales, const uint16_t* x, long long R, int C,
+                              long long ldx);
 void gemm_fp8_fused(void* C, void* C2, long long ldc, const void* aux, long long ldaux,
                     const uint8_t* A, const uint8_t* a_scale, long long lda, const uint8_t* B,
                     const uint8_t* b_scale, long long ldb, const float* bias, float* colsum_out,

@@ -177,3 +177,59 @@ def test_gemm_fp8_fused_mx_output(gpu, M, N, K):
         else:
             v.call("gemm_fp8_fused", c0, None, N, xb, N, qa, sa, K, qw, sw, K, None, None, M, N, K, epi)
         assert np.array_equal(c0.numpy(), c.numpy())
+
+
+@pytest.mark.parametrize("R,C", [(1, 64), (100, 128), (197, 768), (4001, 320), (50432 // 8, 1280)])
+def test_quantize_mx_cols_bit_exact(gpu, R, C):
+    """Column-wise MX (the fp8 weight gradients' operands: blocks of 32 consecutive tokens) equals
+    the row quantizer's restatement applied to the zero-padded transpose, byte for byte, including
+    the padding tokens (zero bytes) and the padding rows' zero scales."""
+    v = gpu
+    rng = np.random.default_rng(R * 7 + C)
+    x = (rng.normal(size=(R, C)) * np.exp2(rng.integers(-12, 12, size=(1, C)))).astype(np.float32)
+    x[rng.random(size=x.shape) < 0.01] = 0.0
+    xb = v.bf16_bits(x)
+    xr = v.bf16_to_f32(xb).reshape(R, C)
+    kp = int(v.lib().mx_cols_padded(R))
+    assert kp == (R + 63) // 64 * 64
+    nsc = int(v.lib().mx_scale_size(C, kp))
+    q = D(v, np.full(C * kp, 0x5A, np.uint8), np.uint8)   # poison: every byte must be written
+    sl = D(v, np.full(nsc, 0x5A, np.uint8), np.uint8)
+    v.call("quantize_mx_cols_bf16_ex", q, sl, D(v, xb, np.uint16), R, C, C)
+    t = np.zeros((C, kp), np.float32)
+    t[:, :R] = xr.T
+    q_ref, sb_ref = mx.quantize(t)
+    assert np.array_equal(sl.numpy(), mx.to_lane_native(sb_ref))
+    assert np.array_equal(q.numpy().reshape(C, kp), q_ref)
+
+
+@pytest.mark.parametrize("OC,Cin,R", [(256, 256, 64), (768, 320, 1000), (1280, 5120, 4112), (512, 768, 6000)])
+def test_gemm_fp8_wgrad_splitk(gpu, OC, Cin, R):
+    """The fp8 weight gradient dW += dout^T . inp (epi 2) on column-quantized operands: one split
+    accumulating in place (the small shapes) or K-split fp32 slabs + the fixed-order reduce (2 and 5
+    splits) equal float64 numpy on the dequantized operands to 1e-4, and two launches give
+    bit-identical results (no atomics)."""
+    v = gpu
+    rng = np.random.default_rng(OC + Cin + R)
+    dout = rng.normal(size=(R, OC)).astype(np.float32)
+    inp = rng.normal(size=(R, Cin)).astype(np.float32)
+    kp = int(v.lib().mx_cols_padded(R))
+
+    def colq(x):
+        C = x.shape[1]
+        q = Z(v, C * kp, np.uint8)
+        sl = Z(v, int(v.lib().mx_scale_size(C, kp)), np.uint8)
+        v.call("quantize_mx_cols_bf16_ex", q, sl, D(v, v.bf16_bits(x), np.uint16), R, C, C)
+        return q, sl, mx.dequantize(q.numpy().reshape(C, kp), mx.from_lane_native(sl.numpy(), C, kp))
+
+    qa, sa, ar = colq(dout)
+    qb, sb, br = colq(inp)
+    dw0 = rng.normal(size=(OC, Cin)).astype(np.float32)
+    want = dw0 + ar @ br.T
+    outs = []
+    for _ in range(2):
+        dw = D(v, dw0)
+        v.call("gemm_fp8_fused", dw, None, Cin, None, 0, qa, sa, kp, qb, sb, kp, None, None, OC, Cin, kp, 2)
+        outs.append(dw.numpy())
+    assert rel_err(outs[0].reshape(OC, Cin), want) < 1e-4
+    assert np.array_equal(outs[0], outs[1])

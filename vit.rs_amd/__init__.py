@@ -104,6 +104,8 @@ _SIGS = {
     "mx_scale_size": (LL, [LL, I]),
     "quantize_mx_bf16_ex": (None, [P, P, P, LL, I, LL, LL]),
     "quantize_mx_f32_ex": (None, [P, P, P, LL, I, LL, LL]),
+    "mx_cols_padded": (LL, [LL]),
+    "quantize_mx_cols_bf16_ex": (None, [P, P, P, LL, I, LL]),
     "gemm_fp8_fused": (None, [P, P, LL, P, LL, P, P, LL, P, P, LL, P, P, I, I, I, I]),
     "gemm_fp8_fused_mx": (None, [P, P, LL, P, LL, P, P, LL, P, P, LL, P, P, I, I, I, I, P, P]),
     "gemm_bf16_set_variant": (None, [I]), "gemm_bf16_set_debug": (None, [I]),

@@ -87,8 +87,8 @@ void gemm_set_debug(int flags);
 
 // fp8 (OCP e4m3) operands with MX block scales (one E8M0 per 32 k-elements), fp32 accumulate
 // (v_mfma_scale_f32_32x32x64_f8f6f4): A [M][K], B [N][K] K-contiguous byte rows (lda/ldb in
-// bytes, % 16 == 0), K % 64 == 0, scales from quantize_mx_* (a_scale / b_scale); every epilogue
-// except the split-K ones.
+// bytes, % 16 == 0), K % 64 == 0, scales from quantize_mx_* (a_scale / b_scale); every epilogue,
+// EPI_F32_ATOMIC as K-split fp32 slabs + a fixed-order reduce (a.ws or the thread workspace).
 void gemm_fp8(const GemmArgs& a, hipStream_t s);
 bool gemm_fp8_supported(const GemmArgs& a);
 // MX quantizer: x [R][K] (row stride ldx elements) -> q [R][K] e4m3 (row stride ldq bytes) +
@@ -102,6 +102,11 @@ void quantize_mx_batched_bf16(uint8_t* q, uint8_t* sl, const bf16_t* x, long lon
                               long long xs, long long qs, long long ss, hipStream_t s);
 void quantize_mx_batched_f32(uint8_t* q, uint8_t* sl, const float* x, long long R, int K, int count,
                              long long xs, long long qs, long long ss, hipStream_t s);
+// column-wise MX for the fp8 weight gradients: x [R tokens][C] bf16 (row stride ldx, C % 64 == 0)
+// -> q [C][Kp] e4m3, Kp = mx_cols_kp(R) (R rounded up to 64; padding tokens are zeros) + scales
+// for C rows and K = Kp (mx_scale_bytes(C, Kp)): the MX quantization of the padded transpose
+void quantize_mx_cols_bf16(uint8_t* q, uint8_t* sl, const bf16_t* x, long long R, int C, long long ldx, hipStream_t s);
+long long mx_cols_kp(long long R);
 long long mx_rows_padded(long long rows);
 size_t mx_scale_bytes(long long rows, int K);
 

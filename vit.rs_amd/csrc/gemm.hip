@@ -879,7 +879,7 @@ GemmParams make_gemm_params(const GemmArgs& a, int kchunk) {
 
 // split-K for one-block-per-CU kernels: the smallest split whose last wave of blocks fills
 // >= 90% of the 256 CUs (or the best fill up to 32), keeping >= 16 K-tiles per split
-static int choose_split_waves(int tiles, int nk) {
+int choose_split_waves(int tiles, int nk) {
     const int slots = 256;
     int best = 1;
     double best_eff = 0.0;
@@ -905,13 +905,13 @@ static int grid_blocks(long long n) {
     return (int)(b < 1 ? 1 : (b > 4096 ? 4096 : b));
 }
 // split-K slabs: the caller's buffer (a.ws) or the thread workspace; error when neither fits
-static float* slab_buffer(const GemmArgs& a, int split) {
+float* slab_buffer(const GemmArgs& a, int split) {
     const size_t need = (size_t)split * a.M * a.N * sizeof(float);
     float* slab = a.ws ? (a.ws_bytes >= need ? a.ws : nullptr) : (float*)workspace(need);
     if (!slab) set_error("gemm: split-K workspace of %zu bytes unavailable", need);
     return slab;
 }
-static void slab_reduce(const GemmArgs& a, float* slab, int split, hipStream_t s) {
+void slab_reduce(const GemmArgs& a, float* slab, int split, hipStream_t s) {
     if (a.N % 4 == 0)
         slab_reduce_k<<<grid_blocks((long long)a.M * a.N / 4), 256, 0, s>>>((float*)a.C, a.ldc, slab, a.M, a.N, split);
     else

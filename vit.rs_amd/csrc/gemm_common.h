@@ -66,6 +66,12 @@ __device__ __forceinline__ void mx_out8(const GemmParams& p, int m, int n, uint3
 // workspace; nullptr when the GEMM sums no columns) and the fixed-order add into colsum_out
 float* colsum_rows_begin(const GemmArgs& a);
 void colsum_rows_end(const GemmArgs& a, float* rows, hipStream_t s);
+// host, split-K of the one-workgroup-per-CU engines (gemm.hip): the split count for `tiles` output
+// tiles over nk K-steps; the fp32 slab workspace of `split` partial planes (a.ws or the thread
+// workspace; nullptr + error when neither fits); C += sum of the slabs in a fixed order
+int choose_split_waves(int tiles, int nk);
+float* slab_buffer(const GemmArgs& a, int split);
+void slab_reduce(const GemmArgs& a, float* slab, int split, hipStream_t s);
 
 // (tile, K-split) of this workgroup.  Workgroups are dealt round-robin over the 8 XCDs in
 // linear-id order (x fastest), so the XCD-aware remap runs over the whole (split, tile) grid: the

@@ -110,9 +110,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(F8Params fp) {
     int wg, split;
     split_remap(p.tiles, wg, split);
     const int tm0 = (wg / ntn) * BM, tn0 = (wg % ntn) * BN;
-    const int nk = p.K / KB;
-    const uint8_t* A = (const uint8_t*)p.A;
-    const uint8_t* B = (const uint8_t*)p.B;
+    // K-split `split` (EPI_F32_SLAB) covers k [kbeg, kend); kchunk % KB == 0
+    const int kbeg = split * p.kchunk;
+    const int nk = (min(p.K, kbeg + p.kchunk) - kbeg) / KB;
+    const int ks0 = kbeg / KB;  // first scale k-step of the split
+    const uint8_t* A = (const uint8_t*)p.A + kbeg;
+    const uint8_t* B = (const uint8_t*)p.B + kbeg;
 
     v16f acc[4][2];
 #pragma unroll
@@ -124,7 +127,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(F8Params fp) {
     auto issue_a = [&](int st) {  // A image pieces + this wave's scale piece of step st
         if (st < nk) {
             stage(A, p.lda, tm0, p.M, st * KB, slot_of(st), wave, lane);
-            stage_scales(fp.sa, fp.sb, tm0 / 32, tn0 / 32, st, fp.rga_tot, fp.rgb_tot,
+            stage_scales(fp.sa, fp.sb, tm0 / 32, tn0 / 32, ks0 + st, fp.rga_tot, fp.rgb_tot,
                          slot_of(st) + 2 * IMG_BYTES, wave, lane);
         }
     };
@@ -296,6 +299,60 @@ __global__ __launch_bounds__(256) void quantize_mx_rows_k(uint8_t* __restrict__ 
     t1 = __builtin_amdgcn_cvt_pk_fp8_f32(v[6] * inv, v[7] * inv, t1, true);
     *reinterpret_cast<uint2*>(q + (long long)row * ldq + col) = make_uint2((uint32_t)t0, (uint32_t)t1);
 }
+
+// Column-wise MX quantization for the weight gradients (dW = dout^T . inp reduces over the token
+// axis, so both operands need MX blocks of 32 consecutive TOKENS): x [R tokens][C] bf16 (row
+// stride ldx) -> q [C][Kp] e4m3 (row c = column c of x, Kp = R rounded up to 64; tokens R..Kp-1
+// are zeros) + lane-native scales for C rows and K = Kp.  Equal, byte for byte, to
+// quantize_mx_bf16 of the zero-padded transpose.  A workgroup takes 128 tokens x 64 columns: the
+// tile is read with 16-B row loads into LDS (one 128-B line per token row), then lane c of wave w
+// gathers column c over tokens 32w..32w+31 (a wave reads one 128-B LDS row per step: no bank
+// conflicts), computes the block's scale and writes the 32 bytes of its block (the 4 waves fill
+// one 128-B line of output row c).  Workgroups past column C write the padding rows' zero scales.
+__global__ __launch_bounds__(256) void quantize_mx_cols_k(uint8_t* __restrict__ q, uint8_t* __restrict__ sl,
+                                                          const uint16_t* __restrict__ x, int R, int C,
+                                                          long long ldx, int Kp, int rg_tot) {
+    __shared__ __attribute__((aligned(16))) uint16_t tile[128 * 64];
+    const int tok0 = blockIdx.x * 128, col0 = blockIdx.y * 64;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int c = col0 + lane, tb = tok0 + 32 * wave;  // this lane's output row and token block
+    if (col0 >= C) {  // padding rows of the scale layout (C .. Rpad-1): scale 0, no data
+        if (tb < Kp) {
+            const int kb = tb >> 5;
+            sl[((long long)(kb >> 1) * rg_tot + (c >> 5)) * 64 + (kb & 1) * 32 + (c & 31)] = 0;
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int idx = i * 256 + tid, row = idx >> 3, ch = idx & 7;
+        u32x4 v = u32x4{0u, 0u, 0u, 0u};
+        if (tok0 + row < R) v = *reinterpret_cast<const u32x4*>(x + (long long)(tok0 + row) * ldx + col0 + ch * 8);
+        *reinterpret_cast<u32x4*>(tile + row * 64 + ch * 8) = v;
+    }
+    __syncthreads();
+    if (tb >= Kp) return;
+    float v[32];
+    float amax = 0.f;
+#pragma unroll
+    for (int i = 0; i < 32; i++) {
+        v[i] = __uint_as_float((uint32_t)tile[(32 * wave + i) * 64 + lane] << 16);
+        amax = fmaxf(amax, fabsf(v[i]));
+    }
+    const int sb = mx_scale_byte(amax), kb = tb >> 5;
+    sl[((long long)(kb >> 1) * rg_tot + (c >> 5)) * 64 + (kb & 1) * 32 + (c & 31)] = (uint8_t)sb;
+    const float inv = __uint_as_float((uint32_t)(254 - sb) << 23);  // 2^(127 - sb), exact
+    uint32_t w[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        int t = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * j] * inv, v[4 * j + 1] * inv, 0, false);
+        t = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * j + 2] * inv, v[4 * j + 3] * inv, t, true);
+        w[j] = (uint32_t)t;
+    }
+    uint8_t* dst = q + (long long)c * Kp + tb;
+    *reinterpret_cast<u32x4*>(dst) = u32x4{w[0], w[1], w[2], w[3]};
+    *reinterpret_cast<u32x4*>(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
+}
 }  // namespace f8
 
 long long mx_rows_padded(long long rows) { return (rows + 255) / 256 * 256; }
@@ -305,7 +362,7 @@ bool gemm_fp8_supported(const GemmArgs& a) {
     auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
     return a.a_kcontig && a.b_kcontig && a.K % 64 == 0 && a.lda % 16 == 0 && a.ldb % 16 == 0 &&
            a.N % 4 == 0 && a.ldc % 4 == 0 && al16(a.A) && al16(a.B) && a.a_scale && a.b_scale &&
-           a.epi != EPI_F32_ATOMIC && a.epi != EPI_F32_SLAB &&
+           a.epi != EPI_F32_SLAB && (a.epi != EPI_F32_ATOMIC || a.N % 4 == 0) &&
            // fused MX output: whole 32-column blocks, GELU/GELU'/product epilogues only (4 lanes per block)
            (!a.mx_q || (a.mx_s && a.N % 32 == 0 && epi_mx(a.epi)));
 }
@@ -317,22 +374,40 @@ void gemm_fp8(const GemmArgs& a, hipStream_t s) {
                   a.K, a.lda, a.ldb, a.epi);
         return;
     }
+    const int tiles = cdiv(a.M, f8::BM) * cdiv(a.N, f8::BN);
+    // EPI_F32_ATOMIC (the weight gradients, K = the token count): K-split partials into fp32 slabs
+    // + one fixed-order reduce (no atomics; deterministic), a single split accumulates in place
+    int split = 1;
+    GemmArgs b = a;
+    float* slab = nullptr;
+    if (a.epi == EPI_F32_ATOMIC) {
+        split = a.splitk > 0 ? a.splitk : choose_split_waves(tiles, a.K / f8::KB);
+        if (split < 1) split = 1;
+        const int kchunk = cdiv(cdiv(a.K, split), f8::KB) * f8::KB;
+        split = cdiv(a.K, kchunk);
+        if (split > 1) {
+            if (!(slab = slab_buffer(a, split))) return;
+            b.epi = EPI_F32_SLAB; b.C = slab; b.ldc = a.N;
+        } else {
+            b.epi = EPI_F32_ACC;
+        }
+    }
     f8::F8Params fp;
-    fp.p = make_gemm_params(a, a.K);
+    fp.p = make_gemm_params(b, cdiv(cdiv(a.K, split), f8::KB) * f8::KB);
     float* cs_rows = colsum_rows_begin(a);
     if ((a.colsum_out || a.colsum_part) && !cs_rows) return;
     fp.p.colsum_out = cs_rows;
-    const int tiles = cdiv(a.M, f8::BM) * cdiv(a.N, f8::BN);
     fp.p.tiles = tiles;
     fp.sa = (const uint8_t*)a.a_scale;
     fp.sb = (const uint8_t*)a.b_scale;
     fp.rga_tot = (int)(mx_rows_padded(a.M) / 32);
     fp.rgb_tot = (int)(mx_rows_padded(a.N) / 32);
-    switch (a.epi) {
+    switch (b.epi) {
 #define VIT_CASE(E) \
-    case E: f8::gemm_kernel<E><<<tiles, f8::NT, 0, s>>>(fp); break;
+    case E: f8::gemm_kernel<E><<<dim3(tiles, split), f8::NT, 0, s>>>(fp); break;
         VIT_CASE(EPI_F32_STORE)
         VIT_CASE(EPI_F32_ACC)
+        VIT_CASE(EPI_F32_SLAB)
         VIT_CASE(EPI_BF16_STORE)
         VIT_CASE(EPI_BF16_GELU)
         VIT_CASE(EPI_F32_RESID)
@@ -343,7 +418,8 @@ void gemm_fp8(const GemmArgs& a, hipStream_t s) {
         default: set_error("gemm_fp8: unsupported epilogue %d", a.epi); return;
     }
     after_launch("gemm_fp8");
-    count_hit(VIT_HIT_GEMM_FP8 + a.epi);
+    count_hit(VIT_HIT_GEMM_FP8 + b.epi);
+    if (slab) slab_reduce(a, slab, split, s);
     colsum_rows_end(a, cs_rows, s);
 }
 
@@ -370,6 +446,19 @@ void quantize_mx_f32(uint8_t* q, uint8_t* sl, const float* x, long long R, int K
                      long long ldq, hipStream_t s) {
     quantize_mx<float>(q, sl, x, R, K, ldx, ldq, 1, 0, 0, 0, s);
 }
+long long mx_cols_kp(long long R) { return (R + 63) / 64 * 64; }
+void quantize_mx_cols_bf16(uint8_t* q, uint8_t* sl, const bf16_t* x, long long R, int C, long long ldx, hipStream_t s) {
+    if (R <= 0 || C <= 0) return;
+    if (C % 64 || ldx % 8 || ((uintptr_t)x & 15) || ((uintptr_t)q & 15) || R >= (1LL << 30)) {
+        set_error("quantize_mx_cols: C %% 64 == 0 and 16-B aligned rows required (C=%d)", C);
+        return;
+    }
+    const int kp = (int)mx_cols_kp(R);
+    const int cpad = (int)mx_rows_padded(C);
+    f8::quantize_mx_cols_k<<<dim3(cdiv(kp, 128), cpad / 64), 256, 0, s>>>(q, sl, (const uint16_t*)x, (int)R, C, ldx, kp,
+                                                                         cpad / 32);
+    after_launch("quantize_mx_cols");
+}
 void quantize_mx_batched_bf16(uint8_t* q, uint8_t* sl, const bf16_t* x, long long R, int K, int count,
                               long long xs, long long qs, long long ss, hipStream_t s) {
     quantize_mx<bf16_t>(q, sl, x, R, K, K, K, count, xs, qs, ss, s);
@@ -392,6 +481,10 @@ void quantize_mx_bf16_ex(uint8_t* q, uint8_t* scales, const uint16_t* x, long lo
 void quantize_mx_f32_ex(uint8_t* q, uint8_t* scales, const float* x, long long R, int K, long long ldx,
                         long long ldq) {
     quantize_mx_f32(q, scales, x, R, K, ldx, ldq, stream());
+}
+long long mx_cols_padded(long long R) { return mx_cols_kp(R); }
+void quantize_mx_cols_bf16_ex(uint8_t* q, uint8_t* scales, const uint16_t* x, long long R, int C, long long ldx) {
+    quantize_mx_cols_bf16(q, scales, (const bf16_t*)x, R, C, ldx, stream());
 }
 void gemm_fp8_fused_mx(void* C, void* C2, long long ldc, const void* aux, long long ldaux, const uint8_t* A,
                        const uint8_t* a_scale, long long lda, const uint8_t* B, const uint8_t* b_scale,

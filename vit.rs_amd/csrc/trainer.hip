@@ -355,6 +355,11 @@ struct Trainer {
     uint8_t* act_q2[4]{};
     uint8_t* act_s2[4]{};
     bool fuse_mx = true;
+    // fp8 weight gradients (VIT_FP8_WGRAD=0: bf16 as before): dout and inp quantized column-wise
+    // (MX blocks of 32 consecutive tokens: the axis the weight gradient reduces over) into [OC][Kp] /
+    // [Cin][Kp] e4m3 rows on the weight-gradient stream, then the MXFP8 engine with K-split slabs
+    bool fp8_wgrad = true;
+    QMat wg_a, wg_b;  // column-quantized dout / inp of the running weight gradient (stream-ordered)
     int wslot(int k, int l) const {    // memory-order index of layer l's copy of weight kind k
         const long long stride = L > 1 ? off[wkinds[k] * L + 1] - off[wkinds[k] * L] : 0;
         return stride < 0 ? L - 1 - l : l;
@@ -629,6 +634,15 @@ struct Trainer {
                 }
                 const char* fe = getenv("VIT_FP8_FUSE");
                 fuse_mx = !(fe && fe[0] == '0');
+                const char* fw = getenv("VIT_FP8_WGRAD");
+                fp8_wgrad = !(fw && fw[0] == '0') && C % 64 == 0;
+                if (fp8_wgrad) {
+                    const long long kp = mx_cols_kp(BT);
+                    wg_a.q = alloc<uint8_t>(4LL * C * kp);
+                    wg_a.s = alloc<uint8_t>((long long)mx_scale_bytes(4LL * C, (int)kp));
+                    wg_b.q = alloc<uint8_t>(4LL * C * kp);
+                    wg_b.s = alloc<uint8_t>((long long)mx_scale_bytes(4LL * C, (int)kp));
+                }
             }
         } else {
             patches_f = alloc<float>((long long)B * NP * KP);
@@ -916,9 +930,23 @@ struct Trainer {
                 VIT_HIP(hipStreamWaitEvent(s2, mev[mb][ready], 0));
             }
         }
-        tbeg(cls, 2.0 * w.M * (double)w.N * w.K, st);
-        gemm_bf16(w, st);
-        tend();
+        if (fp8() && fp8_wgrad) {
+            const long long kp = mx_cols_kp(BT);
+            tbeg(TC_QUANT, 0, st);
+            quantize_mx_cols_bf16(wg_a.q, wg_a.s, dout, BT, OC, OC, st);
+            quantize_mx_cols_bf16(wg_b.q, wg_b.s, inp, BT, Cin, Cin, st);
+            tend();
+            w.A = wg_a.q; w.lda = kp; w.a_kcontig = true; w.a_scale = wg_a.s;
+            w.B = wg_b.q; w.ldb = kp; w.b_kcontig = true; w.b_scale = wg_b.s;
+            w.K = (int)kp;
+            tbeg(cls, 2.0 * w.M * (double)w.N * BT, st);
+            gemm_fp8(w, st);
+            tend();
+        } else {
+            tbeg(cls, 2.0 * w.M * (double)w.N * w.K, st);
+            gemm_bf16(w, st);
+            tend();
+        }
         if (two_streams) VIT_HIP(hipEventRecord(bev[done], s2));
     }
     // a micro-batch stream may overwrite a buffer once the wgrad that reads it (`done`) finished
