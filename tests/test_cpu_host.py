@@ -18,7 +18,7 @@ import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("vit_ops.h", "vit_trainer.h", "vit_checkpoint.h", "vit_data.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("vit_ops.h", "vit_trainer.h", "vit_checkpoint.h", "vit_data.h", "vit_jpeg.h")]
 
 
 def declared_functions():
@@ -62,7 +62,7 @@ def test_library_exports_every_declared_symbol(vit):
 def test_headers_compile_as_c(tmp_path):
     src = tmp_path / "h.c"
     src.write_text('#include "vit_ops.h"\n#include "vit_trainer.h"\n#include "vit_checkpoint.h"\n'
-                   '#include "vit_data.h"\nint main(void){return 0;}\n')
+                   '#include "vit_data.h"\n#include "vit_jpeg.h"\nint main(void){return 0;}\n')
     subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-pedantic", "-I", os.path.join(ROOT, "include"),
                     "-c", str(src), "-o", str(tmp_path / "h.o")], check=True)
 

@@ -61,7 +61,7 @@ def build(quiet=True):
 _VOID = [("vit_clear_error", []), ("vit_set_stream", [ctypes.c_void_p]),
          ("vit_free", [ctypes.c_void_p]), ("vit_event_destroy", [ctypes.c_void_p]),
          ("vit_trainer_destroy", [ctypes.c_void_p]), ("vit_trainer_timing_reset", [ctypes.c_void_p]),
-         ("vit_loader_close", [ctypes.c_void_p]), ("vit_kernel_hits_reset", [])]
+         ("vit_loader_close", [ctypes.c_void_p]), ("vit_jpeg_loader_close", [ctypes.c_void_p]), ("vit_kernel_hits_reset", [])]
 
 # name -> (restype, argtypes)
 P, I, LL, F, S = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_size_t
@@ -145,6 +145,16 @@ _SIGS = {
     "vit_loader_num_records": (LL, [P]), "vit_loader_steps_per_epoch": (I, [P]),
     "vit_loader_next": (I, [P, ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(LL), ctypes.POINTER(I)]),
     "vit_trainer_set_batch_u8": (I, [P, P, P, P, P]),
+    # JPEG input pipeline (include/vit_jpeg.h)
+    "vit_jpeg_probe": (I, [P, LL, ctypes.POINTER(I), ctypes.POINTER(I), ctypes.POINTER(I)]),
+    "vit_jpeg_coefficients": (I, [P, LL, P, LL, P]),
+    "vit_jpeg_loader_open": (P, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, I, ctypes.c_ulonglong, I, I,
+                                 I, I, I, I]),
+    "vit_jpeg_loader_num_records": (LL, [P]), "vit_jpeg_loader_steps_per_epoch": (I, [P]),
+    "vit_jpeg_loader_next": (I, [P, ctypes.POINTER(P), ctypes.POINTER(LL), ctypes.POINTER(I)]),
+    "vit_jpeg_loader_boxes": (I, [P, P]),
+    "vit_jpeg_loader_decode_u8": (I, [P, P, I]),
+    "vit_trainer_set_batch_jpeg": (I, [P, P, P, P]),
     "vit_trainer_save_checkpoint": (I, [P, ctypes.c_char_p]),
     "vit_trainer_load_checkpoint": (I, [P, ctypes.c_char_p]),
 }
@@ -378,6 +388,95 @@ class Loader:
 
 
 # --------------------------------------------------------------------------- model
+def jpeg_probe(data):
+    """(width, height, kind) of a JPEG byte string (kind 0 gray, 1 4:4:4, 2 4:2:2, 3 4:2:0); host-only."""
+    buf = np.frombuffer(data, np.uint8)
+    w, h, k = I(), I(), I()
+    if lib().vit_jpeg_probe(buf.ctypes.data_as(P), buf.size, ctypes.byref(w), ctypes.byref(h), ctypes.byref(k)):
+        check("jpeg_probe")
+    return w.value, h.value, k.value
+
+
+def jpeg_coefficients(data):
+    """(coef int16 [blocks][64] natural order, info int32 [208]) of a JPEG byte string; host-only
+    (the entropy-decoder half of the pipeline, for tests)."""
+    buf = np.frombuffer(data, np.uint8)
+    info = np.zeros(208, np.int32)
+    if lib().vit_jpeg_coefficients(buf.ctypes.data_as(P), buf.size, None, 0, info.ctypes.data_as(P)):
+        check("jpeg_coefficients")
+    nc = int(info[3])
+    nblk = sum(int(info[4 + 4 * c]) * int(info[5 + 4 * c]) for c in range(nc))
+    coef = np.zeros((nblk, 64), np.int16)
+    if lib().vit_jpeg_coefficients(buf.ctypes.data_as(P), buf.size, coef.ctypes.data_as(P), nblk, None):
+        check("jpeg_coefficients")
+    return coef, info
+
+
+def write_jpeg_records(prefix, jpegs, labels):
+    """Pack JPEG byte strings into the loader's record files: prefix.jpg (concatenated),
+    prefix.idx (N+1 int64 offsets), prefix.lab (N int32).  Returns the three paths."""
+    offs = np.zeros(len(jpegs) + 1, np.int64)
+    offs[1:] = np.cumsum([len(j) for j in jpegs])
+    with open(prefix + ".jpg", "wb") as f:
+        for j in jpegs:
+            f.write(j)
+    offs.tofile(prefix + ".idx")
+    np.asarray(labels, np.int32).tofile(prefix + ".lab")
+    return prefix + ".jpg", prefix + ".idx", prefix + ".lab"
+
+
+class JpegLoader:
+    """Packed-JPEG record loader (include/vit_jpeg.h): host threads entropy-decode batches ahead;
+    the GPU half (IDCT, chroma, colour, crop/flip/resize) runs in decode_u8() or feeds a trainer
+    through ViT.set_batch_jpeg()."""
+
+    def __init__(self, jpeg_path, index_path, labels_path, batch, seed=1337, rank=0, world=1,
+                 shuffle=True, augment=False, depth=3, threads=4):
+        self.B = batch
+        self.h = lib().vit_jpeg_loader_open(os.fsencode(jpeg_path), os.fsencode(index_path),
+                                            os.fsencode(labels_path), batch, seed, rank, world, int(shuffle),
+                                            int(augment), depth, threads)
+        if not self.h:
+            check("vit_jpeg_loader_open")
+            raise VitError("vit_jpeg_loader_open failed")
+        self.num_records = int(lib().vit_jpeg_loader_num_records(self.h))
+        self.steps_per_epoch = int(lib().vit_jpeg_loader_steps_per_epoch(self.h))
+
+    def next(self):
+        """Advance to the next batch: (labels int32 [B] copy, epoch, step)."""
+        lp, ep, st = P(), LL(), I()
+        if lib().vit_jpeg_loader_next(self.h, ctypes.byref(lp), ctypes.byref(ep), ctypes.byref(st)):
+            check("vit_jpeg_loader_next")
+        lab = np.ctypeslib.as_array((ctypes.c_int * self.B).from_address(lp.value)).copy()
+        return lab, ep.value, st.value
+
+    def boxes(self):
+        """The current batch's crop boxes [B][5] = x0, y0, w, h, flip."""
+        out = np.zeros((self.B, 5), np.int32)
+        if lib().vit_jpeg_loader_boxes(self.h, out.ctypes.data_as(P)):
+            check("vit_jpeg_loader_boxes")
+        return out
+
+    def decode_u8(self, img, out=None):
+        """GPU half of the current batch -> DeviceArray uint8 [B, img, img, 3]."""
+        if out is None:
+            out = DeviceArray((self.B, img, img, 3), np.uint8)
+        if lib().vit_jpeg_loader_decode_u8(self.h, out.ptr, img):
+            check("vit_jpeg_loader_decode_u8")
+        return out
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().vit_jpeg_loader_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class ViT:
     """Mirror of the reference's `struct ViT` (train_vit.rs:65-86) over the native trainer.
 
@@ -451,6 +550,14 @@ class ViT:
         self._ok(lib().vit_trainer_set_batch(self.h, px.ctypes.data_as(P),
                                              lb.ctypes.data_as(P) if lb is not None else None),
                  "set_batch")
+
+    def set_batch_jpeg(self, loader, mean=IMAGENET_MEAN, std=IMAGENET_STD):
+        """The JpegLoader's current batch -> normalised device pixels + labels
+        (vit_trainer_set_batch_jpeg)."""
+        m = np.asarray(mean, np.float32)
+        sd = np.asarray(std, np.float32)
+        self._ok(lib().vit_trainer_set_batch_jpeg(self.h, loader.h, m.ctypes.data_as(P), sd.ctypes.data_as(P)),
+                 "set_batch_jpeg")
 
     def set_batch_u8(self, images, labels=None, mean=IMAGENET_MEAN, std=IMAGENET_STD):
         """uint8 [B, img, img, 3] (numpy array, or a host pointer from Loader.next_raw) ->

@@ -21,8 +21,11 @@
 #include "../../include/vit_trainer.h"
 #include "../../include/vit_checkpoint.h"
 #include "../../include/vit_data.h"
+#include "../../include/vit_jpeg.h"
 
 namespace vit {
+// jpeg.hip: the JPEG loader's current batch -> device uint8 [B][img][img][3] on st
+bool jpeg_loader_decode_to(vit_jpeg_loader_t* l, uint8_t* out, int img, hipStream_t st, const int** labels);
 namespace {
 
 enum TIdx {
@@ -1223,6 +1226,15 @@ struct Trainer {
 
     // upload one uint8 batch (host) and normalise it into `pixels` (include/vit_data.h)
     bool set_batch_u8(const unsigned char* img, const int* lab, const float* mean, const float* sd) {
+        return stage_batch(img, nullptr, lab, mean, sd);
+    }
+    // the JPEG loader's current batch (include/vit_jpeg.h): decoded on the copy stream into the
+    // same uint8 staging, then the same normalise
+    bool set_batch_jpeg(vit_jpeg_loader_t* jl, const float* mean, const float* sd) {
+        return stage_batch(nullptr, jl, nullptr, mean, sd);
+    }
+    bool stage_batch(const unsigned char* img, vit_jpeg_loader_t* jl, const int* lab, const float* mean,
+                     const float* sd) {
         const int HW = cfg.img * cfg.img;
         const size_t bytes = (size_t)B * HW * 3;
         if (!s_copy) {
@@ -1240,7 +1252,11 @@ struct Trainer {
         u8_k++;
         // the staging slot is free once the normalise of two uploads ago has run
         VIT_HIP(hipStreamWaitEvent(s_copy, u8_used[k], 0));
-        VIT_HIP(hipMemcpyAsync(u8_stage[k], img, bytes, hipMemcpyHostToDevice, s_copy));
+        if (jl) {  // host entropy decode already done by the loader; the pixel work runs here
+            if (!jpeg_loader_decode_to(jl, u8_stage[k], cfg.img, s_copy, &lab)) return false;
+        } else {
+            VIT_HIP(hipMemcpyAsync(u8_stage[k], img, bytes, hipMemcpyHostToDevice, s_copy));
+        }
         if (lab) VIT_HIP(hipMemcpyAsync(lab_stage[k], lab, (size_t)B * 4, hipMemcpyHostToDevice, s_copy));
         VIT_HIP(hipEventRecord(u8_copied[k], s_copy));
         VIT_HIP(hipStreamWaitEvent(s, u8_copied[k], 0));
@@ -1431,6 +1447,13 @@ int vit_trainer_train_step(vit_trainer_t* h, float lr, int b_global) {
     vit_trainer_backward(h);
     vit_trainer_step(h, lr);
     return vit::has_error();
+}
+int vit_trainer_set_batch_jpeg(vit_trainer_t* h, vit_jpeg_loader_t* l, const float* mean3, const float* std3) {
+    if (!h || !l || !mean3 || !std3) {
+        set_error("vit_trainer_set_batch_jpeg: null argument");
+        return 1;
+    }
+    return h->t.set_batch_jpeg(l, mean3, std3) ? 0 : 1;
 }
 int vit_trainer_set_batch_u8(vit_trainer_t* h, const unsigned char* images, const int* labels,
                              const float* mean3, const float* std3) {
