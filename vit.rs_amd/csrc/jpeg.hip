@@ -4,7 +4,8 @@
 //
 // Host (jpeg_host.cpp, `threads` worker threads): markers + Huffman -> sparse quantised blocks.
 // Device, two kernels per batch on one stream:
-//   idct_k          one thread per 8x8 block: scatter the non-zero coefficients (x quantiser) into
+//   idct_k          one thread per 8x8 block: scatter the non-zero coefficients (zig-zag -> natural,
+//                   x quantiser) into
 //                   a column-interleaved LDS image, jpeg_idct_islow's two 1-D passes in int32,
 //                   8 x 8 B row stores into the component plane (uint8, stride bw*8)
 //   color_resize_k  one thread per output pixel of [n][img][img][3] uint8: the 2x2 source pixels
@@ -103,6 +104,13 @@ __device__ __forceinline__ uint32_t range_limit(int x) {
     return v < 128 ? (uint32_t)(v + 128) : v < 512 ? 255u : v < 896 ? 0u : (uint32_t)(v - 896);
 }
 
+// zig-zag position -> natural index (the host emits each block's non-zero coefficients in zig-zag
+// order, as the entropy decoder produces them)
+__constant__ uint8_t kZigD[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                                  12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                                  35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                                  58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
 constexpr int IDCT_T = 64;  // threads (= blocks) per workgroup
 __global__ __launch_bounds__(IDCT_T) void idct_k(uint8_t* __restrict__ planes, const ImgDesc* __restrict__ desc,
                                                  const uint64_t* __restrict__ masks,
@@ -123,7 +131,7 @@ __global__ __launch_bounds__(IDCT_T) void idct_k(uint8_t* __restrict__ planes, c
     const int16_t* v = vals + voff[gb];
     const uint16_t* q = d.qt[c];
     while (m) {
-        const int k = __builtin_ctzll(m);
+        const int k = kZigD[__builtin_ctzll(m)];
         img[k * IDCT_T + t] = (int)*v++ * (int)q[k];
         m &= m - 1;
     }
@@ -232,9 +240,7 @@ __global__ __launch_bounds__(256) void color_resize_k(uint8_t* __restrict__ out,
 // ------------------------------------------------------------------------------ host batch
 struct ImgOut {  // one image's host decode
     Frame f;
-    std::vector<uint64_t> masks;
-    std::vector<int16_t> vals;
-    long long nvals = 0;
+    Sparse sp;
     std::string err;
     bool ok = false;
 };
@@ -256,6 +262,7 @@ struct HostBatch {
     int max_blk = 0;
     std::vector<int> labels;
     std::vector<int> boxes;  // [n][5]
+    std::vector<long long> img_bb, img_vb;  // first block / value of each image
     long long epoch = 0;
     int step = 0;
     int state = 0;  // 0 free, 1 ready, 2 handed out
@@ -287,7 +294,8 @@ struct HostBatch {
     ~HostBatch() { release(); }
 };
 
-// assemble decoded images into hb (descriptors, sparse stream) with their crop boxes
+// lay out hb for the decoded images: sizes, descriptors with their crop boxes, each image's
+// first block / value (the sparse stream itself: copy_image)
 static bool assemble(HostBatch& hb, std::vector<ImgOut>& outs, int n, const int* boxes) {
     long long nblk = 0, nval = 0, plane = 0;
     int max_blk = 0;
@@ -298,7 +306,7 @@ static bool assemble(HostBatch& hb, std::vector<ImgOut>& outs, int n, const int*
         }
         const long long b = outs[i].f.blocks();
         nblk += b;
-        nval += outs[i].nvals;
+        nval += outs[i].sp.nvals;
         max_blk = std::max<int>(max_blk, (int)b);
         for (int c = 0; c < outs[i].f.nc; c++) plane += (long long)outs[i].f.bw[c] * outs[i].f.bh[c] * 64;
     }
@@ -328,9 +336,8 @@ static bool assemble(HostBatch& hb, std::vector<ImgOut>& outs, int n, const int*
     hb.plane_bytes = plane;
     hb.max_blk = max_blk;
     ImgDesc* desc = reinterpret_cast<ImgDesc*>(hb.buf + hb.o_desc);
-    uint64_t* masks = reinterpret_cast<uint64_t*>(hb.buf + hb.o_mask);
-    uint32_t* voff = reinterpret_cast<uint32_t*>(hb.buf + hb.o_voff);
-    int16_t* vals = reinterpret_cast<int16_t*>(hb.buf + hb.o_vals);
+    hb.img_bb.resize((size_t)n);
+    hb.img_vb.resize((size_t)n);
     long long bb = 0, vb = 0, pb = 0;
     for (int i = 0; i < n; i++) {
         const Frame& f = outs[i].f;
@@ -349,28 +356,31 @@ static bool assemble(HostBatch& hb, std::vector<ImgOut>& outs, int n, const int*
         }
         for (int k = 0; k < 4; k++) d.box[k] = boxes[5 * i + k];
         d.flip = boxes[5 * i + 4];
-        const long long nb = d.nblk;
-        memcpy(masks + bb, outs[i].masks.data(), 8 * (size_t)nb);
-        memcpy(vals + vb, outs[i].vals.data(), 2 * (size_t)outs[i].nvals);
-        long long v = vb;
-        for (long long k = 0; k < nb; k++) {
-            voff[bb + k] = (uint32_t)v;
-            v += __builtin_popcountll(outs[i].masks[(size_t)k]);
-        }
-        bb += nb;
-        vb += outs[i].nvals;
+        hb.img_bb[(size_t)i] = bb;
+        hb.img_vb[(size_t)i] = vb;
+        bb += d.nblk;
+        vb += outs[i].sp.nvals;
     }
     return true;
 }
+// the sparse stream of image i into its place (after assemble; independent per image: run on the
+// worker pool)
+static void copy_image(HostBatch& hb, const std::vector<ImgOut>& outs, int i) {
+    uint64_t* masks = reinterpret_cast<uint64_t*>(hb.buf + hb.o_mask);
+    uint32_t* voff = reinterpret_cast<uint32_t*>(hb.buf + hb.o_voff);
+    int16_t* vals = reinterpret_cast<int16_t*>(hb.buf + hb.o_vals);
+    const long long bb = hb.img_bb[(size_t)i], vb = hb.img_vb[(size_t)i];
+    const Sparse& sp = outs[(size_t)i].sp;
+    const long long nb = outs[(size_t)i].f.blocks();
+    memcpy(masks + bb, sp.masks.data(), 8 * (size_t)nb);
+    memcpy(vals + vb, sp.vals.data(), 2 * (size_t)sp.nvals);
+    for (long long k = 0; k < nb; k++) voff[bb + k] = (uint32_t)(vb + sp.voff[(size_t)k]);
+}
 
 // decode one JPEG into out (host)
-static void decode_one(const uint8_t* data, size_t size, ImgOut& out, std::vector<int16_t>& scratch) {
-    out.ok = decode_coefficients(data, size, out.f, scratch, out.err);
-    if (!out.ok) return;
-    const long long nb = out.f.blocks();
-    out.masks.resize((size_t)nb);
-    out.vals.resize((size_t)nb * 64);
-    pack_sparse(scratch.data(), nb, out.masks.data(), out.vals.data(), out.nvals);
+static void decode_one(const uint8_t* data, size_t size, ImgOut& out) {
+    out.err.clear();
+    out.ok = decode_sparse(data, size, out.f, out.sp, out.err);
 }
 
 // crop policy: 0 = the largest centred square; 1 = random-resized crop (area 8-100 %, aspect
@@ -524,6 +534,8 @@ struct vit_jpeg_loader {
     std::atomic<bool> quit{false};
     int job_left = 0;
     const long long* job_recs = nullptr;
+    HostBatch* job_hb = nullptr;
+    bool job_copy = false;
     std::vector<ImgOut> outs;
     DeviceSide dev;
 
@@ -540,7 +552,6 @@ struct vit_jpeg_loader {
         perm_epoch = epoch;
     }
     void worker() {
-        std::vector<int16_t> scratch;
         long long seen = 0;
         for (;;) {
             {
@@ -551,13 +562,15 @@ struct vit_jpeg_loader {
             }
             int done_here = 0;
             for (int i; (i = job_next.fetch_add(1)) < B;) {  // every index is counted, even on stop
-                if (!quit.load(std::memory_order_relaxed)) {
-                    const long long r = job_recs[i];
-                    const uint8_t* base = (const uint8_t*)data.p;
-                    decode_one(base + offs[r], (size_t)(offs[r + 1] - offs[r]), outs[(size_t)i], scratch);
-                } else {
+                if (quit.load(std::memory_order_relaxed)) {
                     outs[(size_t)i].ok = false;
                     outs[(size_t)i].err = "loader closed";
+                } else if (job_copy) {
+                    copy_image(*job_hb, outs, i);
+                } else {
+                    const long long r = job_recs[i];
+                    const uint8_t* base = (const uint8_t*)data.p;
+                    decode_one(base + offs[r], (size_t)(offs[r + 1] - offs[r]), outs[(size_t)i]);
                 }
                 done_here++;
             }
@@ -568,10 +581,13 @@ struct vit_jpeg_loader {
             pdone.notify_all();
         }
     }
-    bool decode_batch(const long long* recs) {
+    // one job over the batch's B images on the pool: decode (recs) or copy into hb
+    bool pool_job(const long long* recs, HostBatch* hb) {
         {
             std::lock_guard<std::mutex> lk(pmu);
             job_recs = recs;
+            job_hb = hb;
+            job_copy = hb != nullptr;
             job_next = 0;
             job_left = B;
             job_gen++;
@@ -590,7 +606,7 @@ struct vit_jpeg_loader {
         std::vector<long long> recs((size_t)B);
         for (int b = 0; b < B; b++) recs[(size_t)b] = perm[(size_t)(base + b)];
         hb.err.clear();
-        if (!decode_batch(recs.data())) return;
+        if (!pool_job(recs.data(), nullptr)) return;
         hb.labels.resize((size_t)B);
         hb.boxes.resize((size_t)B * 5);
         const int* lab = (const int*)labels.p;
@@ -601,7 +617,7 @@ struct vit_jpeg_loader {
             if (o.ok)
                 crop_box(o.f.w, o.f.h, augment, seed ^ sm64(0x6a70656755ULL, (uint64_t)(epoch * N + r)), &hb.boxes[(size_t)b * 5]);
         }
-        assemble(hb, outs, B, hb.boxes.data());
+        if (assemble(hb, outs, B, hb.boxes.data())) pool_job(nullptr, &hb);
         hb.epoch = epoch;
         hb.step = step;
     }

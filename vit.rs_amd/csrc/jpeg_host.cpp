@@ -16,7 +16,7 @@ constexpr uint8_t kZig[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18
                               35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
                               58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
-constexpr int FAST = 9;  // look-up bits of the fast Huffman table
+constexpr int FAST = 11;  // look-up bits of the fast Huffman table
 
 struct Huff {
     bool present = false;
@@ -25,6 +25,22 @@ struct Huff {
     int maxcode[18]{};               // largest code of each length (-1: none); [17] sentinel
     int valptr[17]{}, mincode[17]{};
     uint8_t vals[256]{};
+    // AC tables: the whole (run, value) of a short code + its value bits in one look-up:
+    // fast_ac[look] = value << 16 | run << 8 | bits consumed, 0 when the pair does not fit in FAST
+    int32_t fast_ac[1 << FAST]{};
+
+    void build_fast_ac() {
+        for (int look = 0; look < (1 << FAST); look++) {
+            fast_ac[look] = 0;
+            const int l = fast_len[look];
+            if (!l) continue;
+            const int rs = fast_sym[look], r = rs >> 4, sz = rs & 15;
+            if (!sz || l + sz > FAST) continue;
+            int v = (look >> (FAST - l - sz)) & ((1 << sz) - 1);
+            if (v < (1 << (sz - 1))) v -= (1 << sz) - 1;
+            fast_ac[look] = (int32_t)((uint32_t)v << 16) | (r << 8) | (l + sz);
+        }
+    }
 
     bool build(const uint8_t* counts, const uint8_t* symbols, int nsym) {
         int code = 0, k = 0;
@@ -48,6 +64,7 @@ struct Huff {
         maxcode[17] = 0x7fffffff;
         if (k != nsym) return false;
         memcpy(vals, symbols, (size_t)nsym);
+        build_fast_ac();
         present = true;
         return true;
     }
@@ -63,6 +80,20 @@ struct Bits {
     bool at_marker = false;
 
     void fill() {
+        // fast path: 8 bytes without an 0xFF (no stuffing, no marker) append whole
+        if (!at_marker && p + 8 <= end) {
+            uint64_t w;
+            memcpy(&w, p, 8);
+            w = __builtin_bswap64(w);
+            const uint64_t x = ~w;
+            if (!((x - 0x0101010101010101ULL) & ~x & 0x8080808080808080ULL)) {
+                const int nb = (64 - cnt) >> 3;
+                buf |= (w >> (64 - 8 * nb)) << (64 - cnt - 8 * nb);
+                p += nb;
+                cnt += 8 * nb;
+                return;
+            }
+        }
         while (cnt <= 56) {
             uint32_t b = 0;
             if (!at_marker && p < end) {
@@ -224,30 +255,102 @@ struct Parser {
         return true;
     }
 
-    bool block(Bits& b, const Huff& hd, const Huff& ha, int& pred, int16_t* blk) {
-        const int s = b.decode(hd);
-        if (s < 0 || s > 11) return fail("bad DC code");
-        pred += s ? extend(b.get(s), s) : 0;
-        blk[0] = (int16_t)pred;
+    // one block straight into the sparse form: the non-zero coefficients in zig-zag order at out,
+    // their zig-zag positions as the bits of m; returns the count (or -1).  The bit buffer lives
+    // in locals for the block (written back around refills).
+    int block(Bits& bits, const Huff& hd, const Huff& ha, int& pred, int16_t* out, uint64_t& m) {
+        uint64_t buf = bits.buf;
+        int cnt = bits.cnt;
+        auto refill = [&]() {
+            bits.buf = buf;
+            bits.cnt = cnt;
+            bits.fill();
+            buf = bits.buf;
+            cnt = bits.cnt;
+        };
+        auto huff = [&](const Huff& h) -> int {
+            if (cnt < 16) refill();
+            const int look = (int)(buf >> (64 - FAST));
+            if (h.fast_len[look]) {
+                const int l = h.fast_len[look];
+                buf <<= l;
+                cnt -= l;
+                return h.fast_sym[look];
+            }
+            int l = FAST + 1;
+            int code = (int)(buf >> (64 - l));
+            while (l <= 16 && code > h.maxcode[l]) {
+                l++;
+                code = (int)(buf >> (64 - l));
+            }
+            if (l > 16) return -1;
+            buf <<= l;
+            cnt -= l;
+            return h.vals[h.valptr[l] + code - h.mincode[l]];
+        };
+        auto bitsn = [&](int n) -> int {  // 1 <= n <= 16
+            if (cnt < n) refill();
+            const int v = (int)(buf >> (64 - n));
+            buf <<= n;
+            cnt -= n;
+            return v;
+        };
+        const int s = huff(hd);
+        if (s < 0 || s > 11) return fail("bad DC code") ? 0 : -1;
+        pred += s ? extend(bitsn(s), s) : 0;
+        int n = 0;
+        uint64_t mm = 0;
+        if (pred) {
+            mm = 1;
+            out[n++] = (int16_t)pred;
+        }
         for (int k = 1; k < 64;) {
-            const int rs = b.decode(ha);
-            if (rs < 0) return fail("bad AC code");
+            if (cnt < 16) refill();
+            const int32_t fa = ha.fast_ac[buf >> (64 - FAST)];
+            if (fa) {  // run + value in one look-up
+                const int l = fa & 255;
+                k += (fa >> 8) & 255;
+                buf <<= l;
+                cnt -= l;
+                if (k > 63) return fail("AC coefficient index past 63") ? 0 : -1;
+                mm |= 1ULL << k;
+                out[n++] = (int16_t)(fa >> 16);
+                k++;
+                continue;
+            }
+            const int rs = huff(ha);
+            if (rs < 0) return fail("bad AC code") ? 0 : -1;
             const int r = rs >> 4, sz = rs & 15;
             if (sz) {
                 k += r;
-                if (k > 63) return fail("AC coefficient index past 63");
-                blk[kZig[k]] = (int16_t)extend(b.get(sz), sz);
+                if (k > 63) return fail("AC coefficient index past 63") ? 0 : -1;
+                mm |= 1ULL << k;
+                out[n++] = (int16_t)extend(bitsn(sz), sz);
                 k++;
             } else {
                 if (r != 15) break;  // EOB
                 k += 16;
             }
         }
+        bits.buf = buf;
+        bits.cnt = cnt;
+        m = mm;
+        return n;
+    }
+    // block bi (component-major index) of the image into the sink
+    bool emit(Bits& b, const Huff& hd, const Huff& ha, int& pred, long long bi, Sparse& sp) {
+        if (sp.vals.size() < (size_t)sp.nvals + 64) sp.vals.resize(sp.vals.size() * 2 + 64 * 64);
+        uint64_t m;
+        const int cnt = block(b, hd, ha, pred, sp.vals.data() + sp.nvals, m);
+        if (cnt < 0) return false;
+        sp.masks[(size_t)bi] = m;
+        sp.voff[(size_t)bi] = (uint32_t)sp.nvals;
+        sp.nvals += cnt;
         return true;
     }
 
     // one scan; returns the position after its entropy-coded data
-    bool scan(const uint8_t* q, int len, const uint8_t*& pos, std::vector<int16_t>& coef) {
+    bool scan(const uint8_t* q, int len, const uint8_t*& pos, Sparse& sp) {
         if (!have_frame) return fail("SOS before SOF");
         const int ns = q[0];
         if (ns < 1 || ns > f.nc || len < 4 + 2 * ns) return fail("bad SOS");
@@ -265,11 +368,11 @@ struct Parser {
         }
         const int ss = q[1 + 2 * ns], se = q[2 + 2 * ns], ahl = q[3 + 2 * ns];
         if (ss != 0 || se != 63 || ahl != 0) return fail("not a sequential DCT scan");
-        long long base[MAXC];
+        long long base[MAXC];  // first block of each component
         long long o = 0;
         for (int c = 0; c < f.nc; c++) {
             base[c] = o;
-            o += (long long)f.bw[c] * f.bh[c] * 64;
+            o += (long long)f.bw[c] * f.bh[c];
         }
         Bits b{pos, d + n};
         int pred[MAXC] = {0, 0, 0};
@@ -287,8 +390,8 @@ struct Parser {
             for (int by = 0; by < nby; by++)
                 for (int bx = 0; bx < nbx; bx++) {
                     if (restart_interval && mcus_left == 0 && !do_restart()) return false;
-                    int16_t* blk = coef.data() + base[c] + ((long long)by * f.bw[c] + bx) * 64;
-                    if (!block(b, dc[td[0]], ac[ta[0]], pred[0], blk)) return false;
+                    if (!emit(b, dc[td[0]], ac[ta[0]], pred[0], base[c] + (long long)by * f.bw[c] + bx, sp))
+                        return false;
                     mcus_left--;
                 }
         } else {
@@ -300,8 +403,7 @@ struct Parser {
                         for (int v = 0; v < f.vs[c]; v++)
                             for (int h = 0; h < f.hs[c]; h++) {
                                 const long long bi = (long long)(my * f.vs[c] + v) * f.bw[c] + mx * f.hs[c] + h;
-                                if (!block(b, dc[td[i]], ac[ta[i]], pred[i], coef.data() + base[c] + bi * 64))
-                                    return false;
+                                if (!emit(b, dc[td[i]], ac[ta[i]], pred[i], base[c] + bi, sp)) return false;
                             }
                     }
                     mcus_left--;
@@ -314,7 +416,7 @@ struct Parser {
         return true;
     }
 
-    bool run(std::vector<int16_t>* coef) {
+    bool run(Sparse* sp) {
         if (n < 4 || d[0] != 0xFF || d[1] != 0xD8) return fail("not a JPEG file (no SOI)");
         const uint8_t* p = d + 2;
         const uint8_t* end = d + n;
@@ -338,7 +440,7 @@ struct Parser {
             switch (m) {
                 case 0xC0: case 0xC1:
                     if (!frame(q, len)) return false;
-                    if (!coef) return true;  // headers only
+                    if (!sp) return true;  // headers only
                     break;
                 case 0xC2: case 0xC6: case 0xCA: case 0xCE: return fail("progressive JPEG is not supported");
                 case 0xC3: case 0xC5: case 0xC7: case 0xCB: case 0xCD: case 0xCF:
@@ -352,17 +454,21 @@ struct Parser {
                     break;
                 case 0xDA: {
                     if (!have_frame) return fail("SOS before SOF");
-                    if (!coef) return true;
+                    if (!sp) return true;
                     if (!scanned) {
                         for (int c = 0; c < f.nc; c++) {
                             if (!qt_present[f.tq[c]]) return fail("missing quantisation table");
                             memcpy(f.qt[c], qt[f.tq[c]], sizeof(f.qt[c]));
                         }
-                        coef->assign((size_t)f.blocks() * 64, 0);
+                        // blocks no scan codes (padding of non-interleaved scans) stay all-zero
+                        sp->masks.assign((size_t)f.blocks(), 0);
+                        sp->voff.assign((size_t)f.blocks(), 0);
+                        if (sp->vals.size() < (size_t)f.blocks() * 8) sp->vals.resize((size_t)f.blocks() * 8);
+                        sp->nvals = 0;
                         scanned = true;
                     }
                     const uint8_t* pos = q + len;
-                    if (!scan(q, len, pos, *coef)) return false;
+                    if (!scan(q, len, pos, *sp)) return false;
                     p = pos;
                     continue;
                 }
@@ -371,7 +477,7 @@ struct Parser {
             p = q + len;
         }
         if (!have_frame) return fail("no SOF marker");
-        if (coef && !scanned) return fail("no scan");
+        if (sp && !scanned) return fail("no scan");
         return true;
     }
 };
@@ -383,25 +489,26 @@ bool parse_header(const uint8_t* data, size_t n, Frame& f, std::string& err) {
     return ps.run(nullptr);
 }
 
-bool decode_coefficients(const uint8_t* data, size_t n, Frame& f, std::vector<int16_t>& coef, std::string& err) {
+bool decode_sparse(const uint8_t* data, size_t n, Frame& f, Sparse& sp, std::string& err) {
     Parser ps{data, n, f, err};
-    return ps.run(&coef);
+    return ps.run(&sp);
 }
 
-void pack_sparse(const int16_t* coef, long long nblocks, uint64_t* masks, int16_t* vals, long long& nvals) {
-    long long o = 0;
-    for (long long b = 0; b < nblocks; b++) {
-        const int16_t* blk = coef + b * 64;
-        uint64_t m = 0;
-        for (int k = 0; k < 64; k++) {
-            if (blk[k]) {
-                m |= 1ULL << k;
-                vals[o++] = blk[k];
-            }
+bool decode_coefficients(const uint8_t* data, size_t n, Frame& f, std::vector<int16_t>& coef, std::string& err) {
+    Sparse sp;
+    if (!decode_sparse(data, n, f, sp, err)) return false;
+    const long long nb = f.blocks();
+    coef.assign((size_t)nb * 64, 0);
+    for (long long b = 0; b < nb; b++) {
+        uint64_t m = sp.masks[(size_t)b];
+        const int16_t* v = sp.vals.data() + sp.voff[(size_t)b];
+        while (m) {
+            const int k = __builtin_ctzll(m);
+            coef[(size_t)b * 64 + kZig[k]] = *v++;
+            m &= m - 1;
         }
-        masks[b] = m;
     }
-    nvals = o;
+    return true;
 }
 
 }  // namespace jpg

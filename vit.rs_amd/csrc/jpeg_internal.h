@@ -7,7 +7,7 @@
 // serial bit-level work and runs on host threads; everything per pixel — dequantisation, the
 // 8x8 inverse DCT, chroma upsampling, YCbCr -> RGB, crop / resize / flip, normalisation — runs
 // on the GPU.  Between the two, each 8x8 block travels as a 64-bit mask of its non-zero
-// coefficients (natural order) plus those values (int16): ~4x fewer bytes over PCIe than the
+// coefficients (zig-zag order, as decoded) plus those values (int16): ~4x fewer bytes over PCIe than the
 // dense coefficients or the decoded pixels.
 //
 // Numerics follow the IJG libjpeg algorithms that libjpeg-turbo implements bit-exactly (the
@@ -41,16 +41,22 @@ struct Frame {
     }
 };
 
-// Parse the headers and entropy-decode every scan into dense int16 coefficients, natural order,
-// component-major, each component's blocks row-major (bw x bh).  coef is resized as needed.
-// Returns false with a message on malformed / unsupported input.
+// One image's blocks in sparse form, as decoded: masks[b] = bit k set <=> the coefficient at
+// zig-zag position k of block b (component-major, each component's blocks row-major, bw x bh) is
+// non-zero; its non-zero values, in zig-zag order, start at vals[voff[b]].
+struct Sparse {
+    std::vector<uint64_t> masks;
+    std::vector<uint32_t> voff;
+    std::vector<int16_t> vals;  // capacity; the first nvals are used
+    long long nvals = 0;
+};
+// Parse the headers and entropy-decode every scan straight into the sparse form.  Returns false
+// with a message on malformed / unsupported input.
+bool decode_sparse(const uint8_t* data, size_t n, Frame& f, Sparse& sp, std::string& err);
+// The same as dense int16 coefficients, natural order (tests: vit_jpeg_coefficients).
 bool decode_coefficients(const uint8_t* data, size_t n, Frame& f, std::vector<int16_t>& coef, std::string& err);
 // Headers only (dimensions, components, sampling kind).
 bool parse_header(const uint8_t* data, size_t n, Frame& f, std::string& err);
-
-// Sparse form of one image's blocks: masks[b] = bit k set <=> coefficient k (natural order) of
-// block b is non-zero; the non-zero values of block b follow those of block b-1 in vals.
-void pack_sparse(const int16_t* coef, long long nblocks, uint64_t* masks, int16_t* vals, long long& nvals);
 
 }  // namespace jpg
 }  // namespace vit
