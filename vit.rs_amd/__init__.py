@@ -174,6 +174,8 @@ def lib():
         raise VitError(f"{LIB_PATH} not built; run __graft_entry__.build() or make -C vit.rs_amd")
     L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
     for name, (res, args) in _SIGS.items():
+        if os.environ.get("VIT_LIB") and not hasattr(L, name):
+            continue  # an older A/B build may lack newer entry points
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
