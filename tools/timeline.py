@@ -1,14 +1,19 @@
 """Concurrency analysis of a rocprofv3 kernel trace: for the last N steps (split at sgd_bf16_k),
 the wall span, the union of busy intervals, and per-stream / per-kernel busy time.
-    python tools/timeline.py gpurun_out/tl/run_results.db [steps]"""
+    python tools/timeline.py gpurun_out/tl/run_results.db|run_kernel_trace.csv [steps]"""
 import sqlite3
 import sys
 from collections import defaultdict
 
 db = sys.argv[1]
 nsteps = int(sys.argv[2]) if len(sys.argv) > 2 else 2
-c = sqlite3.connect(db)
-rows = c.execute("select name, stream_id, start, end from kernels order by start").fetchall()
+if db.endswith(".csv"):  # rocprofv3 --output-format csv kernel trace
+    import csv
+    rows = sorted(((r["Kernel_Name"], int(r["Stream_Id"]), int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+                   for r in csv.DictReader(open(db))), key=lambda r: r[2])
+else:
+    c = sqlite3.connect(db)
+    rows = c.execute("select name, stream_id, start, end from kernels order by start").fetchall()
 sgd = [i for i, r in enumerate(rows) if "sgd_bf16_k" in r[0]]
 lo, hi = sgd[-nsteps - 1] + 1, sgd[-1] + 1
 seg = rows[lo:hi]

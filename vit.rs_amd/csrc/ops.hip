@@ -413,6 +413,30 @@ __global__ void im2col_k(TO* __restrict__ out, const float* __restrict__ px, int
         if constexpr (sizeof(TO) == 2) out[idx] = f2bf(v); else out[idx] = v;
     }
 }
+// the same, 8 consecutive k (= 8 consecutive pixels of one image row: P % 8 == 0, IMG % 8 == 0) per
+// thread: two 16-B loads, one 16-B (bf16) or two (fp32) stores, one index decode per 8 outputs
+template <typename TO>
+__global__ void im2col_vec_k(TO* __restrict__ out, const float* __restrict__ px, int B, int IMG, int P) {
+    const int gw = IMG / P, NP = gw * gw, K8 = 3 * P * P / 8;
+    const long long n = (long long)B * NP * K8;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < n;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const long long row = idx / K8;
+        const int k = (int)(idx - row * K8) * 8;
+        const int b = (int)(row / NP), p = (int)(row - (long long)b * NP);
+        const int c = k / (P * P), r = k - c * P * P, kh = r / P, kw = r - kh * P;
+        const int y = (p / gw) * P + kh, x = (p % gw) * P + kw;
+        const float4* src = reinterpret_cast<const float4*>(px + (((long long)b * 3 + c) * IMG + y) * IMG + x);
+        const float4 a = src[0], d = src[1];
+        if constexpr (sizeof(TO) == 2) {
+            reinterpret_cast<uint4*>(out)[idx] = make_uint4(pack_bf16x2(a.x, a.y), pack_bf16x2(a.z, a.w),
+                                                            pack_bf16x2(d.x, d.y), pack_bf16x2(d.z, d.w));
+        } else {
+            reinterpret_cast<float4*>(out)[2 * idx] = a;
+            reinterpret_cast<float4*>(out)[2 * idx + 1] = d;
+        }
+    }
+}
 // encoded[b,0] = cls + wpe[0]; encoded[b,1+p] = emb[b*NP+p] + wpe[1+p]
 __global__ void patch_assemble_k(float* __restrict__ enc, const float* __restrict__ emb,
                                  const float* __restrict__ cls, const float* __restrict__ wpe,
@@ -426,6 +450,35 @@ __global__ void patch_assemble_k(float* __restrict__ enc, const float* __restric
         const int b = (int)(bt / T), t = (int)(bt - (long long)b * T);
         const float base = t == 0 ? cls[c] : emb[((long long)b * NP + t - 1) * C + c];
         enc[idx] = base + wpe[(long long)t * C + c];
+    }
+}
+// the same for C % 4 == 0: 4 columns per thread (16-B loads and stores, one index decode per 4)
+__global__ void patch_assemble_vec_k(float* __restrict__ enc, const float* __restrict__ emb,
+                                     const float* __restrict__ cls, const float* __restrict__ wpe, int B, int NP,
+                                     int C) {
+    const int T = NP + 1, C4 = C / 4;
+    const long long n = (long long)B * T * C4;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < n;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const long long bt = idx / C4;
+        const int c4 = (int)(idx - bt * C4);
+        const int b = (int)(bt / T), t = (int)(bt - (long long)b * T);
+        const float4 base = t == 0 ? reinterpret_cast<const float4*>(cls)[c4]
+                                   : reinterpret_cast<const float4*>(emb + ((long long)b * NP + t - 1) * C)[c4];
+        const float4 w = reinterpret_cast<const float4*>(wpe + (long long)t * C)[c4];
+        reinterpret_cast<float4*>(enc)[idx] = make_float4(base.x + w.x, base.y + w.y, base.z + w.z, base.w + w.w);
+    }
+}
+// patch rows of a bf16 [B][T][C] gradient into [B*NP][C] bf16, 8 columns (16 B) per thread (C % 8 == 0)
+__global__ void patch_gather_vec_k(bf16_t* __restrict__ out, const bf16_t* __restrict__ denc, int B, int NP, int C) {
+    const int T = NP + 1, C8 = C / 8;
+    const long long n = (long long)B * NP * C8;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < n;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const long long r = idx / C8;
+        const int c8 = (int)(idx - r * C8);
+        const int b = (int)(r / NP), p = (int)(r - (long long)b * NP);
+        reinterpret_cast<uint4*>(out)[idx] = reinterpret_cast<const uint4*>(denc + ((long long)b * T + 1 + p) * C)[c8];
     }
 }
 // gather the patch rows of dencoded into [B*NP, C] (TO = float or bf16; TI likewise)
@@ -446,7 +499,7 @@ __global__ void patch_gather_k(TO* __restrict__ out, const TI* __restrict__ denc
         else out[idx] = lo ? lo8_decode(bf2f(v), lo[src]) : bf2f(v);
     }
 }
-// dwpe[t,c] += colsum_t[c] = sum_b denc[b,t,c] (b ascending); colsum_t -> tsum[t][c]
+// dwpe[t,c] += colsum_t[c] = sum_b denc[b,t,c] (a fixed order); colsum_t -> tsum[t][c]
 template <typename TI>
 __global__ void patch_small_grads_k(float* __restrict__ dwpe, float* __restrict__ tsum,
                                     const TI* __restrict__ denc, const uint8_t* __restrict__ lo, int B, int T,
@@ -455,22 +508,77 @@ __global__ void patch_small_grads_k(float* __restrict__ dwpe, float* __restrict_
     for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < n;
          idx += (long long)gridDim.x * blockDim.x) {
         const int t = (int)(idx / C), c = (int)(idx - (long long)t * C);
-        float s = 0.f;
-        for (int b = 0; b < B; b++) {
-            const long long e = ((long long)b * T + t) * C + c;
-            s += lo ? lo8_decode(to_f32(denc[e]), lo[e]) : to_f32(denc[e]);
+        // 8 independent partial sums (images b = j mod 8), added in a fixed order: eight loads in
+        // flight per thread instead of one dependent chain of B
+        float ps[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        const long long bs = (long long)T * C, e0 = (long long)t * C + c;
+        int b = 0;
+        for (; b + 8 <= B; b += 8) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const long long e = e0 + (b + j) * bs;
+                ps[j] += lo ? lo8_decode(to_f32(denc[e]), lo[e]) : to_f32(denc[e]);
+            }
         }
+        for (int j = 0; b < B; b++, j++) {
+            const long long e = e0 + b * bs;
+            ps[j] += lo ? lo8_decode(to_f32(denc[e]), lo[e]) : to_f32(denc[e]);
+        }
+        const float s = ((ps[0] + ps[1]) + (ps[2] + ps[3])) + ((ps[4] + ps[5]) + (ps[6] + ps[7]));
         dwpe[idx] += s;
         tsum[idx] = s;
     }
 }
-// dcls[c] += tsum[0][c];  dpatch_b[c] += sum_{t>0} tsum[t][c] (t ascending: no atomics)
+// The trainer's form ("bf16 + lo8" input, C % 8 == 0): the images split into `nch` chunks; thread
+// (chunk y, position t, 8 columns) sums its chunk's images in order with 16-B / 8-B loads into
+// part[y][t][c..c+8]; psg_final_k adds the chunks in order (deterministic).  The one-thread-per-column
+// loop over all B images above ran latency-bound at 0.6 TB/s.
+__global__ void psg_part_k(float* __restrict__ part, const bf16_t* __restrict__ denc, const uint8_t* __restrict__ lo,
+                           int B, int T, int C, int bc) {
+    const int C8 = C / 8;
+    const long long tc8 = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (tc8 >= (long long)T * C8) return;
+    const int y = blockIdx.y, b0 = y * bc, b1 = min(B, b0 + bc);
+    const long long e0 = tc8 * 8, bs = (long long)T * C;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int b = b0; b < b1; b++) {
+        const long long e = e0 + b * bs;
+        const uint4 h = *reinterpret_cast<const uint4*>(denc + e);
+        const uint2 q = *reinterpret_cast<const uint2*>(lo + e);
+        const uint32_t hw[4] = {h.x, h.y, h.z, h.w}, qw[2] = {q.x, q.y};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t qq = qw[j >> 1] >> (16 * (j & 1));
+            acc[2 * j] += lo8_decode(__uint_as_float(hw[j] << 16), qq & 0xffu);
+            acc[2 * j + 1] += lo8_decode(__uint_as_float(hw[j] & 0xffff0000u), (qq >> 8) & 0xffu);
+        }
+    }
+    float4* dst = reinterpret_cast<float4*>(part + (long long)y * bs + e0);
+    dst[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    dst[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+}
+__global__ void psg_final_k(float* __restrict__ dwpe, float* __restrict__ tsum, const float* __restrict__ part,
+                            long long n, int nch) {
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float s = 0.f;
+    for (int y = 0; y < nch; y++) s += part[y * n + i];
+    dwpe[i] += s;
+    tsum[i] = s;
+}
+// dcls[c] += tsum[0][c];  dpatch_b[c] += sum_{t>0} tsum[t][c] (a fixed order: no atomics)
 __global__ void patch_small_grads_fin_k(float* __restrict__ dcls, float* __restrict__ dpb,
                                         const float* __restrict__ tsum, int T, int C) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
-    float s = 0.f;
-    for (int t = 1; t < T; t++) s += tsum[(long long)t * C + c];
+    float ps[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // t = 1 + j (mod 8): 8 loads in flight
+    int t = 1;
+    for (; t + 8 <= T; t += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) ps[j] += tsum[(long long)(t + j) * C + c];
+    }
+    for (int j = 0; t < T; t++, j++) ps[j] += tsum[(long long)t * C + c];
+    const float s = ((ps[0] + ps[1]) + (ps[2] + ps[3])) + ((ps[4] + ps[5]) + (ps[6] + ps[7]));
     dcls[c] += tsum[c];
     dpb[c] += s;
 }
@@ -637,20 +745,30 @@ void ce_backward(float* dlogits, const float* dlosses, const float* probs, const
     ce_bwd_k<<<grid_for(rows * V, 256), 256, 0, s>>>(dlogits, dlosses, probs, targets, rows, V);
     after_launch("crossentropy_softmax_backward");
 }
-void im2col_f32(float* out, const float* px, int B, int IMG, int P, hipStream_t s) {
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+template <typename TO>
+static void im2col_any(TO* out, const float* px, int B, int IMG, int P, hipStream_t s) {
     const long long n = (long long)B * (IMG / P) * (IMG / P) * 3 * P * P;
-    im2col_k<float><<<grid_for(n, 256), 256, 0, s>>>(out, px, B, IMG, P);
+    if (P % 8 == 0 && IMG % 8 == 0 && al16(out) && al16(px))
+        im2col_vec_k<TO><<<grid_for(n / 8, 256), 256, 0, s>>>(out, px, B, IMG, P);
+    else
+        im2col_k<TO><<<grid_for(n, 256), 256, 0, s>>>(out, px, B, IMG, P);
+}
+void im2col_f32(float* out, const float* px, int B, int IMG, int P, hipStream_t s) {
+    im2col_any<float>(out, px, B, IMG, P, s);
     after_launch("im2col");
 }
 void im2col_bf16(bf16_t* out, const float* px, int B, int IMG, int P, hipStream_t s) {
-    const long long n = (long long)B * (IMG / P) * (IMG / P) * 3 * P * P;
-    im2col_k<bf16_t><<<grid_for(n, 256), 256, 0, s>>>(out, px, B, IMG, P);
+    im2col_any<bf16_t>(out, px, B, IMG, P, s);
     after_launch("im2col_bf16");
 }
 void patch_assemble(float* enc, const float* emb, const float* cls, const float* wpe, int B,
                     int NP, int C, hipStream_t s) {
     const long long n = (long long)B * (NP + 1) * C;
-    patch_assemble_k<<<grid_for(n, 256), 256, 0, s>>>(enc, emb, cls, wpe, B, NP, C);
+    if (C % 4 == 0 && al16(enc) && al16(emb) && al16(cls) && al16(wpe))
+        patch_assemble_vec_k<<<grid_for(n / 4, 256), 256, 0, s>>>(enc, emb, cls, wpe, B, NP, C);
+    else
+        patch_assemble_k<<<grid_for(n, 256), 256, 0, s>>>(enc, emb, cls, wpe, B, NP, C);
     after_launch("patch_assemble");
 }
 void patch_gather_f32(float* out, const float* denc, int B, int NP, int C, hipStream_t s) {
@@ -670,7 +788,10 @@ void patch_gather_f32(float* out, const bf16_t* denc, const uint8_t* lo, int B, 
 }
 void patch_gather_bf16(bf16_t* out, const bf16_t* denc, int B, int NP, int C, hipStream_t s) {
     const long long n = (long long)B * NP * C;
-    patch_gather_k<bf16_t, bf16_t><<<grid_for(n, 256), 256, 0, s>>>(out, denc, nullptr, B, NP, C);
+    if (C % 8 == 0 && al16(out) && al16(denc))
+        patch_gather_vec_k<<<grid_for(n / 8, 256), 256, 0, s>>>(out, denc, B, NP, C);
+    else
+        patch_gather_k<bf16_t, bf16_t><<<grid_for(n, 256), 256, 0, s>>>(out, denc, nullptr, B, NP, C);
     after_launch("patch_gather_bf16");
 }
 template <typename TI>
@@ -688,8 +809,16 @@ void patch_small_grads(float* dcls, float* dwpe, float* dpb, const float* denc, 
     after_launch("patch_small_grads");
 }
 void patch_small_grads(float* dcls, float* dwpe, float* dpb, const bf16_t* denc, const uint8_t* lo, int B, int T,
-                       int C, hipStream_t s, float* ws) {
-    patch_small_grads_any(dcls, dwpe, dpb, denc, lo, B, T, C, s, ws);
+                       int C, hipStream_t s, float* ws, float* part) {
+    if (part && lo && C % 8 == 0 && al16(denc) && ((uintptr_t)lo & 7) == 0 && ws) {
+        const int bc = cdiv(B, PSG_CHUNKS), nch = cdiv(B, bc);
+        const long long n = (long long)T * C;
+        psg_part_k<<<dim3(cdiv(n / 8, 256), nch), 256, 0, s>>>(part, denc, lo, B, T, C, bc);
+        psg_final_k<<<cdiv(n, 256), 256, 0, s>>>(dwpe, ws, part, n, nch);
+        patch_small_grads_fin_k<<<cdiv(C, 256), 256, 0, s>>>(dcls, dpb, ws, T, C);
+    } else {
+        patch_small_grads_any(dcls, dwpe, dpb, denc, lo, B, T, C, s, ws);
+    }
     after_launch("patch_small_grads");
 }
 

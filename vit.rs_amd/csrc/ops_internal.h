@@ -48,8 +48,10 @@ void patch_gather_bf16(bf16_t* out, const bf16_t* denc, int B, int NP, int C, hi
 // (no atomics); ws (nullable = thread workspace): T*C floats of per-position sums
 void patch_small_grads(float* dcls, float* dwpe, float* dpb, const float* denc, int B, int T,
                        int C, hipStream_t s, float* ws = nullptr);
+// part (nullable): PSG_CHUNKS * T * C floats of per-image-chunk partial sums (the chunked form)
+constexpr int PSG_CHUNKS = 16;
 void patch_small_grads(float* dcls, float* dwpe, float* dpb, const bf16_t* denc, const uint8_t* lo, int B, int T,
-                       int C, hipStream_t s, float* ws = nullptr);
+                       int C, hipStream_t s, float* ws = nullptr, float* part = nullptr);
 // attention.hip
 void attn_forward_f32(float* out, float* preatt, float* att, const float* inp, int B, int T, int C,
                       int NH, hipStream_t s);

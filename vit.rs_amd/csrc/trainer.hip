@@ -288,6 +288,7 @@ struct Trainer {
     float *dlosses = nullptr, *dlogits = nullptr, *dlnf = nullptr, *dcls_x = nullptr;
     float *dres_a = nullptr, *dres_b = nullptr, *dln = nullptr;
     float* pos_sums = nullptr;  // [T][C] per-position column sums of the patch-embedding backward
+    float* psg_part = nullptr;  // [PSG_CHUNKS][T][C] per-image-chunk partial sums of the same
     uint8_t *dres_lo = nullptr, *dres_lo2 = nullptr;  // lo8 planes of the bf16 residual-gradient stream
     // deterministic small gradients (no float atomics): stream-s scratch for the fixed-order column
     // sums of the head / fp32 path, and in bf16 / fp8 mode the per-layer partial rows of the
@@ -545,6 +546,7 @@ struct Trainer {
             dres_b = alloc<float>(BT * C);
         }
         pos_sums = alloc<float>((long long)T * C);
+        if (lowp()) psg_part = alloc<float>((long long)PSG_CHUNKS * T * C);
         {  // column-sum / LayerNorm partial rows on s (head, fp32 path)
             const long long a1 = (long long)ln_bwd_blocks(BT) * 2 * C;
             const long long a2 = (long long)cdiv(BT, 256) * std::max(4 * C, NC);
@@ -1099,7 +1101,7 @@ struct Trainer {
             w.ws = gemm_ws; w.ws_bytes = gemm_ws_bytes;
             gemm_bf16(w, s);
         }
-        patch_small_grads(G(P_CLS), G(P_WPE), G(P_PATCH_B), rbA, loA, B, T, C, s, pos_sums);
+        patch_small_grads(G(P_CLS), G(P_WPE), G(P_PATCH_B), rbA, loA, B, T, C, s, pos_sums, psg_part);
         tend();
         chunk_done(L + 1);
     }
