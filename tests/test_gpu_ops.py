@@ -301,9 +301,9 @@ def test_attention_backward_variants(gpu, oracle64, monkeypatch, B, T, NH, HS):
     """Every backward kernel (VIT_ATTN_BWD: persistent one-pass default, one workgroup per item,
     paired roles) on the same inputs: each within the bf16 gate of the fp64 oracle, the variants
     within bf16 rounding of each other, and each deterministic (two launches bitwise equal).
-    ViT-H/14's geometry (head size 80, T = 257) takes the paired-role kernel for every variant (the
-    one-pass kernels need 9 waves of 32 keys there, past the register budget; 6 waves of 48 keys fit
-    but leave two SIMDs with twice the work: 770 vs 669 us, measured r03 and not kept)."""
+    ViT-H/14's geometry (head size 80, T = 257 = 8 x 32 + 1): the one-pass kernel over the first 256
+    keys and all 257 queries plus attn_xkey_k for the last key (its dS per query joins the main
+    kernel's dQ as a rank-1 term); VIT_ATTN_BWD=pair keeps the paired-role kernel."""
     v, o = gpu, oracle64
     C = HS * NH
     rng = np.random.default_rng(T * 7 + NH)  # the seed of test_attention_fused_bf16

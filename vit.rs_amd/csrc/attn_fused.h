@@ -663,6 +663,12 @@ template <int HS>
 constexpr int slice_stride() { return sw_slice<HS>() ? 64 : Geo<HS>::SK; }
 template <int HS>
 constexpr int sds_stride() { return sw_ds<HS>() ? 32 : BWD_SDS; }
+// element (row j, column d) of a slice image as fp32
+template <int HS>
+__device__ __forceinline__ float slice_at(const bf16_t* img, int j, int d) {
+    if constexpr (sw_slice<HS>()) return bf2f(*reinterpret_cast<const bf16_t*>(reinterpret_cast<const char*>(img) + sl_off(j, 2 * d)));
+    else return bf2f(img[j * Geo<HS>::SK + d]);
+}
 // 16-B piece cc of slice row t into a slice image
 template <int HS>
 __device__ __forceinline__ void slice_put(bf16_t* img, int t, int cc, uint4 v) {
@@ -777,9 +783,12 @@ __device__ __forceinline__ void bwd_slice_a(BwdRegs<HS, KK>& R, const bf16_t* Qc
 }
 
 // phase B: dQ^T tiles (dt, u) of the slice at q0, spread over the NW waves; dq = dqkv Q rows of the item
-template <int HS, int NSL, int NW>
+// xk_ds / xk_k (XK): dS[q][T-1] per query of the slice and K[T-1] (fp32) of a key the kernel does not
+// own (attn_xkey_k): its rank-1 term dS[q][T-1] K[T-1] joins the dQ accumulators before the store
+template <int HS, int NSL, int NW, bool XK = false>
 __device__ __forceinline__ void bwd_slice_b(const bf16_t* Ks, const bf16_t* dSs, bf16_t* dq, long long C3, int q0,
-                                            int T, float scale, int w, int lane) {
+                                            int T, float scale, int w, int lane, const float* xk_ds = nullptr,
+                                            const float* xk_k = nullptr) {
     constexpr int DT = Geo<HS>::DT, SV = Geo<HS>::SV;
     constexpr bool SW = sw_ds<HS>();
     const int i = lane & 15, g = lane >> 4;
@@ -801,6 +810,11 @@ __device__ __forceinline__ void bwd_slice_b(const bf16_t* Ks, const bf16_t* dSs,
         acc += acc1;
         // lane (i,g): d = 16dt + 4g + r, q = q0 + 16u + i (padded queries: dS = 0)
         const int q = q0 + 16 * u + i;
+        if constexpr (XK) {
+            const float e = xk_ds[16 * u + i];
+#pragma unroll
+            for (int r = 0; r < 4; r++) acc[r] += e * xk_k[16 * dt + 4 * g + r];
+        }
         if (q < T) store4(dq + (long long)q * C3 + 16 * dt + 4 * g, acc, scale);
     };
     constexpr bool BAL = NW == 7 && 2 * DT == 8;  // one loop body (two inlined copies spill)
@@ -869,9 +883,15 @@ __device__ __forceinline__ void bwd_item_end(BwdRegs<HS, KK>& R, bf16_t* dq, lon
         }
 }
 
-template <int HS, int NKT>
+// XK: T = TP + 1 (ViT-H/14, ViT-L/14 at 224^2: T = 257 = 8 x 32 + 1): the waves own keys 0 .. TP-1
+// on the MFMA path, the queries run in TP/32 + 1 slices, and the last key is handled beside them on
+// the VALU: per slice, 16 lanes per query form s = Q K[T-1] and dP = dO V[T-1] from the slice images
+// (DPP row sums), dS = P (dP - delta) joins phase B's dQ as a rank-1 term, and 2 HS threads
+// accumulate dK[T-1] = sum_q dS Q and dV[T-1] = sum_q P dO over the slices (fixed order)
+template <int HS, int NKT, bool XK = false>
 struct Bwd1 {
     static constexpr int TP = NKT * 16, NW = NKT / 2, NT = NW * 64, NSL = TP / 32;
+    static constexpr int TPQ = TP + (XK ? 32 : 0), NSLQ = TPQ / 32;  // padded queries, query slices
     static constexpr int SK = slice_stride<HS>();  // Q / dO slices: row and transposed reads
     static constexpr int SV = Geo<HS>::SV;   // K image: transposed reads only
     static constexpr int SDS = sds_stride<HS>();
@@ -880,7 +900,8 @@ struct Bwd1 {
     static constexpr int D_OFF = Q_OFF + 2 * 32 * SK * 2;
     static constexpr int S_OFF = D_OFF + 2 * 32 * SK * 2;
     static constexpr int L_OFF = S_OFF + TP * SDS * 2;
-    static constexpr int BYTES = L_OFF + 2 * TP * 4;
+    static constexpr int X_OFF = L_OFF + 2 * TPQ * 4;  // XK: the slice's dS, P of key T-1; K, V rows of it
+    static constexpr int BYTES = X_OFF + (XK ? (64 + 2 * HS) * 4 : 0);
     static constexpr int PER = (32 * Geo<HS>::CH + NT - 1) / NT;  // 16-B pieces per thread per slice operand
 };
 // LDS, and registers: up to 8 waves (2 per SIMD, 256 VGPRs) for HS <= 80; 4 waves for HS 96/128
@@ -890,8 +911,14 @@ constexpr bool bwd1_fits() {
     return Bwd1<HS, NKT>::BYTES <= 160 * 1024 && (NKT / 2 <= 4 || (NKT / 2 <= 8 && HS <= 80)) &&
            NKT / 2 <= ATTN_PART_ROWS;
 }
-
+// the XK form at NKT key tiles: the same register rule, LDS with the extra query slice
 template <int HS, int NKT>
+constexpr bool bwd1_fits_xk() {
+    return Bwd1<HS, NKT, true>::BYTES <= 160 * 1024 && (NKT / 2 <= 4 || (NKT / 2 <= 8 && HS <= 80)) &&
+           NKT / 2 + 1 <= ATTN_PART_ROWS;
+}
+
+template <int HS, int NKT, bool XK = false>
 __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restrict__ dqkv,
                                                                const bf16_t* __restrict__ dout,
                                                                const bf16_t* __restrict__ qkv,
@@ -899,8 +926,9 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
                                                                const float* __restrict__ lse, int T,
                                                                int C, int NH, float* __restrict__ dsum) {
     using G = Geo<HS>;
-    using Z = Bwd1<HS, NKT>;
+    using Z = Bwd1<HS, NKT, XK>;
     constexpr int TP = Z::TP, NW = Z::NW, NT = Z::NT, NSL = Z::NSL, SK = Z::SK, SV = Z::SV;
+    constexpr int TPQ = Z::TPQ, NSLQ = Z::NSLQ;
     constexpr int KS = G::KS, CH = G::CH, PER = Z::PER;
     __shared__ __attribute__((aligned(16))) char lds[Z::BYTES];
     bf16_t* Ks = reinterpret_cast<bf16_t*>(lds + Z::K_OFF);
@@ -908,7 +936,11 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
     bf16_t* Ds = reinterpret_cast<bf16_t*>(lds + Z::D_OFF);
     bf16_t* dSs = reinterpret_cast<bf16_t*>(lds + Z::S_OFF);
     float* lse_s = reinterpret_cast<float*>(lds + Z::L_OFF);
-    float* del_s = lse_s + TP;
+    float* del_s = lse_s + TPQ;
+    float* xds_s = reinterpret_cast<float*>(lds + Z::X_OFF);  // XK only: dS, P of key T-1 (32 each), K, V rows
+    float* xp_s = xds_s + 32;
+    float* xk_s = xp_s + 32;
+    float* xv_s = xk_s + HS;
     const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
     const long long C3 = 3LL * C;
     const bf16_t* base = qkv + (long long)b * T * C3 + h * HS;
@@ -959,7 +991,7 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
     }
     put_slice(0);
     // lse and delta = rowsum(dO * O) for every query (padded queries: lse = +inf -> P = 0)
-    for (int t = tid; t < TP; t += NT) {
+    for (int t = tid; t < TPQ; t += NT) {
         float dl = 0.f, ls = INFINITY;
         if (t < T) {
             ls = lse[(long long)bh * T + t];
@@ -971,23 +1003,74 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
         lse_s[t] = ls;
         del_s[t] = dl;
     }
+    if constexpr (XK) {
+        for (int d = tid; d < HS; d += NT) {
+            xk_s[d] = bf2f(base[C + (long long)(T - 1) * C3 + d]);
+            xv_s[d] = bf2f(base[2 * C + (long long)(T - 1) * C3 + d]);
+        }
+    }
     __syncthreads();
+    float xacc = 0.f, xsds = 0.f;  // XK: this thread's dK / dV element of key T-1; sum of its dS
     const float scale = 1.0f / sqrtf((float)HS);
     const float c = LOG2E * scale;
     R.zero();
 #pragma unroll 1
-    for (int sl = 0; sl < NSL; sl++) {
+    for (int sl = 0; sl < NSLQ; sl++) {
         const int q0 = sl * 32, cur = sl & 1;
-        if (sl + 1 < NSL) fetch_slice(q0 + 32);  // lands in registers during phase A
+        if (sl + 1 < NSLQ) fetch_slice(q0 + 32);  // lands in registers during phase A
         bwd_slice_a<HS>(R, Qs + cur * 32 * SK, Ds + cur * 32 * SK, lse_s + q0, del_s + q0, dSs + key0 * Z::SDS, c, lane);
+        if constexpr (XK) {  // key T-1 against the slice's 32 queries: 16 lanes per query
+            const bf16_t* Qc = Qs + cur * 32 * SK;
+            const bf16_t* Dc = Ds + cur * 32 * SK;
+            for (int idx = tid; idx < 512; idx += NT) {
+                const int j = idx >> 4, part = idx & 15;
+                float sq = 0.f, dp = 0.f;
+#pragma unroll
+                for (int d = part; d < HS; d += 16) {
+                    sq += slice_at<HS>(Qc, j, d) * xk_s[d];
+                    dp += slice_at<HS>(Dc, j, d) * xv_s[d];
+                }
+                sq = row_sum16(sq);
+                dp = row_sum16(dp);
+                if (part == 15) {
+                    const float p = q0 + j < T ? fexp2(sq * c - lse_s[q0 + j]) : 0.f;
+                    xds_s[j] = p * (dp - del_s[q0 + j]);
+                    xp_s[j] = p;
+                }
+            }
+        }
         __syncthreads();
-        if (sl + 1 < NSL) put_slice(cur ^ 1);  // its buffer was last read in the previous slice
-        bwd_slice_b<HS, NSL, NW>(Ks, dSs, dq, C3, q0, T, scale, w, lane);
+        if constexpr (XK) {
+            if (tid < 2 * HS) {
+                const bf16_t* img = (tid < HS ? Qs : Ds) + cur * 32 * SK;
+                const float* wv = tid < HS ? xds_s : xp_s;
+                const int d = tid < HS ? tid : tid - HS;
+                for (int j = 0; j < 32; j++) {
+                    xacc += wv[j] * slice_at<HS>(img, j, d);
+                    xsds += xds_s[j];
+                }
+            }
+        }
+        if (sl + 1 < NSLQ) put_slice(cur ^ 1);  // its buffer was last read in the previous slice
+        bwd_slice_b<HS, NSL, NW, XK>(Ks, dSs, dq, C3, q0, T, scale, w, lane, xds_s, xk_s);
         __syncthreads();
     }
-    // per-wave column-sum rows: dsum[((b NW + w) NH + h)][3 HS]
+    // per-wave column-sum rows: dsum[((b NWR + w) NH + h)][3 HS], NWR = NW (+ 1: attn_xkey_k's row)
+    constexpr int NWR = NW + (XK ? 1 : 0);
     bwd_item_end<HS>(R, dq, C, key0, T, scale,
-                     dsum ? dsum + ((long long)(b * NW + w) * NH + h) * 3 * HS : nullptr, lane);
+                     dsum ? dsum + ((long long)(b * NWR + w) * NH + h) * 3 * HS : nullptr, lane);
+    if constexpr (XK) {  // key T-1's dK, dV and its column-sum row (index NW of the item)
+        if (tid < 2 * HS) {
+            const int d = tid < HS ? tid : tid - HS;
+            const float v = tid < HS ? xacc * scale : xacc;
+            dq[(long long)(T - 1) * C3 + (tid < HS ? C : 2 * C) + d] = f2bf(v);
+            if (dsum) {
+                float* row = dsum + ((long long)(b * NWR + NW) * NH + h) * 3 * HS;
+                row[(tid < HS ? HS : 2 * HS) + d] = v;
+                if (tid < HS) row[d] = scale * xsds * xk_s[d];
+            }
+        }
+    }
 }
 
 template <int HS, int NKT, int KK = 2>
@@ -1251,6 +1334,16 @@ int launch_bwd(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t
             return NKT / 2;
         }
     }
+    // T = 32k + 1 (ViT-H/14, ViT-L/14 at 224^2: T = 257): the one-pass kernel over the first T-1 keys
+    // (NKT - 2 tiles) and all queries, the last key on its VALU side path (XK)
+    if constexpr (NKT > 2 && bwd1_fits_xk<HS, NKT - 2>()) {
+        if (v != 2 && T == (NKT - 2) * 16 + 1) {
+            constexpr int NW = (NKT - 2) / 2;
+            attn_bwd1_k<HS, NKT - 2, true><<<BH, NW * 64, 0, s>>>(dqkv, dout, qkv, out, lse, T, C, NH, part);
+            count_hit(VIT_HIT_ATTN_BWD_ONEPASS);
+            return NW + 1;
+        }
+    }
     attn_bwd_pair_k<HS, NKT><<<2 * cdiv(BH, 8) * 8, 256, 0, s>>>(dqkv, dout, qkv, out, lse, T, C, NH, BH, part);
     count_hit(VIT_HIT_ATTN_BWD_PAIR);
     return 1;
@@ -1297,7 +1390,7 @@ VIT_FA_DECLARE(128)
         return fa::dispatch_fwd<HS>(cdiv(T, 32) * 2, out, lse, qkv, B, T, C, NH, s);                \
     }                                                                                               \
     int fa_backward_h##HS(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t* out,   \
-                          const float* lse, int B, int T, int C, int NH, float* part, hipStream_t s) {  \
+                          const float* lse, int B, int T, int C, int NH, float* part, hipStream_t s) { \
         return fa::dispatch_bwd<HS>(cdiv(T, 32) * 2, dqkv, dout, qkv, out, lse, B, T, C, NH, part, s); \
     }                                                                                               \
     int fa_max_t_h##HS() { return fa::max_tp<HS>(); }
