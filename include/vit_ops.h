@@ -58,6 +58,8 @@ enum {
     VIT_HIT_ATTN_BWD_ONEPASS = 83,   /* one-pass backward, one workgroup per (b,h) */
     VIT_HIT_ATTN_BWD_PAIR = 84,      /* paired-role backward */
     VIT_HIT_ATTN_GENERIC = 85,       /* generic VALU attention (T past the MFMA kernels' LDS) */
+    VIT_HIT_ATTN_BWD_XKEY = 86,      /* one-pass backward + the last key's side path (T = 32k + 1) */
+    VIT_HIT_QUANT_ROWCOL = 87,       /* fused row + column MX quantization */
     VIT_HIT_COUNT = 96
 };
 int vit_kernel_hits(long long* out, int n); /* copies min(n, VIT_HIT_COUNT); returns VIT_HIT_COUNT */
@@ -198,6 +200,14 @@ void quantize_mx_f32_ex(uint8_t* q, uint8_t* scales, const float* x, long long R
 long long mx_cols_padded(long long R);
 void quantize_mx_cols_bf16_ex(uint8_t* q, uint8_t* scales, const uint16_t* x, long long R, int C,
                               long long ldx);
+/* both forms in one read of x [R][C] (row stride ldx): qr [R][C] + scales_r exactly as
+ * quantize_mx_bf16_ex(qr, scales_r, x, R, C, ldx, C), and the column form of tokens
+ * [tok_off, tok_off + ntok) of a [C][ldqc] matrix + scales_c (mx_scale_size(C, ldqc) bytes) exactly
+ * as the same span of quantize_mx_cols_bf16_ex over the whole token axis; tok_off % 64 == 0,
+ * R <= ntok <= R rounded up to 64 (tokens R .. ntok-1 are zero padding). */
+void quantize_mx_rowcol_bf16_ex(uint8_t* qr, uint8_t* scales_r, uint8_t* qc, uint8_t* scales_c,
+                                const uint16_t* x, long long R, int C, long long ldx, long long ldqc,
+                                long long tok_off, long long ntok);
 void gemm_fp8_fused(void* C, void* C2, long long ldc, const void* aux, long long ldaux,
                     const uint8_t* A, const uint8_t* a_scale, long long lda, const uint8_t* B,
                     const uint8_t* b_scale, long long ldb, const float* bias, float* colsum_out,

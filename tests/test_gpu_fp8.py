@@ -203,6 +203,45 @@ def test_quantize_mx_cols_bit_exact(gpu, R, C):
     assert np.array_equal(q.numpy().reshape(C, kp), q_ref)
 
 
+@pytest.mark.parametrize("R,C,parts", [(100, 128, 1), (197, 768, 1), (4001, 320, 1), (2 * 257 * 16, 1280, 2),
+                                        (3 * 1024 + 70, 192, 3)])
+def test_quantize_mx_rowcol_bit_exact(gpu, R, C, parts):
+    """The fused row+column quantizer (the fp8 trainer's ln1 / atty / ln2 / dres / dqkv) equals the
+    two separate quantizers byte for byte: the row form of each micro-batch slice against
+    quantize_mx_bf16_ex, the column form assembled from `parts` slices (token offsets multiples of
+    64, the last one carrying the padding tokens) against one quantize_mx_cols_bf16_ex over all R."""
+    v = gpu
+    rng = np.random.default_rng(R + C + parts)
+    x = (rng.normal(size=(R, C)) * np.exp2(rng.integers(-12, 12, size=(1, C)))).astype(np.float32)
+    x[rng.random(size=x.shape) < 0.01] = 0.0
+    xb = v.bf16_bits(x)
+    xd = D(v, xb, np.uint16)
+    kp = int(v.lib().mx_cols_padded(R))
+    nsc = int(v.lib().mx_scale_size(C, kp))
+    qc_ref, sc_ref = Z(v, C * kp, np.uint8), Z(v, nsc, np.uint8)
+    v.call("quantize_mx_cols_bf16_ex", qc_ref, sc_ref, xd, R, C, C)
+    qc = D(v, np.full(C * kp, 0x5A, np.uint8), np.uint8)
+    sc = D(v, np.full(nsc, 0x5A, np.uint8), np.uint8)
+    step = ((R + parts - 1) // parts + 63) // 64 * 64 if parts > 1 else R
+    bounds = [min(i * step, R) for i in range(parts)] + [R]
+    for lo, hi in zip(bounds[:-1], bounds[1:]):
+        n = hi - lo
+        if n <= 0:
+            continue
+        ntok = kp - lo if hi == R else n
+        nsr = int(v.lib().mx_scale_size(n, C))
+        qr = D(v, np.full(n * C, 0x5A, np.uint8), np.uint8)
+        sr = D(v, np.full(nsr, 0x5A, np.uint8), np.uint8)
+        xs = D(v, xb.reshape(R, C)[lo:hi].copy(), np.uint16)
+        v.call("quantize_mx_rowcol_bf16_ex", qr, sr, qc, sc, xs, n, C, C, kp, lo, ntok)
+        qr_ref, sr_ref = Z(v, n * C, np.uint8), Z(v, nsr, np.uint8)
+        v.call("quantize_mx_bf16_ex", qr_ref, sr_ref, xs, n, C, C, C)
+        assert np.array_equal(sr.numpy(), sr_ref.numpy()), f"row scales differ at slice {lo}"
+        assert np.array_equal(qr.numpy(), qr_ref.numpy()), f"row bytes differ at slice {lo}"
+    assert np.array_equal(sc.numpy(), sc_ref.numpy()), "column scales differ"
+    assert np.array_equal(qc.numpy(), qc_ref.numpy()), "column bytes differ"
+
+
 @pytest.mark.parametrize("OC,Cin,R", [(256, 256, 64), (768, 320, 1000), (1280, 5120, 4112), (512, 768, 6000)])
 def test_gemm_fp8_wgrad_splitk(gpu, OC, Cin, R):
     """The fp8 weight gradient dW += dout^T . inp (epi 2) on column-quantized operands: one split

@@ -440,6 +440,38 @@ def test_fp8_fused_mx_epilogues_bit_identical(gpu, monkeypatch):
         assert np.array_equal(res["1"][2], res["0"][2])
 
 
+def test_fp8_rowcol_quantize_bit_identical(gpu, monkeypatch):
+    """fp8 mode's fused row+column quantization (ln1 / atty / ln2 column forms kept from the
+    forward, dres3 / dres2 / dqkv column forms written by the input-gradient GEMMs' quantize step and
+    read by the weight gradients on the second stream) against separate column quantization in the
+    weight gradients (VIT_FP8_ROWCOL=0): bit-identical loss, logits and gradients, one and two
+    micro-batches (B=128 at T=17: 2176 and 1088 tokens, whole 64-token column chunks), and the fused
+    quantizer actually ran (6 launches per layer and micro-batch)."""
+    v = gpu
+    cfg = v.data.CONFIGS["test_h64"]
+    B = 128
+    params = v.data.init_params(cfg, "parity", seed=5)
+    px, lab = v.data.synthetic_batch(cfg, B, seed=6)
+    for mb in ("1", "2"):
+        monkeypatch.setenv("VIT_MICROBATCH", mb)
+        res = {}
+        for rc in ("1", "0"):
+            monkeypatch.setenv("VIT_FP8_ROWCOL", rc)
+            m = v.ViT.build(cfg, B, v.VIT_FP8, params=params)
+            m.zero_grad()
+            v.kernel_hits_reset()
+            loss = m.forward(px, lab)
+            m.backward()
+            hits = v.kernel_hits()
+            res[rc] = (loss, m.logits(), m.grads())
+            m.close()
+            want = 6 * cfg.num_layers * int(mb) if rc == "1" else 0
+            assert hits[v.HIT_QUANT_ROWCOL] == want, (mb, rc, hits[v.HIT_QUANT_ROWCOL])
+        assert res["1"][0] == res["0"][0]
+        assert np.array_equal(res["1"][1], res["0"][1])
+        assert np.array_equal(res["1"][2], res["0"][2])
+
+
 def test_fp8_training_reduces_loss(gpu):
     """fp8 mode fits one batch like the bf16 mode (40 SGD steps, loss / 10) and its first steps
     track the bf16 trajectory within 1e-1 (measured 6 %: e4m3 rounding of every GEMM operand)."""

@@ -106,6 +106,7 @@ _SIGS = {
     "quantize_mx_f32_ex": (None, [P, P, P, LL, I, LL, LL]),
     "mx_cols_padded": (LL, [LL]),
     "quantize_mx_cols_bf16_ex": (None, [P, P, P, LL, I, LL]),
+    "quantize_mx_rowcol_bf16_ex": (None, [P, P, P, P, P, LL, I, LL, LL, LL, LL]),
     "gemm_fp8_fused": (None, [P, P, LL, P, LL, P, P, LL, P, P, LL, P, P, I, I, I, I]),
     "gemm_fp8_fused_mx": (None, [P, P, LL, P, LL, P, P, LL, P, P, LL, P, P, I, I, I, I, P, P]),
     "gemm_bf16_set_variant": (None, [I]), "gemm_bf16_set_debug": (None, [I]),
@@ -191,6 +192,7 @@ def lib():
 HIT_GEMM_128, HIT_GEMM_256x256, HIT_GEMM_256x128, HIT_GEMM_FP8, HIT_GEMM_F32 = 0, 16, 32, 48, 64
 HIT_SPLITK_REDUCE, HIT_ATTN_FWD_MFMA, HIT_ATTN_BWD_PERSISTENT = 80, 81, 82
 HIT_ATTN_BWD_ONEPASS, HIT_ATTN_BWD_PAIR, HIT_ATTN_GENERIC = 83, 84, 85
+HIT_ATTN_BWD_XKEY, HIT_QUANT_ROWCOL = 86, 87
 
 
 def kernel_hits():

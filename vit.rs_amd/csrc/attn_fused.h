@@ -1340,7 +1340,7 @@ int launch_bwd(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t
         if (v != 2 && T == (NKT - 2) * 16 + 1) {
             constexpr int NW = (NKT - 2) / 2;
             attn_bwd1_k<HS, NKT - 2, true><<<BH, NW * 64, 0, s>>>(dqkv, dout, qkv, out, lse, T, C, NH, part);
-            count_hit(VIT_HIT_ATTN_BWD_ONEPASS);
+            count_hit(VIT_HIT_ATTN_BWD_XKEY);
             return NW + 1;
         }
     }

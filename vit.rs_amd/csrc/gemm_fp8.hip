@@ -357,6 +357,87 @@ __global__ __launch_bounds__(TOK * 2) void quantize_mx_cols_k(uint8_t* __restric
     *reinterpret_cast<u32x4*>(dst) = u32x4{w[0], w[1], w[2], w[3]};
     *reinterpret_cast<u32x4*>(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
 }
+
+// Row- and column-wise MX in one pass over x (the fp8 trainer quantizes its GEMM inputs ln1, atty,
+// ln2 and the output gradients dres3, dres2, dqkv both ways: row-wise for the forward / input-
+// gradient GEMM, column-wise for the weight gradient; one read of x instead of two).  Same tile
+// as quantize_mx_cols_k; while a lane holds its 8 elements of a token row on their way into LDS it
+// also forms the row-wise block (4 lanes per 32-column block, as quantize_mx_rows_k), so both
+// outputs equal the two separate quantizers byte for byte.  The column form covers tokens
+// [tok_off, tok_off + ntok) of a [C][ldqc] matrix (one micro-batch of a larger token axis;
+// tok_off % 64 == 0, tokens R .. ntok-1 are zero padding); the row form is [R][C] with its own
+// Rpad (grid.x = Rpad / TOK covers the padding rows' zero scales).
+template <int TOK>
+__global__ __launch_bounds__(TOK * 2) void quantize_mx_rowcol_k(uint8_t* __restrict__ qr, uint8_t* __restrict__ slr,
+                                                               uint8_t* __restrict__ qc, uint8_t* __restrict__ slc,
+                                                               const uint16_t* __restrict__ x, int R, int C,
+                                                               long long ldx, int rgr_tot, long long ldqc, int tok_off,
+                                                               int ntok, int rgc_tot) {
+    constexpr int NT = TOK * 2;
+    __shared__ __attribute__((aligned(16))) uint16_t tile[TOK * 64];
+    const int tok0 = blockIdx.x * TOK, col0 = blockIdx.y * 64;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int c = col0 + lane, tb = tok0 + 32 * wave;
+    if (col0 >= C) {  // padding rows of the column form's scale layout
+        if (tb < ntok) {
+            const int kb = (tok_off + tb) >> 5;
+            slc[((long long)(kb >> 1) * rgc_tot + (c >> 5)) * 64 + (kb & 1) * 32 + (c & 31)] = 0;
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < TOK * 8 / NT; i++) {
+        const int idx = i * NT + tid, row = idx >> 3, ch = idx & 7, tok = tok0 + row;
+        u32x4 w = u32x4{0u, 0u, 0u, 0u};
+        if (tok < R) w = *reinterpret_cast<const u32x4*>(x + (long long)tok * ldx + col0 + ch * 8);
+        *reinterpret_cast<u32x4*>(tile + row * 64 + ch * 8) = w;
+        float v[8];
+        float amax = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            v[2 * e] = __uint_as_float(w[e] << 16);
+            v[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+            amax = fmaxf(amax, fmaxf(fabsf(v[2 * e]), fabsf(v[2 * e + 1])));
+        }
+        amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+        amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+        const int sb = tok < R ? mx_scale_byte(amax) : 0;
+        if ((ch & 3) == 0) {
+            const int kb = (col0 + ch * 8) >> 5;
+            slr[((long long)(kb >> 1) * rgr_tot + (tok >> 5)) * 64 + (kb & 1) * 32 + (tok & 31)] = (uint8_t)sb;
+        }
+        if (tok < R) {
+            const float inv = __uint_as_float((uint32_t)(254 - sb) << 23);
+            int t0 = __builtin_amdgcn_cvt_pk_fp8_f32(v[0] * inv, v[1] * inv, 0, false);
+            t0 = __builtin_amdgcn_cvt_pk_fp8_f32(v[2] * inv, v[3] * inv, t0, true);
+            int t1 = __builtin_amdgcn_cvt_pk_fp8_f32(v[4] * inv, v[5] * inv, 0, false);
+            t1 = __builtin_amdgcn_cvt_pk_fp8_f32(v[6] * inv, v[7] * inv, t1, true);
+            *reinterpret_cast<uint2*>(qr + (long long)tok * C + col0 + ch * 8) = make_uint2((uint32_t)t0, (uint32_t)t1);
+        }
+    }
+    __syncthreads();
+    if (tb >= ntok) return;
+    float v[32];
+    float amax = 0.f;
+#pragma unroll
+    for (int i = 0; i < 32; i++) {
+        v[i] = __uint_as_float((uint32_t)tile[(32 * wave + i) * 64 + lane] << 16);
+        amax = fmaxf(amax, fabsf(v[i]));
+    }
+    const int sb = mx_scale_byte(amax), kb = (tok_off + tb) >> 5;
+    slc[((long long)(kb >> 1) * rgc_tot + (c >> 5)) * 64 + (kb & 1) * 32 + (c & 31)] = (uint8_t)sb;
+    const float inv = __uint_as_float((uint32_t)(254 - sb) << 23);
+    uint32_t w[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        int t = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * j] * inv, v[4 * j + 1] * inv, 0, false);
+        t = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * j + 2] * inv, v[4 * j + 3] * inv, t, true);
+        w[j] = (uint32_t)t;
+    }
+    uint8_t* dst = qc + (long long)c * ldqc + tok_off + tb;
+    *reinterpret_cast<u32x4*>(dst) = u32x4{w[0], w[1], w[2], w[3]};
+    *reinterpret_cast<u32x4*>(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
+}
 }  // namespace f8
 
 long long mx_rows_padded(long long rows) { return (rows + 255) / 256 * 256; }
@@ -464,6 +545,24 @@ void quantize_mx_cols_bf16(uint8_t* q, uint8_t* sl, const bf16_t* x, long long R
                                                                               kp, cpad / 32);
     after_launch("quantize_mx_cols");
 }
+bool quantize_mx_rowcol_bf16(uint8_t* qr, uint8_t* slr, uint8_t* qc, uint8_t* slc, const bf16_t* x, long long R,
+                             int C, long long ldx, long long ldqc, long long tok_off, long long ntok, hipStream_t s) {
+    if (R <= 0 || C <= 0) return true;
+    if (C % 64 || ldx % 8 || ldqc % 16 || tok_off % 64 || tok_off < 0 || ntok < R || ntok > mx_cols_kp(R) ||
+        tok_off + ntok > ldqc || ((uintptr_t)x & 15) || ((uintptr_t)qr & 15) || ((uintptr_t)qc & 15) ||
+        R >= (1LL << 30) || ldqc >= (1LL << 31)) {
+        set_error("quantize_mx_rowcol: C %% 64, tok_off %% 64, R <= ntok <= R rounded to 64 and 16-B aligned rows "
+                  "required (C=%d R=%lld tok_off=%lld ntok=%lld ldqc=%lld)", C, R, tok_off, ntok, ldqc);
+        return false;
+    }
+    const long long rp = mx_rows_padded(R);
+    const int cpad = (int)mx_rows_padded(C);
+    f8::quantize_mx_rowcol_k<128><<<dim3((unsigned)(rp / 128), cpad / 64), 256, 0, s>>>(
+        qr, slr, qc, slc, (const uint16_t*)x, (int)R, C, ldx, (int)(rp / 32), ldqc, (int)tok_off, (int)ntok, cpad / 32);
+    after_launch("quantize_mx_rowcol");
+    count_hit(VIT_HIT_QUANT_ROWCOL);
+    return true;
+}
 void quantize_mx_batched_bf16(uint8_t* q, uint8_t* sl, const bf16_t* x, long long R, int K, int count,
                               long long xs, long long qs, long long ss, hipStream_t s) {
     quantize_mx<bf16_t>(q, sl, x, R, K, K, K, count, xs, qs, ss, s);
@@ -490,6 +589,10 @@ void quantize_mx_f32_ex(uint8_t* q, uint8_t* scales, const float* x, long long R
 long long mx_cols_padded(long long R) { return mx_cols_kp(R); }
 void quantize_mx_cols_bf16_ex(uint8_t* q, uint8_t* scales, const uint16_t* x, long long R, int C, long long ldx) {
     quantize_mx_cols_bf16(q, scales, (const bf16_t*)x, R, C, ldx, stream());
+}
+void quantize_mx_rowcol_bf16_ex(uint8_t* qr, uint8_t* scales_r, uint8_t* qc, uint8_t* scales_c, const uint16_t* x,
+                                long long R, int C, long long ldx, long long ldqc, long long tok_off, long long ntok) {
+    quantize_mx_rowcol_bf16(qr, scales_r, qc, scales_c, (const bf16_t*)x, R, C, ldx, ldqc, tok_off, ntok, stream());
 }
 void gemm_fp8_fused_mx(void* C, void* C2, long long ldc, const void* aux, long long ldaux, const uint8_t* A,
                        const uint8_t* a_scale, long long lda, const uint8_t* B, const uint8_t* b_scale,

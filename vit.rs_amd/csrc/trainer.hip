@@ -364,6 +364,18 @@ struct Trainer {
     // [Cin][Kp] e4m3 rows on the weight-gradient stream, then the MXFP8 engine with K-split slabs
     bool fp8_wgrad = true;
     QMat wg_a, wg_b;  // column-quantized dout / inp of the running weight gradient (stream-ordered)
+    // fused row+column quantization (quantize_mx_rowcol_bf16): the column forms of ln1, atty, ln2
+    // per layer (written by the forward GEMMs' quantize step, read by the backward's weight
+    // gradients) and of dres3, dres2, dqkv (written by the input-gradient GEMMs' quantize step on
+    // the micro-batch streams, read by the next weight gradient on s2; the waits that already
+    // order dres / dqkv reuse order these too)
+    bool rowcol_ok = false;
+    long long kp_tok = 0;  // mx_cols_kp(B*T)
+    QMat actc[3], dcol[3];
+    bool rowcol_on() const { return fp8() && rowcol_ok && ((long long)(B / nmb) * T) % 64 == 0; }
+    QMat actc_of(int k, int l) const {
+        return {actc[k].q + (long long)l * C * kp_tok, actc[k].s + (long long)l * mx_scale_bytes(C, (int)kp_tok)};
+    }
     int wslot(int k, int l) const {    // memory-order index of layer l's copy of weight kind k
         const long long stride = L > 1 ? off[wkinds[k] * L + 1] - off[wkinds[k] * L] : 0;
         return stride < 0 ? L - 1 - l : l;
@@ -647,6 +659,18 @@ struct Trainer {
                     wg_a.s = alloc<uint8_t>((long long)mx_scale_bytes(4LL * C, (int)kp));
                     wg_b.q = alloc<uint8_t>(4LL * C * kp);
                     wg_b.s = alloc<uint8_t>((long long)mx_scale_bytes(4LL * C, (int)kp));
+                    const char* rc = getenv("VIT_FP8_ROWCOL");
+                    rowcol_ok = !(rc && rc[0] == '0');
+                    kp_tok = kp;
+                    if (rowcol_ok) {
+                        for (int k = 0; k < 3; k++) {
+                            actc[k].q = alloc<uint8_t>((long long)L * C * kp);
+                            actc[k].s = alloc<uint8_t>((long long)L * mx_scale_bytes(C, (int)kp));
+                            const long long w = k == 2 ? 3LL * C : C;
+                            dcol[k].q = alloc<uint8_t>(w * kp);
+                            dcol[k].s = alloc<uint8_t>((long long)mx_scale_bytes(w, (int)kp));
+                        }
+                    }
                 }
             }
         } else {
@@ -770,8 +794,10 @@ struct Trainer {
     // MXFP8 engine against the weight's fp8 copy
     // pre: the A operand already in MX form (a fused epilogue wrote it); otherwise it is quantized
     // here.  mx_out: ask this GEMM's epilogue for the MX copy of its bf16 output (fp8 mode, fused)
+    // colq: also write the column form of this micro-batch's A rows into colq (rowcol_on());
+    // rec_ev: then record micro-batch event rec_ev (the weight gradient that reads colq waits on it)
     void gemm_w(int cls, GemmArgs a, int ti, int l, bool transposed, int mb, hipStream_t st, bool pre = false,
-                bool mx_out = false) {
+                bool mx_out = false, const QMat* colq = nullptr, int rec_ev = -1) {
         if (!fp8()) { gemm(cls, a, true, st); return; }
         if (mx_out) { a.mx_q = act_q2[mb]; a.mx_s = act_s2[mb]; }
         const uint8_t* aq = act_q[mb];
@@ -781,8 +807,16 @@ struct Trainer {
             as = act_s2[mb];
         } else {
             tbeg(TC_QUANT, 0, st);
-            quantize_mx_bf16(act_q[mb], act_s[mb], (const bf16_t*)a.A, a.M, a.K, a.lda, a.K, st);
+            if (colq) {
+                const long long r0 = (long long)mb * (B / nmb) * T;
+                const long long ntok = mb == nmb - 1 ? kp_tok - r0 : a.M;
+                quantize_mx_rowcol_bf16(act_q[mb], act_s[mb], colq->q, colq->s, (const bf16_t*)a.A, a.M, a.K, a.lda,
+                                        kp_tok, r0, ntok, st);
+            } else {
+                quantize_mx_bf16(act_q[mb], act_s[mb], (const bf16_t*)a.A, a.M, a.K, a.lda, a.K, st);
+            }
             tend();
+            if (rec_ev >= 0 && two_streams) VIT_HIP(hipEventRecord(mev[mb][rec_ev], st));
         }
         const QMat w = transposed ? wtq_of(ti, l) : wq_of(ti, l);
         a.A = aq; a.lda = a.K; a.a_scale = as;
@@ -888,7 +922,10 @@ struct Trainer {
                 GemmArgs q;
                 q.A = a.ln1 + r0 * C; q.lda = C; q.B = W(P_QKVW, l); q.ldb = C; q.C = a.qkv + r0 * 3 * C;
                 q.ldc = 3 * C; q.bias = P(P_QKVB, l); q.M = (int)R; q.N = 3 * C; q.K = C; q.epi = EPI_BF16_STORE;
-                gemm_w(TC_QKV_FWD, q, P_QKVW, l, false, mb, st);
+                const bool rc = rowcol_on();
+                QMat c_ln1 = rc ? actc_of(0, l) : QMat{}, c_atty = rc ? actc_of(1, l) : QMat{},
+                     c_ln2 = rc ? actc_of(2, l) : QMat{};
+                gemm_w(TC_QKV_FWD, q, P_QKVW, l, false, mb, st, false, false, rc ? &c_ln1 : nullptr);
                 tbeg(TC_ATTN_FWD, 4.0 * Bm * (double)T * T * C, st);
                 attn_forward_fused(a.atty + r0 * C, a.lse + (long long)mb * Bm * NH * T, a.qkv + r0 * 3 * C, Bm, T, C, NH, st);
                 tend();
@@ -896,7 +933,7 @@ struct Trainer {
                 pr.A = a.atty + r0 * C; pr.lda = C; pr.B = W(P_ATTPROJW, l); pr.ldb = C; pr.C = a.res2 + r0 * C;
                 pr.ldc = C; pr.bias = P(P_ATTPROJB, l); pr.aux = x; pr.ldaux = C;
                 pr.M = (int)R; pr.N = C; pr.K = C; pr.epi = EPI_F32_RESID;
-                gemm_w(TC_PROJ_FWD, pr, P_ATTPROJW, l, false, mb, st);
+                gemm_w(TC_PROJ_FWD, pr, P_ATTPROJW, l, false, mb, st, false, false, rc ? &c_atty : nullptr);
                 tbeg(TC_LN_FWD, 0, st);
                 ln_forward_bf16(a.ln2 + r0 * C, a.ln2_mean + r0, a.ln2_rstd + r0, a.res2 + r0 * C, P(P_LN2W, l),
                                 P(P_LN2B, l), R, C, st);
@@ -906,7 +943,7 @@ struct Trainer {
                 f.A = a.ln2 + r0 * C; f.lda = C; f.B = W(P_FCW, l); f.ldb = C; f.C = a.fchd + r0 * 4 * C;
                 f.C2 = a.fchg + r0 * 4 * C; f.ldc = 4 * C; f.bias = P(P_FCB, l); f.M = (int)R; f.N = 4 * C;
                 f.K = C; f.epi = EPI_BF16_GELU_D;
-                gemm_w(TC_FC_FWD, f, P_FCW, l, false, mb, st, false, fuse_mx);
+                gemm_w(TC_FC_FWD, f, P_FCW, l, false, mb, st, false, fuse_mx, rc ? &c_ln2 : nullptr);
                 GemmArgs fp;
                 fp.A = a.fchg + r0 * 4 * C; fp.lda = 4 * C; fp.B = W(P_FCPROJW, l); fp.ldb = 4 * C;
                 fp.C = a.res3 + r0 * C; fp.ldc = C; fp.bias = P(P_FCPROJB, l); fp.aux = a.res2 + r0 * C;
@@ -921,8 +958,9 @@ struct Trainer {
     // dW[OC,Cin] += dout^T . inp (reduction over all B*T rows, split-K slabs) on the weight-
     // gradient stream once every micro-batch stream has passed `ready` (dout final there); the
     // event `done` marks the end of its reads of dout / inp
+    // dout_c / inp_c: column forms already written (rowcol_on(); dout_c's producer recorded `ready`)
     void wgrad(int cls, const bf16_t* dout, int OC, const bf16_t* inp, int Cin, float* dW, int ready,
-               int done) {
+               int done, const QMat* dout_c = nullptr, const QMat* inp_c = nullptr) {
         GemmArgs w;
         w.A = dout; w.lda = OC; w.a_kcontig = false;
         w.B = inp; w.ldb = Cin; w.b_kcontig = false;
@@ -931,18 +969,21 @@ struct Trainer {
         hipStream_t st = two_streams ? s2 : s;
         if (two_streams) {
             for (int mb = 0; mb < nmb; mb++) {
-                VIT_HIP(hipEventRecord(mev[mb][ready], ms[mb]));
+                if (!dout_c) VIT_HIP(hipEventRecord(mev[mb][ready], ms[mb]));
                 VIT_HIP(hipStreamWaitEvent(s2, mev[mb][ready], 0));
             }
         }
         if (fp8() && fp8_wgrad) {
             const long long kp = mx_cols_kp(BT);
-            tbeg(TC_QUANT, 0, st);
-            quantize_mx_cols_bf16(wg_a.q, wg_a.s, dout, BT, OC, OC, st);
-            quantize_mx_cols_bf16(wg_b.q, wg_b.s, inp, BT, Cin, Cin, st);
-            tend();
-            w.A = wg_a.q; w.lda = kp; w.a_kcontig = true; w.a_scale = wg_a.s;
-            w.B = wg_b.q; w.ldb = kp; w.b_kcontig = true; w.b_scale = wg_b.s;
+            const QMat qa = dout_c ? *dout_c : wg_a, qb = inp_c ? *inp_c : wg_b;
+            if (!dout_c || !inp_c) {
+                tbeg(TC_QUANT, 0, st);
+                if (!dout_c) quantize_mx_cols_bf16(wg_a.q, wg_a.s, dout, BT, OC, OC, st);
+                if (!inp_c) quantize_mx_cols_bf16(wg_b.q, wg_b.s, inp, BT, Cin, Cin, st);
+                tend();
+            }
+            w.A = qa.q; w.lda = kp; w.a_kcontig = true; w.a_scale = qa.s;
+            w.B = qb.q; w.ldb = kp; w.b_kcontig = true; w.b_scale = qb.s;
             w.K = (int)kp;
             tbeg(cls, 2.0 * w.M * (double)w.N * BT, st);
             gemm_fp8(w, st);
@@ -1013,8 +1054,12 @@ struct Trainer {
         for (int l = L - 1; l >= 0; l--) {
             LayerActs& a = la[l];
             const float* xl = l == 0 ? encoded : la[l - 1].res3;
+            // rowcol: the weight gradients whose dout column form the dgrads' quantize step writes
+            // are issued after those dgrads (s2 waits on the event recorded after the quantize)
+            const bool rc = rowcol_on();
+            QMat c_ln1 = rc ? actc_of(0, l) : QMat{}, c_atty = rc ? actc_of(1, l) : QMat{}, c_ln2 = rc ? actc_of(2, l) : QMat{};
             // fcproj: dfch = (dres3 . fcprojw) * gelu'(fch) (stored as fchd);  fcprojw += dres3^T . fchg
-            wgrad(TC_FCPROJ_WGRAD, rbA, C, a.fchg, 4 * C, G(P_FCPROJW, l), EV_RESA, EV_W1);
+            if (!rc) wgrad(TC_FCPROJ_WGRAD, rbA, C, a.fchg, 4 * C, G(P_FCPROJW, l), EV_RESA, EV_W1);
             for (int mb = 0; mb < nmb; mb++) {
                 const long long r0 = mb * R;
                 after_wgrad(EV_W2, ms[mb]);  // the previous layer's fc wgrad has read dfch
@@ -1023,10 +1068,11 @@ struct Trainer {
                 d1.C = dfch + r0 * 4 * C; d1.ldc = 4 * C; d1.aux = a.fchd + r0 * 4 * C; d1.ldaux = 4 * C;
                 d1.M = (int)R; d1.N = 4 * C; d1.K = C; d1.epi = EPI_BF16_MUL;
                 d1.colsum_part = sg_rows(l, sg_fcb) + (long long)mb * cdiv(R, 128) * 4 * C;
-                gemm_w(TC_FCPROJ_DGRAD, d1, P_FCPROJW, l, true, mb, ms[mb], false, fuse_mx);
+                gemm_w(TC_FCPROJ_DGRAD, d1, P_FCPROJW, l, true, mb, ms[mb], false, fuse_mx, rc ? &dcol[0] : nullptr, EV_RESA);
             }
+            if (rc) wgrad(TC_FCPROJ_WGRAD, rbA, C, a.fchg, 4 * C, G(P_FCPROJW, l), EV_RESA, EV_W1, &dcol[0]);
             // fc: dln2 = dfch . fcw;  fcw += dfch^T . ln2
-            wgrad(TC_FC_WGRAD, dfch, 4 * C, a.ln2, C, G(P_FCW, l), EV_DFCH, EV_W2);
+            wgrad(TC_FC_WGRAD, dfch, 4 * C, a.ln2, C, G(P_FCW, l), EV_DFCH, EV_W2, nullptr, rc ? &c_ln2 : nullptr);
             for (int mb = 0; mb < nmb; mb++) {
                 const long long r0 = mb * R;
                 GemmArgs d2;
@@ -1043,13 +1089,13 @@ struct Trainer {
                 tend();
             }
             // attproj
-            wgrad(TC_PROJ_WGRAD, rbB, C, a.atty, C, G(P_ATTPROJW, l), EV_RESB, EV_W3);
+            if (!rc) wgrad(TC_PROJ_WGRAD, rbB, C, a.atty, C, G(P_ATTPROJW, l), EV_RESB, EV_W3);
             for (int mb = 0; mb < nmb; mb++) {
                 const long long r0 = mb * R;
                 GemmArgs d3;
                 d3.A = rbB + r0 * C; d3.lda = C; dgrad_b(d3, P_ATTPROJW, l, C, C);
                 d3.C = datty + r0 * C; d3.ldc = C; d3.M = (int)R; d3.N = C; d3.K = C; d3.epi = EPI_BF16_STORE;
-                gemm_w(TC_PROJ_DGRAD, d3, P_ATTPROJW, l, true, mb, ms[mb]);
+                gemm_w(TC_PROJ_DGRAD, d3, P_ATTPROJW, l, true, mb, ms[mb], false, false, rc ? &dcol[1] : nullptr, EV_RESB);
                 // attention (+ qkv_b)
                 after_wgrad(EV_W4, ms[mb]);  // the previous layer's qkv wgrad has read dqkv
                 tbeg(TC_ATTN_BWD, 8.0 * Bm * (double)T * T * C, ms[mb]);
@@ -1059,14 +1105,15 @@ struct Trainer {
                                     attn_part + (long long)attn_backward_ws_floats(mb * Bm, T, C, NH), true);
                 tend();
             }
+            if (rc) wgrad(TC_PROJ_WGRAD, rbB, C, a.atty, C, G(P_ATTPROJW, l), EV_RESB, EV_W3, &dcol[1], &c_atty);
             // qkv
-            wgrad(TC_QKV_WGRAD, dqkv, 3 * C, a.ln1, C, G(P_QKVW, l), EV_DQKV, EV_W4);
+            if (!rc) wgrad(TC_QKV_WGRAD, dqkv, 3 * C, a.ln1, C, G(P_QKVW, l), EV_DQKV, EV_W4);
             for (int mb = 0; mb < nmb; mb++) {
                 const long long r0 = mb * R;
                 GemmArgs d4;
                 d4.A = dqkv + r0 * 3 * C; d4.lda = 3 * C; dgrad_b(d4, P_QKVW, l, 3 * C, C);
                 d4.C = dln_bf + r0 * C; d4.ldc = C; d4.M = (int)R; d4.N = C; d4.K = 3 * C; d4.epi = EPI_BF16_STORE;
-                gemm_w(TC_QKV_DGRAD, d4, P_QKVW, l, true, mb, ms[mb]);
+                gemm_w(TC_QKV_DGRAD, d4, P_QKVW, l, true, mb, ms[mb], false, false, rc ? &dcol[2] : nullptr, EV_DQKV);
                 // ln1 backward: dres = dres2 + LN1'(dln1); fcproj_b of layer l-1 += colsum(dres)
                 after_wgrad(EV_W1, ms[mb]);  // this layer's fcproj wgrad has read rbA
                 tbeg(TC_LN_BWD, 0, ms[mb]);
@@ -1076,6 +1123,7 @@ struct Trainer {
                                         sg_rows(l, sg_ln1) + (long long)mb * ln_bwd_blocks(R) * (l > 0 ? 3 : 2) * C);
                 tend();
             }
+            if (rc) wgrad(TC_QKV_WGRAD, dqkv, 3 * C, a.ln1, C, G(P_QKVW, l), EV_DQKV, EV_W4, &dcol[2], &c_ln1);
             sg_finalize(l, R);
             chunk_done(L - l);
         }
