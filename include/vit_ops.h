@@ -219,6 +219,16 @@ void gemm_fp8_fused_mx(void* C, void* C2, long long ldc, const void* aux, long l
                        const uint8_t* a_scale, long long lda, const uint8_t* B, const uint8_t* b_scale,
                        long long ldb, const float* bias, float* colsum_out, int M, int N, int K, int epi,
                        uint8_t* mx_q, uint8_t* mx_s);
+/* gemm_fp8_fused_mx plus the column-wise MX copy of the same output (the weight gradient's
+ * operand): output row m -> token mxc_off + m of mxc_q [N][mxc_ld] + scales mxc_s
+ * (mx_scale_size(N, mxc_ld) bytes), equal byte for byte to quantize_mx_cols_bf16_ex of the bf16
+ * output; M % 64 == 0, N % 64 == 0, mxc_off % 64 == 0.  The MX-copied bf16 output (C2 of epi 4 / 8,
+ * C of epi 6 / 9) may be NULL: not stored. */
+void gemm_fp8_fused_mxc(void* C, void* C2, long long ldc, const void* aux, long long ldaux, const uint8_t* A,
+                        const uint8_t* a_scale, long long lda, const uint8_t* B, const uint8_t* b_scale,
+                        long long ldb, const float* bias, float* colsum_out, int M, int N, int K, int epi,
+                        uint8_t* mx_q, uint8_t* mx_s, uint8_t* mxc_q, uint8_t* mxc_s, long long mxc_ld,
+                        long long mxc_off);
 /* tools: GEMM engine selection (1 = 128x128 everywhere, 2 = production: 256x256 one workgroup per
  * CU with the split-K weight gradients on 256x128, 4 = 256x128 two per CU everywhere) and
  * diagnostics (flag 2: skip epilogues, main-loop timing only) */

@@ -179,6 +179,56 @@ def test_gemm_fp8_fused_mx_output(gpu, M, N, K):
         assert np.array_equal(c0.numpy(), c.numpy())
 
 
+@pytest.mark.parametrize("M,N,K", [(320, 512, 128), (1088, 3072, 192), (256, 1280, 320)])
+def test_gemm_fp8_fused_mx_cols_output(gpu, M, N, K):
+    """The column-wise MX copy the GELU-pair (fc fwd) and product (fcproj dgrad) epilogues write
+    for the weight gradient, at a token offset inside a longer token axis, is byte-identical to
+    quantize_mx_cols_bf16_ex of the bf16 output (M % 128 == 64 exercises the edge-tile path);
+    bytes outside its token range are untouched; and omitting the MX-copied bf16 output (the
+    trainer's fp8 mode) leaves every other output unchanged."""
+    v = gpu
+    rng = np.random.default_rng(M + 3 * N + K)
+    a = rng.normal(size=(M, K)).astype(np.float32)
+    w = (rng.normal(size=(N, K)) * 0.05).astype(np.float32)
+    qa, sa, _, _ = quant_gpu(v, a, "bf16")
+    qw, sw, _, _ = quant_gpu(v, w, "f32")
+    bias = D(v, rng.normal(size=N).astype(np.float32))
+    xb = D(v, v.bf16_bits(rng.normal(size=(M, N)).astype(np.float32)), np.uint16)
+    off, ld = 128, 128 + M + 64
+    nsr, nsc = int(v.lib().mx_scale_size(M, N)), int(v.lib().mx_scale_size(N, ld))
+
+    def run(epi, keep):
+        c, c2 = Z(v, M * N, np.uint16), Z(v, M * N, np.uint16)
+        fq, fs = Z(v, M * N, np.uint8), Z(v, nsr, np.uint8)
+        cq = D(v, np.full(N * ld, 0x5A, np.uint8), np.uint8)
+        cs = D(v, np.full(nsc, 0x5A, np.uint8), np.uint8)
+        if epi == 8:
+            v.call("gemm_fp8_fused_mxc", c, c2 if keep else None, N, None, 0, qa, sa, K, qw, sw, K, bias, None,
+                   M, N, K, epi, fq, fs, cq, cs, ld, off)
+        else:
+            v.call("gemm_fp8_fused_mxc", c if keep else None, None, N, xb, N, qa, sa, K, qw, sw, K, None, None,
+                   M, N, K, epi, fq, fs, cq, cs, ld, off)
+        return c, c2, fq, fs, cq, cs
+
+    for epi in (8, 9):
+        c, c2, fq, fs, cq, cs = run(epi, True)
+        out = c2 if epi == 8 else c
+        rq, rs = Z(v, N * M, np.uint8), Z(v, int(v.lib().mx_scale_size(N, M)), np.uint8)
+        v.call("quantize_mx_cols_bf16_ex", rq, rs, out, M, N, N)
+        got = cq.numpy().reshape(N, ld)
+        assert np.array_equal(got[:, off:off + M], rq.numpy().reshape(N, M)), f"epi {epi}: e4m3 bytes differ"
+        assert (got[:, :off] == 0x5A).all() and (got[:, off + M:] == 0x5A).all()
+        blk = mx.from_lane_native(cs.numpy(), N, ld)
+        assert np.array_equal(blk[:, off // 32:(off + M) // 32], mx.from_lane_native(rs.numpy(), N, M)), \
+            f"epi {epi}: scale bytes differ"
+        c_, c2_, fq_, fs_, cq_, cs_ = run(epi, False)
+        for x, y in ((fq, fq_), (fs, fs_), (cq, cq_), (cs, cs_)):
+            assert np.array_equal(x.numpy(), y.numpy())
+        if epi == 8:  # the GELU' output is still stored; the GELU output was not
+            assert np.array_equal(c.numpy(), c_.numpy())
+            assert not c2_.numpy().any()
+
+
 @pytest.mark.parametrize("R,C", [(1, 64), (100, 128), (197, 768), (4001, 320), (50432 // 8, 1280)])
 def test_quantize_mx_cols_bit_exact(gpu, R, C):
     """Column-wise MX (the fp8 weight gradients' operands: blocks of 32 consecutive tokens) equals

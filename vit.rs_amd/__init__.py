@@ -109,6 +109,7 @@ _SIGS = {
     "quantize_mx_rowcol_bf16_ex": (None, [P, P, P, P, P, LL, I, LL, LL, LL, LL]),
     "gemm_fp8_fused": (None, [P, P, LL, P, LL, P, P, LL, P, P, LL, P, P, I, I, I, I]),
     "gemm_fp8_fused_mx": (None, [P, P, LL, P, LL, P, P, LL, P, P, LL, P, P, I, I, I, I, P, P]),
+    "gemm_fp8_fused_mxc": (None, [P, P, LL, P, LL, P, P, LL, P, P, LL, P, P, I, I, I, I, P, P, P, P, LL, LL]),
     "gemm_bf16_set_variant": (None, [I]), "gemm_bf16_set_debug": (None, [I]),
     "vit_kernel_hits": (I, [P, I]),
     "convert_f32_to_bf16": (None, [P, P, LL]),

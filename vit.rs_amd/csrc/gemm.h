@@ -71,6 +71,16 @@ struct GemmArgs {
     // the bf16 output.
     uint8_t* mx_q = nullptr;
     uint8_t* mx_s = nullptr;
+    // fused column-wise MX copy of the same output (fp8 engine: the weight gradient's operand, MX
+    // blocks of 32 consecutive output rows): output row m -> token mxc_off + m of a [N][mxc_ld]
+    // fp8 matrix + lane-native scales for mx_rows_padded(N) rows; M % 64 == 0, N % 64 == 0,
+    // mxc_off % 64 == 0.  Bit-identical to quantize_mx_cols_bf16 of the bf16 output.  With
+    // mx_q / mxc_q set, the MX-copied bf16 output (C2 of GELU / GELU_D, C of DGELU / MUL) may be
+    // nullptr: not stored.
+    uint8_t* mxc_q = nullptr;
+    uint8_t* mxc_s = nullptr;
+    long long mxc_ld = 0;
+    long long mxc_off = 0;
 };
 
 // fp32 operands, exact-fp32 MFMA (v_mfma_f32_16x16x4_f32); any shape/stride. Parity path.

@@ -873,6 +873,11 @@ GemmParams make_gemm_params(const GemmArgs& a, int kchunk) {
     p.mx_q = a.mx_q;
     p.mx_s = a.mx_s;
     p.mx_rg = (int)(mx_rows_padded(a.M) / 32);
+    p.mxc_q = a.mxc_q;
+    p.mxc_s = a.mxc_s;
+    p.mxc_ld = a.mxc_ld;
+    p.mxc_off = (int)a.mxc_off;
+    p.mxc_rg = (int)(mx_rows_padded(a.N) / 32);
     p.tiles = 1;
     return p;
 }
@@ -922,7 +927,7 @@ void slab_reduce(const GemmArgs& a, float* slab, int split, hipStream_t s) {
 
 void gemm_f32(const GemmArgs& a, hipStream_t s) {
     if (a.M <= 0 || a.N <= 0) return;
-    if (a.mx_q) {
+    if (a.mx_q || a.mxc_q) {
         set_error("gemm_f32: the fused MX output is an fp8-engine feature");
         return;
     }
@@ -1080,7 +1085,7 @@ static void gemm_bf16_g4(const GemmArgs& a, hipStream_t s) {
 
 void gemm_bf16(const GemmArgs& a, hipStream_t s) {
     if (a.M <= 0 || a.N <= 0) return;
-    if (a.mx_q) {
+    if (a.mx_q || a.mxc_q) {
         set_error("gemm_bf16: the fused MX output is an fp8-engine feature");
         return;
     }

@@ -22,6 +22,10 @@ struct GemmParams {
     uint8_t* mx_q;  // fused MX output (GemmArgs::mx_q / mx_s); mx_rg = padded rows / 32
     uint8_t* mx_s;
     int mx_rg;
+    uint8_t* mxc_q;  // fused column-wise MX output (GemmArgs::mxc_*); mxc_rg = padded N / 32
+    uint8_t* mxc_s;
+    long long mxc_ld;
+    int mxc_off, mxc_rg;
 };
 
 // E8M0 scale byte of an MX block: X + 127 with X = ceil(log2(amax / 448)) (no element overflows
@@ -60,6 +64,16 @@ __device__ __forceinline__ void mx_out8(const GemmParams& p, int m, int n, uint3
     int t1 = __builtin_amdgcn_cvt_pk_fp8_f32(v[4] * inv, v[5] * inv, 0, false);
     t1 = __builtin_amdgcn_cvt_pk_fp8_f32(v[6] * inv, v[7] * inv, t1, true);
     *reinterpret_cast<uint2*>(p.mx_q + (long long)m * p.N + n) = make_uint2((uint32_t)t0, (uint32_t)t1);
+}
+
+// the 8 bf16 values (packed as stored) back into the wave's staging rows as fp32, for the
+// column-wise MX pass (mx_cols_pass)
+__device__ __forceinline__ void stage_back8(float* w, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<f4*>(w) = f4{__uint_as_float(w0 << 16), __uint_as_float(w0 & 0xffff0000u),
+                                   __uint_as_float(w1 << 16), __uint_as_float(w1 & 0xffff0000u)};
+    *reinterpret_cast<f4*>(w + 4) = f4{__uint_as_float(w2 << 16), __uint_as_float(w2 & 0xffff0000u),
+                                       __uint_as_float(w3 << 16), __uint_as_float(w3 & 0xffff0000u)};
 }
 
 // host: the partial-row buffer of an aux epilogue's column sums (colsum_part or the thread
@@ -173,7 +187,7 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, int m, int n, f32x
 // the column sums of the DGELU output (fused bias gradient).
 template <int EPI>
 __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, float (&v)[8],
-                                          float (&cs)[8], int lane = 0) {
+                                          float (&cs)[8], int lane = 0, float* wb = nullptr) {
     if constexpr (epi_bias(EPI)) {
         if (p.bias) {
             const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
@@ -210,8 +224,9 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, flo
         for (int j = 0; j < 8; j++) gv[j] = gelu_fast_f(v[j]);
         *reinterpret_cast<uint4*>((bf16_t*)p.C + off) = pack8(v);
         const uint4 g8 = pack8(gv);
-        *reinterpret_cast<uint4*>((bf16_t*)p.C2 + off) = g8;
+        if (p.C2) *reinterpret_cast<uint4*>((bf16_t*)p.C2 + off) = g8;
         if (p.mx_q) mx_out8(p, m, n, g8.x, g8.y, g8.z, g8.w, lane);
+        if (wb) stage_back8(wb, g8.x, g8.y, g8.z, g8.w);
     } else if constexpr (EPI == EPI_F32_RESID) {
         const float* r = (const float*)p.aux + (long long)m * p.ldaux + n;
         const float4 r0 = reinterpret_cast<const float4*>(r)[0];
@@ -225,8 +240,9 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, flo
         for (int j = 0; j < 8; j++) gelu_pair_fast_f(v[j], gv[j], dv[j]);
         *reinterpret_cast<uint4*>((bf16_t*)p.C + off) = pack8(dv);
         const uint4 g8 = pack8(gv);
-        *reinterpret_cast<uint4*>((bf16_t*)p.C2 + off) = g8;
+        if (p.C2) *reinterpret_cast<uint4*>((bf16_t*)p.C2 + off) = g8;
         if (p.mx_q) mx_out8(p, m, n, g8.x, g8.y, g8.z, g8.w, lane);
+        if (wb) stage_back8(wb, g8.x, g8.y, g8.z, g8.w);
     } else if constexpr (epi_aux16(EPI)) {
         const uint4 h = *reinterpret_cast<const uint4*>((const bf16_t*)p.aux + (long long)m * p.ldaux + n);
         const uint32_t hw[4] = {h.x, h.y, h.z, h.w};
@@ -244,8 +260,9 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, flo
 #pragma unroll
         for (int j = 0; j < 8; j++) cs[j] += v[j];
         const uint4 d8 = pack8(v);
-        *reinterpret_cast<uint4*>((bf16_t*)p.C + off) = d8;
+        if (p.C) *reinterpret_cast<uint4*>((bf16_t*)p.C + off) = d8;
         if (p.mx_q) mx_out8(p, m, n, d8.x, d8.y, d8.z, d8.w, lane);
+        if (wb) stage_back8(wb, d8.x, d8.y, d8.z, d8.w);
     }
 }
 
@@ -348,16 +365,18 @@ __device__ __forceinline__ void staged_pass_interior(const GemmParams& p, const 
             for (int j = 0; j < 8; j++) gv[j] = gelu_fast_f(v[j]);
             epi_st16(p, (bf16_t*)p.C + off, pack8(v));
             const u32x4 g8 = pack8(gv);
-            epi_st16(p, (bf16_t*)p.C2 + off, g8);
+            if (p.C2) epi_st16(p, (bf16_t*)p.C2 + off, g8);
             if (p.mx_q) mx_out8(p, mrow + r, n, g8[0], g8[1], g8[2], g8[3], cc_lane);
+            if (p.mxc_q) stage_back8(const_cast<float*>(st) + r * STG_LD + cc, g8[0], g8[1], g8[2], g8[3]);
         } else if constexpr (EPI == EPI_BF16_GELU_D) {
             float gv[8], dv[8];
 #pragma unroll
             for (int j = 0; j < 8; j++) gelu_pair_fast_f(v[j], gv[j], dv[j]);
             epi_st16(p, (bf16_t*)p.C + off, pack8(dv));
             const u32x4 g8 = pack8(gv);
-            epi_st16(p, (bf16_t*)p.C2 + off, g8);
+            if (p.C2) epi_st16(p, (bf16_t*)p.C2 + off, g8);
             if (p.mx_q) mx_out8(p, mrow + r, n, g8[0], g8[1], g8[2], g8[3], cc_lane);
+            if (p.mxc_q) stage_back8(const_cast<float*>(st) + r * STG_LD + cc, g8[0], g8[1], g8[2], g8[3]);
         } else if constexpr (AUX16) {
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -373,8 +392,9 @@ __device__ __forceinline__ void staged_pass_interior(const GemmParams& p, const 
 #pragma unroll
             for (int j = 0; j < 8; j++) cs[j] += v[j];
             const u32x4 d8 = pack8(v);
-            epi_st16(p, (bf16_t*)p.C + off, d8);
+            if (p.C) epi_st16(p, (bf16_t*)p.C + off, d8);
             if (p.mx_q) mx_out8(p, mrow + r, n, d8[0], d8[1], d8[2], d8[3], cc_lane);
+            if (p.mxc_q) stage_back8(const_cast<float*>(st) + r * STG_LD + cc, d8[0], d8[1], d8[2], d8[3]);
         }
     }
 }
@@ -403,7 +423,8 @@ __device__ __forceinline__ void staged_pass(const GemmParams& p, const float* st
         const int m = m0 + pass * 64 + r, n = n0 + cc;
         if (m >= p.M) continue;
         if (n + 8 <= p.N) {
-            epilogue8<EPI>(p, m, n, v, cs, lane);
+            epilogue8<EPI>(p, m, n, v, cs, lane,
+                           epi_mx(EPI) && p.mxc_q ? const_cast<float*>(st) + r * STG_LD + cc : nullptr);
         } else if (n + 4 <= p.N) {  // ragged N (N % 8 == 4): the 4-wide form
             f32x4_t t = lo;
             epilogue<EPI>(p, m, n, t);
@@ -414,6 +435,39 @@ __device__ __forceinline__ void staged_pass(const GemmParams& p, const float* st
                 cs[3] += t[3];
             }
         }
+    }
+}
+// column-wise MX of one 64-row pass whose bf16 outputs stage_back8 left in `st` (the fp8 engine,
+// GemmArgs::mxc_q): lane c takes column n0 + c, two 32-row blocks (a wave reads one staging row
+// per step: conflict free), and writes 32 e4m3 bytes of the column's token run + the block's
+// scale byte (as quantize_mx_cols_k).  M % 64 == 0 (host): a pass is wholly inside or outside M.
+__device__ __forceinline__ void mx_cols_pass(const GemmParams& p, const float* st, int lane, int mrow, int n0) {
+    if (mrow >= p.M) return;
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const int c = n0 + lane;
+#pragma unroll
+    for (int b = 0; b < 2; b++) {
+        float v[32];
+        float amax = 0.f;
+#pragma unroll
+        for (int i = 0; i < 32; i++) {
+            v[i] = st[(32 * b + i) * STG_LD + lane];
+            amax = fmaxf(amax, fabsf(v[i]));
+        }
+        const int sb = mx_scale_byte(amax);
+        const int tok = p.mxc_off + mrow + 32 * b, kb = tok >> 5;
+        p.mxc_s[((long long)(kb >> 1) * p.mxc_rg + (c >> 5)) * 64 + (kb & 1) * 32 + (c & 31)] = (uint8_t)sb;
+        const float inv = __uint_as_float((uint32_t)(254 - sb) << 23);
+        uint32_t w[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            int t = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * j] * inv, v[4 * j + 1] * inv, 0, false);
+            t = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * j + 2] * inv, v[4 * j + 3] * inv, t, true);
+            w[j] = (uint32_t)t;
+        }
+        uint8_t* dst = p.mxc_q + (long long)c * p.mxc_ld + tok;
+        *reinterpret_cast<u32x4*>(dst) = u32x4{w[0], w[1], w[2], w[3]};
+        *reinterpret_cast<u32x4*>(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
     }
 }
 template <int EPI>

@@ -237,6 +237,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(F8Params fp) {
                         f32x4_t{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
                 }
         staged_pass<EPI>(p, st, lane, m0, n0, pass, interior, cs);
+        if constexpr (epi_mx(EPI)) {
+            if (p.mxc_q) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                mx_cols_pass(p, st, lane, m0 + pass * 64, n0);
+            }
+        }
     }
     staged_colsum<EPI>(p, lane, m0, n0, cs);
 }
@@ -449,7 +455,12 @@ bool gemm_fp8_supported(const GemmArgs& a) {
            a.N % 4 == 0 && a.ldc % 4 == 0 && al16(a.A) && al16(a.B) && a.a_scale && a.b_scale &&
            a.epi != EPI_F32_SLAB && (a.epi != EPI_F32_ATOMIC || a.N % 4 == 0) &&
            // fused MX output: whole 32-column blocks, GELU/GELU'/product epilogues only (4 lanes per block)
-           (!a.mx_q || (a.mx_s && a.N % 32 == 0 && epi_mx(a.epi)));
+           (!a.mx_q || (a.mx_s && a.N % 32 == 0 && epi_mx(a.epi))) &&
+           (!a.mxc_q || (a.mxc_s && epi_mx(a.epi) && a.M % 64 == 0 && a.N % 64 == 0 && a.mxc_off % 64 == 0 &&
+                         a.mxc_off >= 0 && a.mxc_ld % 16 == 0 && a.mxc_off + a.M <= a.mxc_ld && al16(a.mxc_q))) &&
+           // an omitted bf16 output needs an MX copy in its place
+           (a.C2 || !(a.epi == EPI_BF16_GELU || a.epi == EPI_BF16_GELU_D) || a.mx_q || a.mxc_q) &&
+           (a.C || !epi_aux16(a.epi) || a.mx_q || a.mxc_q);
 }
 
 void gemm_fp8(const GemmArgs& a, hipStream_t s) {
@@ -607,6 +618,19 @@ void gemm_fp8_fused_mx(void* C, void* C2, long long ldc, const void* aux, long l
         set_error("gemm_fp8_fused_mx: the MX output needs epi 4 / 8 (GELU pairs) or 6 / 9 (GELU', product)");
         return;
     }
+    gemm_fp8(a, stream());
+}
+void gemm_fp8_fused_mxc(void* C, void* C2, long long ldc, const void* aux, long long ldaux, const uint8_t* A,
+                        const uint8_t* a_scale, long long lda, const uint8_t* B, const uint8_t* b_scale,
+                        long long ldb, const float* bias, float* colsum_out, int M, int N, int K, int epi,
+                        uint8_t* mx_q, uint8_t* mx_s, uint8_t* mxc_q, uint8_t* mxc_s, long long mxc_ld,
+                        long long mxc_off) {
+    GemmArgs a;
+    a.C = C; a.C2 = C2; a.ldc = ldc; a.aux = aux; a.ldaux = ldaux;
+    a.A = A; a.a_scale = a_scale; a.lda = lda; a.B = B; a.b_scale = b_scale; a.ldb = ldb;
+    a.bias = bias; a.colsum_out = colsum_out; a.M = M; a.N = N; a.K = K; a.epi = epi;
+    a.mx_q = mx_q; a.mx_s = mx_s;
+    a.mxc_q = mxc_q; a.mxc_s = mxc_s; a.mxc_ld = mxc_ld; a.mxc_off = mxc_off;
     gemm_fp8(a, stream());
 }
 void gemm_fp8_fused(void* C, void* C2, long long ldc, const void* aux, long long ldaux, const uint8_t* A,

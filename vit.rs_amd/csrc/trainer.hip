@@ -372,7 +372,15 @@ struct Trainer {
     bool rowcol_ok = false;
     long long kp_tok = 0;  // mx_cols_kp(B*T)
     QMat actc[3], dcol[3];
+    // ... and of the 4C-wide GELU output (fc fwd epilogue, per layer) and its gradient dfch (fcproj
+    // dgrad epilogue): with those and the row forms fused too (fuse_mx), neither bf16 tensor is
+    // stored (GemmArgs::mxc_q; nothing else reads them in fp8 mode)
+    QMat fchgc, dfchc;
     bool rowcol_on() const { return fp8() && rowcol_ok && ((long long)(B / nmb) * T) % 64 == 0; }
+    bool epicol_on() const { return rowcol_on() && fuse_mx && (4 * C) % 64 == 0; }
+    QMat fchgc_of(int l) const {
+        return {fchgc.q + (long long)l * 4 * C * kp_tok, fchgc.s + (long long)l * mx_scale_bytes(4LL * C, (int)kp_tok)};
+    }
     QMat actc_of(int k, int l) const {
         return {actc[k].q + (long long)l * C * kp_tok, actc[k].s + (long long)l * mx_scale_bytes(C, (int)kp_tok)};
     }
@@ -670,6 +678,10 @@ struct Trainer {
                             dcol[k].q = alloc<uint8_t>(w * kp);
                             dcol[k].s = alloc<uint8_t>((long long)mx_scale_bytes(w, (int)kp));
                         }
+                        fchgc.q = alloc<uint8_t>((long long)L * 4 * C * kp);
+                        fchgc.s = alloc<uint8_t>((long long)L * mx_scale_bytes(4LL * C, (int)kp));
+                        dfchc.q = alloc<uint8_t>(4LL * C * kp);
+                        dfchc.s = alloc<uint8_t>((long long)mx_scale_bytes(4LL * C, (int)kp));
                     }
                 }
             }
@@ -943,6 +955,11 @@ struct Trainer {
                 f.A = a.ln2 + r0 * C; f.lda = C; f.B = W(P_FCW, l); f.ldb = C; f.C = a.fchd + r0 * 4 * C;
                 f.C2 = a.fchg + r0 * 4 * C; f.ldc = 4 * C; f.bias = P(P_FCB, l); f.M = (int)R; f.N = 4 * C;
                 f.K = C; f.epi = EPI_BF16_GELU_D;
+                if (epicol_on()) {  // the GELU output only as its row (mx_out) and column MX forms
+                    const QMat g = fchgc_of(l);
+                    f.C2 = nullptr;
+                    f.mxc_q = g.q; f.mxc_s = g.s; f.mxc_ld = kp_tok; f.mxc_off = r0;
+                }
                 gemm_w(TC_FC_FWD, f, P_FCW, l, false, mb, st, false, fuse_mx, rc ? &c_ln2 : nullptr);
                 GemmArgs fp;
                 fp.A = a.fchg + r0 * 4 * C; fp.lda = 4 * C; fp.B = W(P_FCPROJW, l); fp.ldb = 4 * C;
@@ -1059,6 +1076,8 @@ struct Trainer {
             const bool rc = rowcol_on();
             QMat c_ln1 = rc ? actc_of(0, l) : QMat{}, c_atty = rc ? actc_of(1, l) : QMat{}, c_ln2 = rc ? actc_of(2, l) : QMat{};
             // fcproj: dfch = (dres3 . fcprojw) * gelu'(fch) (stored as fchd);  fcprojw += dres3^T . fchg
+            const bool ec = epicol_on();
+            QMat c_fchg = ec ? fchgc_of(l) : QMat{};
             if (!rc) wgrad(TC_FCPROJ_WGRAD, rbA, C, a.fchg, 4 * C, G(P_FCPROJW, l), EV_RESA, EV_W1);
             for (int mb = 0; mb < nmb; mb++) {
                 const long long r0 = mb * R;
@@ -1068,11 +1087,18 @@ struct Trainer {
                 d1.C = dfch + r0 * 4 * C; d1.ldc = 4 * C; d1.aux = a.fchd + r0 * 4 * C; d1.ldaux = 4 * C;
                 d1.M = (int)R; d1.N = 4 * C; d1.K = C; d1.epi = EPI_BF16_MUL;
                 d1.colsum_part = sg_rows(l, sg_fcb) + (long long)mb * cdiv(R, 128) * 4 * C;
+                if (ec) {  // dfch only as its row (mx_out) and column MX forms
+                    d1.C = nullptr;
+                    d1.mxc_q = dfchc.q; d1.mxc_s = dfchc.s; d1.mxc_ld = kp_tok; d1.mxc_off = r0;
+                }
                 gemm_w(TC_FCPROJ_DGRAD, d1, P_FCPROJW, l, true, mb, ms[mb], false, fuse_mx, rc ? &dcol[0] : nullptr, EV_RESA);
+                if (ec && two_streams) VIT_HIP(hipEventRecord(mev[mb][EV_DFCH], ms[mb]));  // dfchc final
             }
-            if (rc) wgrad(TC_FCPROJ_WGRAD, rbA, C, a.fchg, 4 * C, G(P_FCPROJW, l), EV_RESA, EV_W1, &dcol[0]);
+            if (rc) wgrad(TC_FCPROJ_WGRAD, rbA, C, a.fchg, 4 * C, G(P_FCPROJW, l), EV_RESA, EV_W1, &dcol[0],
+                          ec ? &c_fchg : nullptr);
             // fc: dln2 = dfch . fcw;  fcw += dfch^T . ln2
-            wgrad(TC_FC_WGRAD, dfch, 4 * C, a.ln2, C, G(P_FCW, l), EV_DFCH, EV_W2, nullptr, rc ? &c_ln2 : nullptr);
+            wgrad(TC_FC_WGRAD, dfch, 4 * C, a.ln2, C, G(P_FCW, l), EV_DFCH, EV_W2, ec ? &dfchc : nullptr,
+                  rc ? &c_ln2 : nullptr);
             for (int mb = 0; mb < nmb; mb++) {
                 const long long r0 = mb * R;
                 GemmArgs d2;
