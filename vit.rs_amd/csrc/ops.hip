@@ -437,6 +437,30 @@ __global__ void im2col_vec_k(TO* __restrict__ out, const float* __restrict__ px,
         }
     }
 }
+// the same into rows of KPP columns (zeros past K = 3*P*P), 8 columns (one 16-B store) per thread
+__global__ void im2col_pad_k(bf16_t* __restrict__ out, const float* __restrict__ px, int B, int IMG, int P, int KPP) {
+    const int gw = IMG / P, NP = gw * gw, K = 3 * P * P, K8 = KPP / 8, PP = P * P;
+    const long long n = (long long)B * NP * K8;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < n;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const long long row = idx / K8;
+        const int k0 = (int)(idx - row * K8) * 8;
+        const int b = (int)(row / NP), p = (int)(row - (long long)b * NP);
+        const int y0 = (p / gw) * P, x0 = (p % gw) * P;
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int k = k0 + j;
+            v[j] = 0.f;
+            if (k < K) {
+                const int c = k / PP, r = k - c * PP, kh = r / P, kw = r - kh * P;
+                v[j] = px[(((long long)b * 3 + c) * IMG + y0 + kh) * IMG + x0 + kw];
+            }
+        }
+        *reinterpret_cast<uint4*>(out + row * KPP + k0) =
+            make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+    }
+}
 // encoded[b,0] = cls + wpe[0]; encoded[b,1+p] = emb[b*NP+p] + wpe[1+p]
 __global__ void patch_assemble_k(float* __restrict__ enc, const float* __restrict__ emb,
                                  const float* __restrict__ cls, const float* __restrict__ wpe,
@@ -761,6 +785,15 @@ void im2col_f32(float* out, const float* px, int B, int IMG, int P, hipStream_t 
 void im2col_bf16(bf16_t* out, const float* px, int B, int IMG, int P, hipStream_t s) {
     im2col_any<bf16_t>(out, px, B, IMG, P, s);
     after_launch("im2col_bf16");
+}
+void im2col_pad_bf16(bf16_t* out, const float* px, int B, int IMG, int P, int KPP, hipStream_t s) {
+    const long long n = (long long)B * (IMG / P) * (IMG / P) * (KPP / 8);
+    if (KPP % 8 || KPP < 3 * P * P || !al16(out)) {
+        set_error("im2col_pad_bf16: KPP %% 8 == 0, KPP >= 3*P*P and a 16-B aligned output required (KPP=%d)", KPP);
+        return;
+    }
+    im2col_pad_k<<<grid_for(n, 256), 256, 0, s>>>(out, px, B, IMG, P, KPP);
+    after_launch("im2col_pad_bf16");
 }
 void patch_assemble(float* enc, const float* emb, const float* cls, const float* wpe, int B,
                     int NP, int C, hipStream_t s) {

@@ -34,6 +34,9 @@ void ce_backward(float* dlogits, const float* dlosses, const float* probs, const
                  long long rows, int V, hipStream_t s);
 void im2col_f32(float* out, const float* px, int B, int IMG, int P, hipStream_t s);
 void im2col_bf16(bf16_t* out, const float* px, int B, int IMG, int P, hipStream_t s);
+// rows padded to KPP columns (zeros past 3*P*P; KPP % 8 == 0): the bf16 GEMM operand of a patch
+// whose 3*P*P is not a multiple of 8 (ViT-H/14: 588 -> 640)
+void im2col_pad_bf16(bf16_t* out, const float* px, int B, int IMG, int P, int KPP, hipStream_t s);
 void patch_assemble(float* enc, const float* emb, const float* cls, const float* wpe, int B,
                     int NP, int C, hipStream_t s);
 // out[c][r] = in[r][c] for `count` R x Cc bf16 matrices `stride` elements apart (in and out)

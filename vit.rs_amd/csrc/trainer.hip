@@ -61,6 +61,14 @@ __global__ void rows_to_bf16_k(bf16_t* __restrict__ out, uint8_t* __restrict__ l
     out[o] = h;
     lo[o] = (uint8_t)lo8_encode(in[i], bf2f(h));
 }
+// dst [rows][n] += src [rows][lds] (its first n columns)
+__global__ void add_cols_k(float* __restrict__ dst, const float* __restrict__ src, int rows, int n, int lds) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < (long long)rows * n;
+         i += (long long)gridDim.x * blockDim.x) {
+        const long long r = i / n;
+        dst[i] += src[r * lds + (i - r * n)];
+    }
+}
 __global__ void fill_k(float* p, float v, int n) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) p[i] = v;
@@ -278,7 +286,15 @@ struct Trainer {
     };
     std::vector<LayerActs> la;
     float* encoded = nullptr;
-    bool patch_f32 = false;  // bf16 mode, KP % 8 != 0: patch embedding on the fp32 GEMM
+    bool patch_f32 = false;  // bf16 mode, KP % 8 != 0 and VIT_PATCH_PAD=0: patch embedding on the fp32 GEMM
+    // bf16 / fp8 mode, KP % 8 != 0 (ViT-H/14: 588): the patch GEMMs run on the bf16 engine over
+    // KPP = KP rounded up to 64 columns: zero-padded im2col rows, a zero-padded bf16 weight copy
+    // (refreshed with the transposed copies) and a padded fp32 weight-gradient scratch whose first
+    // KP columns are added to the gradient arena
+    bool patch_pad = false;
+    int KPP = 0;
+    bf16_t* wpatch_pad = nullptr;
+    float* dwpatch_pad = nullptr;
     bf16_t* patches_bf = nullptr;
     float* patches_f = nullptr;
     float* emb_tmp = nullptr;
@@ -584,16 +600,24 @@ struct Trainer {
                 return false;
             }
             // a patch whose im2col row (3*P*P) is not a multiple of 8 bf16 (ViT-H/14: 588) cannot
-            // feed the bf16 GEMM's 16-B loads: the patch embedding then runs on the fp32 GEMM
-            // (0.2 % of the step's flops) from the fp32 master weights
-            patch_f32 = KP % 8 != 0;
+            // feed the bf16 GEMM's 16-B loads as it is: padded to KPP columns (the fp32 GEMM from
+            // the fp32 master weights with VIT_PATCH_PAD=0, the round-2 form: 3 ms/step at H/14)
+            const char* pp = getenv("VIT_PATCH_PAD");
+            patch_f32 = KP % 8 != 0 && pp && pp[0] == '0';
+            patch_pad = KP % 8 != 0 && !patch_f32;
+            KPP = patch_pad ? (KP + 63) / 64 * 64 : KP;
             pbf = alloc<bf16_t>(arena_elems);
             pbfT = alloc<bf16_t>(arena_elems);
             if (patch_f32) {
                 patches_f = alloc<float>((long long)B * NP * KP);
                 dpatch_f = alloc<float>((long long)B * NP * C);
             } else {
-                patches_bf = alloc<bf16_t>((long long)B * NP * KP);
+                patches_bf = alloc<bf16_t>((long long)B * NP * KPP);
+            }
+            if (patch_pad) {
+                wpatch_pad = alloc<bf16_t>((long long)C * KPP);
+                dwpatch_pad = alloc<float>((long long)C * KPP);
+                if (wpatch_pad) VIT_HIP(hipMemset(wpatch_pad, 0, (size_t)C * KPP * 2));
             }
             for (int l = 0; l < L; l++) {
                 LayerActs& a = la[l];
@@ -774,6 +798,9 @@ struct Trainer {
             const int l0 = stride < 0 ? L - 1 : 0;
             transpose_bf16(WT(kinds[k], l0), W(kinds[k], l0), rows[k], cols[k], L, stride < 0 ? -stride : stride, s);
         }
+        if (patch_pad)  // the patch weight's padded copy (columns KP .. KPP-1 stay zero)
+            VIT_HIP(hipMemcpy2DAsync(wpatch_pad, (size_t)KPP * 2, W(P_PATCH_W), (size_t)KP * 2, (size_t)KP * 2, C,
+                                     hipMemcpyDeviceToDevice, s));
         tend();
         if (fp8()) refresh_fp8();
     }
@@ -912,6 +939,11 @@ struct Trainer {
                            cfg.patch, st);
                 a.A = patches_f + img0 * NP * KP; a.lda = KP; a.B = P(P_PATCH_W); a.ldb = KP;
                 gemm_f32(a, st);
+            } else if (patch_pad) {
+                im2col_pad_bf16(patches_bf + img0 * NP * KPP, pixels + img0 * 3 * cfg.img * cfg.img, Bm, cfg.img,
+                                cfg.patch, KPP, st);
+                a.A = patches_bf + img0 * NP * KPP; a.lda = KPP; a.B = wpatch_pad; a.ldb = KPP; a.K = KPP;
+                gemm_bf16(a, st);
             } else {
                 im2col_bf16(patches_bf + img0 * NP * KP, pixels + img0 * 3 * cfg.img * cfg.img, Bm, cfg.img,
                             cfg.patch, st);
@@ -1170,10 +1202,16 @@ struct Trainer {
             patch_gather_bf16(dpatch_bf, rbA, B, NP, C, s);
             GemmArgs w;
             w.A = dpatch_bf; w.lda = C; w.a_kcontig = false;
-            w.B = patches_bf; w.ldb = KP; w.b_kcontig = false;
+            w.B = patches_bf; w.ldb = KPP; w.b_kcontig = false;
             w.C = G(P_PATCH_W); w.ldc = KP; w.M = C; w.N = KP; w.K = B * NP; w.epi = EPI_F32_ATOMIC;
             w.ws = gemm_ws; w.ws_bytes = gemm_ws_bytes;
+            if (patch_pad) {  // dW over KPP columns into the scratch, then its first KP columns into G
+                VIT_HIP(hipMemsetAsync(dwpatch_pad, 0, (size_t)C * KPP * 4, s));
+                w.C = dwpatch_pad; w.ldc = KPP; w.N = KPP;
+            }
             gemm_bf16(w, s);
+            if (patch_pad)
+                add_cols_k<<<grid_for((long long)C * KP, 256), 256, 0, s>>>(G(P_PATCH_W), dwpatch_pad, C, KP, KPP);
         }
         patch_small_grads(G(P_CLS), G(P_WPE), G(P_PATCH_B), rbA, loA, B, T, C, s, pos_sums, psg_part);
         tend();
