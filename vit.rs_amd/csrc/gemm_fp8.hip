@@ -373,17 +373,20 @@ __global__ __launch_bounds__(TOK * 2) void quantize_mx_cols_k(uint8_t* __restric
 // [tok_off, tok_off + ntok) of a [C][ldqc] matrix (one micro-batch of a larger token axis;
 // tok_off % 64 == 0, tokens R .. ntok-1 are zero padding); the row form is [R][C] with its own
 // Rpad (grid.x = Rpad / TOK covers the padding rows' zero scales).
-template <int TOK>
-__global__ __launch_bounds__(TOK * 2) void quantize_mx_rowcol_k(uint8_t* __restrict__ qr, uint8_t* __restrict__ slr,
+// COLS = 128: two column groups per workgroup (8 waves), so every token row's row-form bytes
+// leave as one full 128-B line (64 columns wrote half lines from two workgroups far apart).
+template <int TOK, int COLS>
+__global__ __launch_bounds__(TOK * 2 * (COLS / 64)) void quantize_mx_rowcol_k(uint8_t* __restrict__ qr, uint8_t* __restrict__ slr,
                                                                uint8_t* __restrict__ qc, uint8_t* __restrict__ slc,
                                                                const uint16_t* __restrict__ x, int R, int C,
                                                                long long ldx, int rgr_tot, long long ldqc, int tok_off,
                                                                int ntok, int rgc_tot) {
-    constexpr int NT = TOK * 2;
-    __shared__ __attribute__((aligned(16))) uint16_t tile[TOK * 64];
-    const int tok0 = blockIdx.x * TOK, col0 = blockIdx.y * 64;
+    constexpr int NT = TOK * 2 * (COLS / 64), G8 = COLS / 8;
+    __shared__ __attribute__((aligned(16))) uint16_t tile[TOK * COLS];
+    const int tok0 = blockIdx.x * TOK, col0 = blockIdx.y * COLS;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int c = col0 + lane, tb = tok0 + 32 * wave;
+    const int cg = wave / (TOK / 32);  // the column phase: wave -> (64-column group, token block)
+    const int c = col0 + 64 * cg + lane, tb = tok0 + 32 * (wave % (TOK / 32));
     if (col0 >= C) {  // padding rows of the column form's scale layout
         if (tb < ntok) {
             const int kb = (tok_off + tb) >> 5;
@@ -392,11 +395,11 @@ __global__ __launch_bounds__(TOK * 2) void quantize_mx_rowcol_k(uint8_t* __restr
         return;
     }
 #pragma unroll
-    for (int i = 0; i < TOK * 8 / NT; i++) {
-        const int idx = i * NT + tid, row = idx >> 3, ch = idx & 7, tok = tok0 + row;
+    for (int i = 0; i < TOK * G8 / NT; i++) {
+        const int idx = i * NT + tid, row = idx / G8, ch = idx % G8, tok = tok0 + row;
         u32x4 w = u32x4{0u, 0u, 0u, 0u};
         if (tok < R) w = *reinterpret_cast<const u32x4*>(x + (long long)tok * ldx + col0 + ch * 8);
-        *reinterpret_cast<u32x4*>(tile + row * 64 + ch * 8) = w;
+        *reinterpret_cast<u32x4*>(tile + row * COLS + ch * 8) = w;
         float v[8];
         float amax = 0.f;
 #pragma unroll
@@ -427,7 +430,7 @@ __global__ __launch_bounds__(TOK * 2) void quantize_mx_rowcol_k(uint8_t* __restr
     float amax = 0.f;
 #pragma unroll
     for (int i = 0; i < 32; i++) {
-        v[i] = __uint_as_float((uint32_t)tile[(32 * wave + i) * 64 + lane] << 16);
+        v[i] = __uint_as_float((uint32_t)tile[(tb - tok0 + i) * COLS + 64 * cg + lane] << 16);
         amax = fmaxf(amax, fabsf(v[i]));
     }
     const int sb = mx_scale_byte(amax), kb = (tok_off + tb) >> 5;
@@ -568,8 +571,19 @@ bool quantize_mx_rowcol_bf16(uint8_t* qr, uint8_t* slr, uint8_t* qc, uint8_t* sl
     }
     const long long rp = mx_rows_padded(R);
     const int cpad = (int)mx_rows_padded(C);
-    f8::quantize_mx_rowcol_k<128><<<dim3((unsigned)(rp / 128), cpad / 64), 256, 0, s>>>(
-        qr, slr, qc, slc, (const uint16_t*)x, (int)R, C, ldx, (int)(rp / 32), ldqc, (int)tok_off, (int)ntok, cpad / 32);
+    // 128 columns from C = 2048 (ViT-H/14 micro-batch, tools/bench_quant.py: 3840 columns 64 -> 50 us,
+    // 5120: 88 -> 78 us; 1280: 17.0 vs 17.5 us, kept at 64); VIT_ROWCOL_COLS=64|128 forces one
+    static const int force = [] {
+        const char* e = getenv("VIT_ROWCOL_COLS");
+        return e ? atoi(e) : 0;
+    }();
+    const int cols = force == 64 || force == 128 ? force : (C >= 2048 ? 128 : 64);
+    if (cols == 128 && C % 128 == 0)
+        f8::quantize_mx_rowcol_k<128, 128><<<dim3((unsigned)(rp / 128), cpad / 128), 512, 0, s>>>(
+            qr, slr, qc, slc, (const uint16_t*)x, (int)R, C, ldx, (int)(rp / 32), ldqc, (int)tok_off, (int)ntok, cpad / 32);
+    else
+        f8::quantize_mx_rowcol_k<128, 64><<<dim3((unsigned)(rp / 128), cpad / 64), 256, 0, s>>>(
+            qr, slr, qc, slc, (const uint16_t*)x, (int)R, C, ldx, (int)(rp / 32), ldqc, (int)tok_off, (int)ntok, cpad / 32);
     after_launch("quantize_mx_rowcol");
     count_hit(VIT_HIT_QUANT_ROWCOL);
     return true;
