@@ -254,7 +254,7 @@ def test_quantize_mx_cols_bit_exact(gpu, R, C):
 
 
 @pytest.mark.parametrize("R,C,parts", [(100, 128, 1), (197, 768, 1), (4001, 320, 1), (2 * 257 * 16, 1280, 2),
-                                        (3 * 1024 + 70, 192, 3)])
+                                        (3 * 1024 + 70, 192, 3), (1000, 2304, 2), (300, 3840, 1)])
 def test_quantize_mx_rowcol_bit_exact(gpu, R, C, parts):
     """The fused row+column quantizer (the fp8 trainer's ln1 / atty / ln2 / dres / dqkv) equals the
     two separate quantizers byte for byte: the row form of each micro-batch slice against
