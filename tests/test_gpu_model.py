@@ -472,6 +472,33 @@ def test_fp8_rowcol_quantize_bit_identical(gpu, monkeypatch):
         assert np.array_equal(res["1"][2], res["0"][2])
 
 
+def test_fp8_weight_copy_by_columns_bit_identical(gpu, monkeypatch):
+    """fp8 mode's MX copy of W^T for the input-gradient GEMMs, made by column-quantizing W (no bf16
+    transpose; VIT_FP8_WT_COLS=1, the default) against transpose + row quantization: bit-identical
+    loss, logits and gradients after a forward / backward, an SGD step and a second step."""
+    v = gpu
+    cfg = v.data.CONFIGS["test_h64"]
+    params = v.data.init_params(cfg, "parity", seed=11)
+    px, lab = v.data.synthetic_batch(cfg, 8, seed=12)
+    res = {}
+    for on in ("1", "0"):
+        monkeypatch.setenv("VIT_FP8_WT_COLS", on)
+        m = v.ViT.build(cfg, 8, v.VIT_FP8, params=params)
+        out = []
+        for _ in range(2):
+            m.zero_grad()
+            loss = m.forward(px, lab)
+            m.backward()
+            out.append((loss, m.logits(), m.grads()))
+            m.optimizer_step(1e-3)
+        res[on] = out
+        m.close()
+    for a_, b_ in zip(res["1"], res["0"]):
+        assert a_[0] == b_[0]
+        assert np.array_equal(a_[1], b_[1])
+        assert np.array_equal(a_[2], b_[2])
+
+
 def test_fp8_training_reduces_loss(gpu):
     """fp8 mode fits one batch like the bf16 mode (40 SGD steps, loss / 10) and its first steps
     track the bf16 trajectory within 1e-1 (measured 6 %: e4m3 rounding of every GEMM operand)."""

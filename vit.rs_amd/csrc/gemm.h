@@ -116,6 +116,9 @@ void quantize_mx_batched_f32(uint8_t* q, uint8_t* sl, const float* x, long long 
 // -> q [C][Kp] e4m3, Kp = mx_cols_kp(R) (R rounded up to 64; padding tokens are zeros) + scales
 // for C rows and K = Kp (mx_scale_bytes(C, Kp)): the MX quantization of the padded transpose
 void quantize_mx_cols_bf16(uint8_t* q, uint8_t* sl, const bf16_t* x, long long R, int C, long long ldx, hipStream_t s);
+// `count` matrices xs elements apart -> outputs qs / ss bytes apart
+void quantize_mx_cols_batched_bf16(uint8_t* q, uint8_t* sl, const bf16_t* x, long long R, int C, long long ldx,
+                                   int count, long long xs, long long qs, long long ss, hipStream_t s);
 // both forms in one read: qr [R][C] (row stride C) + row scales, and the column form of tokens
 // [tok_off, tok_off + ntok) of qc [C][ldqc] + its scales (false + set_error on a bad shape)
 bool quantize_mx_rowcol_bf16(uint8_t* qr, uint8_t* slr, uint8_t* qc, uint8_t* slc, const bf16_t* x, long long R,

@@ -320,8 +320,12 @@ __global__ __launch_bounds__(256) void quantize_mx_rows_k(uint8_t* __restrict__ 
 template <int TOK>  // tokens per workgroup (TOK / 32 waves)
 __global__ __launch_bounds__(TOK * 2) void quantize_mx_cols_k(uint8_t* __restrict__ q, uint8_t* __restrict__ sl,
                                                              const uint16_t* __restrict__ x, int R, int C,
-                                                             long long ldx, int Kp, int rg_tot) {
+                                                             long long ldx, int Kp, int rg_tot, long long xs,
+                                                             long long qs, long long ss) {
     constexpr int NT = TOK * 2;
+    x += blockIdx.z * xs;  // blockIdx.z: matrix of a batch (the L layers of one weight kind)
+    q += blockIdx.z * qs;
+    sl += blockIdx.z * ss;
     __shared__ __attribute__((aligned(16))) uint16_t tile[TOK * 64];
     const int tok0 = blockIdx.x * TOK, col0 = blockIdx.y * 64;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -546,18 +550,22 @@ void quantize_mx_f32(uint8_t* q, uint8_t* sl, const float* x, long long R, int K
     quantize_mx<float>(q, sl, x, R, K, ldx, ldq, 1, 0, 0, 0, s);
 }
 long long mx_cols_kp(long long R) { return (R + 63) / 64 * 64; }
-void quantize_mx_cols_bf16(uint8_t* q, uint8_t* sl, const bf16_t* x, long long R, int C, long long ldx, hipStream_t s) {
-    if (R <= 0 || C <= 0) return;
-    if (C % 64 || ldx % 8 || ((uintptr_t)x & 15) || ((uintptr_t)q & 15) || R >= (1LL << 30)) {
+void quantize_mx_cols_batched_bf16(uint8_t* q, uint8_t* sl, const bf16_t* x, long long R, int C, long long ldx,
+                                   int count, long long xs, long long qs, long long ss, hipStream_t s) {
+    if (R <= 0 || C <= 0 || count <= 0) return;
+    if (C % 64 || ldx % 8 || xs % 8 || qs % 16 || ((uintptr_t)x & 15) || ((uintptr_t)q & 15) || R >= (1LL << 30)) {
         set_error("quantize_mx_cols: C %% 64 == 0 and 16-B aligned rows required (C=%d)", C);
         return;
     }
     const int kp = (int)mx_cols_kp(R);
     const int cpad = (int)mx_rows_padded(C);
     // 128 tokens per workgroup (256 measured within 2 %, r03)
-    f8::quantize_mx_cols_k<128><<<dim3(cdiv(kp, 128), cpad / 64), 256, 0, s>>>(q, sl, (const uint16_t*)x, (int)R, C, ldx,
-                                                                              kp, cpad / 32);
+    f8::quantize_mx_cols_k<128><<<dim3(cdiv(kp, 128), cpad / 64, count), 256, 0, s>>>(
+        q, sl, (const uint16_t*)x, (int)R, C, ldx, kp, cpad / 32, xs, qs, ss);
     after_launch("quantize_mx_cols");
+}
+void quantize_mx_cols_bf16(uint8_t* q, uint8_t* sl, const bf16_t* x, long long R, int C, long long ldx, hipStream_t s) {
+    quantize_mx_cols_batched_bf16(q, sl, x, R, C, ldx, 1, 0, 0, 0, s);
 }
 bool quantize_mx_rowcol_bf16(uint8_t* qr, uint8_t* slr, uint8_t* qc, uint8_t* slc, const bf16_t* x, long long R,
                              int C, long long ldx, long long ldqc, long long tok_off, long long ntok, hipStream_t s) {

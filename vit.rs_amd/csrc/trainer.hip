@@ -379,6 +379,7 @@ struct Trainer {
     // (MX blocks of 32 consecutive tokens: the axis the weight gradient reduces over) into [OC][Kp] /
     // [Cin][Kp] e4m3 rows on the weight-gradient stream, then the MXFP8 engine with K-split slabs
     bool fp8_wgrad = true;
+    bool wt_cols = true;  // fp8: the dgrads' MX weight copy by column-quantizing W (VIT_FP8_WT_COLS=0: transpose + rows)
     QMat wg_a, wg_b;  // column-quantized dout / inp of the running weight gradient (stream-ordered)
     // fused row+column quantization (quantize_mx_rowcol_bf16): the column forms of ln1, atty, ln2
     // per layer (written by the forward GEMMs' quantize step, read by the backward's weight
@@ -683,6 +684,8 @@ struct Trainer {
                 }
                 const char* fe = getenv("VIT_FP8_FUSE");
                 fuse_mx = !(fe && fe[0] == '0');
+                const char* wc = getenv("VIT_FP8_WT_COLS");
+                wt_cols = !(wc && wc[0] == '0') && C % 64 == 0;
                 const char* fw = getenv("VIT_FP8_WGRAD");
                 fp8_wgrad = !(fw && fw[0] == '0') && C % 64 == 0;
                 if (fp8_wgrad) {
@@ -792,7 +795,8 @@ struct Trainer {
         const int kinds[4] = {P_QKVW, P_ATTPROJW, P_FCW, P_FCPROJW};
         const int rows[4] = {3 * C, C, 4 * C, C}, cols[4] = {C, C, C, 4 * C};
         tbeg(TC_MISC, 0);
-        for (int k = 0; k < 4; k++) {
+        // fp8 mode reads no bf16 transposed copy (refresh_fp8 column-quantizes W for the dgrads)
+        for (int k = 0; k < 4 && !(fp8() && wt_cols); k++) {
             const long long stride = L > 1 ? off[kinds[k] * L + 1] - off[kinds[k] * L] : 0;
             // negative stride: pass the lowest-addressed layer (layers are stored in reverse)
             const int l0 = stride < 0 ? L - 1 : 0;
@@ -815,8 +819,12 @@ struct Trainer {
             const long long N = wq_n[k], K = wq_k[k];
             quantize_mx_batched_f32(wq[k].q, wq[k].s, P(wkinds[k], l0), N, (int)K, L, as, N * K,
                                     (long long)mx_scale_bytes(N, (int)K), s);
-            quantize_mx_batched_bf16(wtq[k].q, wtq[k].s, WT(wkinds[k], l0), K, (int)N, L, as, N * K,
-                                     (long long)mx_scale_bytes(K, (int)N), s);
+            if (wt_cols)  // Wt's MX rows = W's MX columns: byte-identical, without the bf16 transpose
+                quantize_mx_cols_batched_bf16(wtq[k].q, wtq[k].s, W(wkinds[k], l0), N, (int)K, K, L, as, N * K,
+                                              (long long)mx_scale_bytes(K, (int)N), s);
+            else
+                quantize_mx_batched_bf16(wtq[k].q, wtq[k].s, WT(wkinds[k], l0), K, (int)N, L, as, N * K,
+                                         (long long)mx_scale_bytes(K, (int)N), s);
         }
         tend();
     }
