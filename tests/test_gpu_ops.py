@@ -296,14 +296,16 @@ def test_attention_fused_bf16(gpu, oracle64, monkeypatch, B, T, NH, HS, path):
         assert rel_err(g[:, :, k], r[:, :, k]) < 3e-2, name
 
 
-@pytest.mark.parametrize("B,T,NH,HS", [(2, 197, 3, 64), (24, 197, 12, 64), (30, 100, 12, 64), (3, 257, 16, 80)])
+@pytest.mark.parametrize("B,T,NH,HS", [(2, 197, 3, 64), (24, 197, 12, 64), (30, 100, 12, 64), (3, 257, 16, 80),
+                                       (2, 129, 4, 64), (2, 161, 2, 80), (2, 65, 2, 32)])
 def test_attention_backward_variants(gpu, oracle64, monkeypatch, B, T, NH, HS):
     """Every backward kernel (VIT_ATTN_BWD: persistent one-pass default, one workgroup per item,
     paired roles) on the same inputs: each within the bf16 gate of the fp64 oracle, the variants
     within bf16 rounding of each other, and each deterministic (two launches bitwise equal).
-    ViT-H/14's geometry (head size 80, T = 257 = 8 x 32 + 1): the one-pass kernel over the first 256
-    keys and all 257 queries plus attn_xkey_k for the last key (its dS per query joins the main
-    kernel's dQ as a rank-1 term); VIT_ATTN_BWD=pair keeps the paired-role kernel."""
+    T = 32k + 1 (ViT-H/14: head size 80, T = 257; and 129 / 161 / 65 at head sizes 64 / 80 / 32): the
+    one-pass kernel over the first T-1 keys and all T queries with the last key on its VALU side
+    path (its dS per query joins dQ as a rank-1 term, its dK / dV rows summed by one thread per
+    output); VIT_ATTN_BWD=pair keeps the paired-role kernel."""
     v, o = gpu, oracle64
     C = HS * NH
     rng = np.random.default_rng(T * 7 + NH)  # the seed of test_attention_fused_bf16

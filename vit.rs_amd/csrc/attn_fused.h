@@ -915,7 +915,7 @@ constexpr bool bwd1_fits() {
 template <int HS, int NKT>
 constexpr bool bwd1_fits_xk() {
     return Bwd1<HS, NKT, true>::BYTES <= 160 * 1024 && (NKT / 2 <= 4 || (NKT / 2 <= 8 && HS <= 80)) &&
-           NKT / 2 + 1 <= ATTN_PART_ROWS;
+           NKT / 2 + 1 <= ATTN_PART_ROWS && NKT / 2 * 64 >= 2 * HS;  // a thread per dK / dV output of the last key
 }
 
 template <int HS, int NKT, bool XK = false>
@@ -1045,6 +1045,7 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
                 const bf16_t* img = (tid < HS ? Qs : Ds) + cur * 32 * SK;
                 const float* wv = tid < HS ? xds_s : xp_s;
                 const int d = tid < HS ? tid : tid - HS;
+#pragma unroll 8
                 for (int j = 0; j < 32; j++) {
                     xacc += wv[j] * slice_at<HS>(img, j, d);
                     xsds += xds_s[j];
@@ -1061,13 +1062,13 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
                      dsum ? dsum + ((long long)(b * NWR + w) * NH + h) * 3 * HS : nullptr, lane);
     if constexpr (XK) {  // key T-1's dK, dV and its column-sum row (index NW of the item)
         if (tid < 2 * HS) {
-            const int d = tid < HS ? tid : tid - HS;
-            const float v = tid < HS ? xacc * scale : xacc;
-            dq[(long long)(T - 1) * C3 + (tid < HS ? C : 2 * C) + d] = f2bf(v);
+            const int o = tid, d = o < HS ? o : o - HS;
+            const float v = o < HS ? xacc * scale : xacc;
+            dq[(long long)(T - 1) * C3 + (o < HS ? C : 2 * C) + d] = f2bf(v);
             if (dsum) {
                 float* row = dsum + ((long long)(b * NWR + NW) * NH + h) * 3 * HS;
-                row[(tid < HS ? HS : 2 * HS) + d] = v;
-                if (tid < HS) row[d] = scale * xsds * xk_s[d];
+                row[(o < HS ? HS : 2 * HS) + d] = v;
+                if (o < HS) row[d] = scale * xsds * xk_s[d];
             }
         }
     }
