@@ -669,6 +669,12 @@ __device__ __forceinline__ float slice_at(const bf16_t* img, int j, int d) {
     if constexpr (sw_slice<HS>()) return bf2f(*reinterpret_cast<const bf16_t*>(reinterpret_cast<const char*>(img) + sl_off(j, 2 * d)));
     else return bf2f(img[j * Geo<HS>::SK + d]);
 }
+// dims 8p .. 8p+7 of slice row j (one 16-B read; the swizzle moves whole 16-B chunks)
+template <int HS>
+__device__ __forceinline__ uint4 slice_chunk8(const bf16_t* img, int j, int p) {
+    if constexpr (sw_slice<HS>()) return *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(img) + sl_off(j, 16 * p));
+    else return *reinterpret_cast<const uint4*>(img + j * Geo<HS>::SK + 8 * p);
+}
 // 16-B piece cc of slice row t into a slice image
 template <int HS>
 __device__ __forceinline__ void slice_put(bf16_t* img, int t, int cc, uint4 v) {
@@ -1011,6 +1017,17 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
     }
     __syncthreads();
     float xacc = 0.f, xsds = 0.f;  // XK: this thread's dK / dV element of key T-1; sum of its dS
+    // XK: the 8 dims 8p .. 8p+7 (p = tid & 15 < HS / 8) of key T-1's K and V rows, in registers for
+    // the item: each query's s = q . k and dP = do . v is 16 lanes x one 16-B slice read
+    float xkr[8], xvr[8];
+    if constexpr (XK) {
+        const int p8 = (tid & 15) * 8;
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+            xkr[e] = p8 < HS ? xk_s[p8 + e] : 0.f;
+            xvr[e] = p8 < HS ? xv_s[p8 + e] : 0.f;
+        }
+    }
     const float scale = 1.0f / sqrtf((float)HS);
     const float c = LOG2E * scale;
     R.zero();
@@ -1023,12 +1040,16 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
             const bf16_t* Qc = Qs + cur * 32 * SK;
             const bf16_t* Dc = Ds + cur * 32 * SK;
             for (int idx = tid; idx < 512; idx += NT) {
-                const int j = idx >> 4, part = idx & 15;
+                const int j = idx >> 4, part = idx & 15;  // part == tid & 15 (NT % 16 == 0)
                 float sq = 0.f, dp = 0.f;
+                if (part * 8 < HS) {
+                    const uint4 qv = slice_chunk8<HS>(Qc, j, part), dv = slice_chunk8<HS>(Dc, j, part);
+                    const uint32_t qw[4] = {qv.x, qv.y, qv.z, qv.w}, dw[4] = {dv.x, dv.y, dv.z, dv.w};
 #pragma unroll
-                for (int d = part; d < HS; d += 16) {
-                    sq += slice_at<HS>(Qc, j, d) * xk_s[d];
-                    dp += slice_at<HS>(Dc, j, d) * xv_s[d];
+                    for (int e = 0; e < 4; e++) {
+                        sq += __uint_as_float(qw[e] << 16) * xkr[2 * e] + __uint_as_float(qw[e] & 0xffff0000u) * xkr[2 * e + 1];
+                        dp += __uint_as_float(dw[e] << 16) * xvr[2 * e] + __uint_as_float(dw[e] & 0xffff0000u) * xvr[2 * e + 1];
+                    }
                 }
                 sq = row_sum16(sq);
                 dp = row_sum16(dp);
