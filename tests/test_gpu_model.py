@@ -521,6 +521,24 @@ def test_fp8_training_reduces_loss(gpu):
     assert early < 1e-1, (early, traj)
 
 
+def test_fp8_loss_curve_fixture(gpu):
+    """fp8 mode against its own recorded trajectory (tests/golden/fp8_curve_test_h64.json, made by
+    tests/golden/make_fp8_curve.py): 14 SGD steps of test_h64 at B=128 (two micro-batches, every
+    fused MX path: row+column quantizer, epilogue MX forms, split-K fp8 weight gradients; lr 0.01).  The
+    reference has no fp8 path, so this only pins drift: each loss within 2e-3 relative (the
+    path is deterministic; the margin absorbs rounding changes outside the fp8 GEMMs)."""
+    import json
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import make_fp8_curve
+    v = gpu
+    ref = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fp8_curve_test_h64.json")))
+    got = np.array(make_fp8_curve.curve(v, len(ref["losses"])))
+    want = np.array(ref["losses"])
+    assert np.abs(got / want - 1).max() < 2e-3, (got.tolist(), want.tolist())
+
+
 def test_vit_h14_fp8_full_width_step(gpu):
     """Config 5 at full width (C=1280, hs 80, T=257), 4 layers, B=32, fp8 mode: finite loss near
     ln(1000), finite non-zero grads in every tensor family, loss drops after one SGD step."""
