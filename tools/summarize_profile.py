@@ -37,6 +37,14 @@ CLASS_KERNELS = {
 }
 
 
+# one kernel instance serving two classes, told apart per dispatch by traffic: the fp32-residual
+# epilogue runs proj fwd (A 1 x C wide) and fcproj fwd (A 4 x C wide) alternately in every layer;
+# the smaller half of its dispatches (by bytes) is proj fwd, the larger fcproj fwd
+SPLIT_KERNELS = {
+    r"g2::gemm_kernel<true, true, 5\b": ("gemm_proj_fwd", "gemm_fcproj_fwd"),
+}
+
+
 def find(src, pattern):
     hits = glob.glob(os.path.join(src, "**", pattern), recursive=True)
     return sorted(hits)[0] if hits else None
@@ -93,6 +101,15 @@ def main():
             tot = sum(traffic[k]["bytes_per_dispatch"] * traffic[k]["dispatches"] for k in ks)
             n = sum(traffic[k]["dispatches"] for k in ks)
             classes[cls] = {"kernels": ks, "bytes_per_dispatch": tot / n}
+    for rx, (lo_cls, hi_cls) in SPLIT_KERNELS.items():
+        for k in set(fetch) & set(write):
+            if not re.search(rx, k) or len(fetch[k]) != len(write[k]) or len(fetch[k]) < 2:
+                continue
+            per = sorted(2.0 * f_ + w_ for f_, w_ in zip(fetch[k], write[k]))
+            h = len(per) // 2
+            classes[lo_cls] = {"kernels": [k], "bytes_per_dispatch": sum(per[:h]) / h, "split": "smaller half"}
+            classes[hi_cls] = {"kernels": [k], "bytes_per_dispatch": sum(per[h:]) / (len(per) - h),
+                               "split": "larger half"}
     with open(os.path.join(dst, f"{a.tag}_traffic.json"), "w") as f:
         json.dump({"tag": a.tag, "correction": "FETCH_SIZE*2 + WRITE_SIZE, KiB->bytes",
                    "classes": classes, "kernels": traffic}, f, indent=1)
