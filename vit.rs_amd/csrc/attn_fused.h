@@ -790,7 +790,8 @@ __device__ __forceinline__ void bwd_slice_a(BwdRegs<HS, KK>& R, const bf16_t* Qc
 
 // phase B: dQ^T tiles (dt, u) of the slice at q0, spread over the NW waves; dq = dqkv Q rows of the item
 // xk_ds / xk_k (XK): dS[q][T-1] per query of the slice and K[T-1] (fp32) of a key the kernel does not
-// own (attn_xkey_k): its rank-1 term dS[q][T-1] K[T-1] joins the dQ accumulators before the store
+// own on the MFMA path (the XK side path): its rank-1 term dS[q][T-1] K[T-1] joins the dQ
+// accumulators before the store
 template <int HS, int NSL, int NW, bool XK = false>
 __device__ __forceinline__ void bwd_slice_b(const bf16_t* Ks, const bf16_t* dSs, bf16_t* dq, long long C3, int q0,
                                             int T, float scale, int w, int lane, const float* xk_ds = nullptr,
@@ -1077,7 +1078,7 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
         bwd_slice_b<HS, NSL, NW, XK>(Ks, dSs, dq, C3, q0, T, scale, w, lane, xds_s, xk_s);
         __syncthreads();
     }
-    // per-wave column-sum rows: dsum[((b NWR + w) NH + h)][3 HS], NWR = NW (+ 1: attn_xkey_k's row)
+    // per-wave column-sum rows: dsum[((b NWR + w) NH + h)][3 HS], NWR = NW (+ 1: the last key's row, XK)
     constexpr int NWR = NW + (XK ? 1 : 0);
     bwd_item_end<HS>(R, dq, C, key0, T, scale,
                      dsum ? dsum + ((long long)(b * NWR + w) * NH + h) * 3 * HS : nullptr, lane);
