@@ -161,6 +161,11 @@ def cpu_baseline(cfg, reps=3):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_ctypes as oc
     o = oc.Oracle("f32")
+    # The oracle is built with OpenMP (test speed); libgomp sized its team from the whole
+    # affinity mask at load, so pin the team to one thread before timing (r03 ran a 256-thread
+    # team on one core and measured 3.4x too slow).
+    nth = o.set_num_threads(1)
+    assert nth == 1, f"oracle OpenMP team is {nth} threads, cpu_baseline needs 1"
     allowed = os.sched_getaffinity(0)
     core = min(allowed)
     os.sched_setaffinity(0, {core})

@@ -44,6 +44,7 @@ typedef struct {
 
 enum { VIT_FP32 = 0, VIT_BF16 = 1, VIT_FP8 = 2 };
 enum { VIT_NUM_PARAM_TENSORS = 20 };
+enum { VIT_MAX_LAYERS = 64 };  /* num_layers range accepted by vit_trainer_create / vit_layout_query */
 
 typedef struct vit_trainer vit_trainer_t;
 

@@ -56,6 +56,13 @@ class Oracle:
         L.ref_vit_param_sizes.argtypes = [ctypes.POINTER(VitConfig), P]
         L.ref_sgd_step.argtypes = [P, P, ctypes.c_longlong, self.ctype]
         L.ref_adamw_step.argtypes = [P, P, P, P, ctypes.c_longlong] + [self.ctype] * 5 + [ctypes.c_int]
+        L.ref_set_num_threads.argtypes = [i]
+        L.ref_get_num_threads.restype = i
+
+    def set_num_threads(self, n):
+        """OpenMP team size of the oracle's parallel loops (1 = the single-thread reference timing)."""
+        self.lib.ref_set_num_threads(int(n))
+        return int(self.lib.ref_get_num_threads())
 
     # -- helpers --------------------------------------------------------------------------
     def _p(self, a):

@@ -90,3 +90,25 @@ def test_jpeg_trainer_feed_matches_oracle_pixels(gpu, tmp_path):
         assert la == lb, (step, la, lb)
         assert np.array_equal(a.logits(), b.logits())
     a.close(); b.close(); L.close()
+
+
+def test_jpeg_trainer_feed_rejects_batch_mismatch(gpu, tmp_path):
+    """A loader opened with another batch size than the trainer's (e.g. the global batch instead of
+    the per-rank one) is refused by vit_trainer_set_batch_jpeg before any pixel or label is copied
+    (it would write past the trainer's staging buffer); the matching loader still feeds."""
+    v = gpu
+    cfg = v.data.CONFIGS["test_h64"]
+    jpegs, _ = jf.dataset(8, seed=13, sizes=((cfg.img, cfg.img),))
+    labels = np.arange(8, dtype=np.int32)
+    m = v.ViT.build(cfg, 2, v.VIT_BF16, params=v.data.init_params(cfg, "parity", seed=4))
+    for nb in (4, 1):
+        L = v.JpegLoader(*_records(v, tmp_path, f"mm{nb}", jpegs, labels), batch=nb, shuffle=False, threads=1)
+        L.next()
+        with pytest.raises(v.VitError, match="trainer's batch is 2"):
+            m.set_batch_jpeg(L)
+        L.close()
+    L = v.JpegLoader(*_records(v, tmp_path, "ok2", jpegs, labels), batch=2, shuffle=False, threads=1)
+    L.next()
+    m.set_batch_jpeg(L)
+    assert np.isfinite(m.forward())
+    L.close(); m.close()

@@ -4,7 +4,8 @@ Every comparison is per tensor (logits and each of the 20 gradient tensors) with
 rule of tests/parity.py (floor restated in DESIGN.md §2):
   fp32 mode (the reference op sequence on the GPU): max-normalised 1e-4 and elementwise
       |gpu - ref| <= 1e-4 |ref| + 1e-5 max|ref| on >= 99.99 %, loss 1e-4 — the north-star bar;
-  bf16 mode (the benchmarked fast path): 2e-2 / 2e-2 |ref| + 2e-3 max|ref| on >= 99.99 %, loss 1e-2;
+  bf16 mode (the benchmarked fast path): 2e-2 / 2e-2 |ref| + 1e-2 max|ref| on >= 99.99 %, loss 1e-2
+      (parity.BF16: tol 2e-2, floor_rel 1e-2);
   fp8 mode: the operand-rounding error model of tests/parity.py (<= 1.5 x 16 x the bf16 error).
 These configs are small (B <= 8): their GEMMs run the 128x128 engine.  The kernel set the bench
 times is checked at a production batch in test_gpu_production.py.
@@ -564,3 +565,112 @@ def test_vit_h14_fp8_full_width_step(gpu):
     loss1 = m.forward()
     assert loss1 < loss0
     m.close()
+
+
+def test_vit_h14_fp8_config5_shard_full_step(gpu):
+    """BASELINE config 5's per-GPU workload (ViT-H/14, 224^2, C=1280, L=32, NH=16, hs 80, T=257,
+    B=128 per GPU = the DP=8 shard of a 1024 global batch) in fp8 mode, through the C ABI exactly
+    as bench.py runs it (two micro-batch streams, stream concurrency on): one full step has a finite
+    loss near ln(1000), finite non-zero gradients in every tensor family, and the loss drops after
+    one SGD step.  The launch counters prove the kernels that only appear at this size ran: the
+    MXFP8 engine (every GEMM of every layer), the fused row+column quantizer, and the one-pass
+    attention backward with the T = 32k+1 last-key side path over 2048 (b, h) items.
+    Replaces train_vit.rs:188-373 (forward / backward), :543-555 (weight gradients), :559-601
+    (attention_backward) at this size; size-independent properties, not an oracle comparison
+    (the oracle would take hours at 32 layers x 128 images)."""
+    v = gpu
+    cfg = v.data.CONFIGS["vit_h14"]
+    assert (cfg.num_layers, cfg.channels, cfg.T, cfg.head_size) == (32, 1280, 257, 80)
+    B = 128
+    params = v.data.init_params(cfg, "parity", seed=51)
+    px, lab = v.data.synthetic_batch(cfg, B, seed=52)
+    m = v.ViT.build(cfg, B, v.VIT_FP8, params=params)
+    del params
+    m.set_concurrency(True)
+    m.set_batch(px, lab)
+    m.sync()
+    v.kernel_hits_reset()
+    m.zero_grad()
+    loss0 = m.forward()
+    m.backward()
+    m.sync()
+    hits = v.kernel_hits()
+    assert np.isfinite(loss0) and abs(loss0 - np.log(1000)) < 1.5, loss0
+    g = m.grads()
+    assert g.size == cfg.num_params()
+    assert np.all(np.isfinite(g))
+    gs = cfg.split(g)
+    zero = [n for n, a in gs.items() if not np.abs(a).max() > 0]
+    assert not zero, zero
+    del g, gs
+    L = cfg.num_layers
+    # fp8 engine: qkv / proj / fc / fcproj forward + input gradients (+ weight gradients) per layer
+    assert hits[v.HIT_GEMM_FP8:v.HIT_GEMM_FP8 + 16].sum() >= 8 * L, hits[v.HIT_GEMM_FP8:v.HIT_GEMM_FP8 + 16]
+    assert hits[v.HIT_QUANT_ROWCOL] >= 6 * L, hits[v.HIT_QUANT_ROWCOL]
+    assert hits[v.HIT_ATTN_BWD_XKEY] >= L, hits[v.HIT_ATTN_BWD_XKEY]
+    assert hits[v.HIT_ATTN_FWD_MFMA] >= L
+    assert hits[v.HIT_ATTN_GENERIC] == 0 and hits[v.HIT_ATTN_BWD_PAIR] == 0
+    m.optimizer_step(0.02)
+    m.zero_grad()
+    loss1 = m.forward()
+    assert np.isfinite(loss1) and loss1 < loss0, (loss0, loss1)
+    m.close()
+
+
+def _shard_sum(v, cfg, prec, params, px, lab, nshard, nmb=1):
+    """Gradients of `nshard` equal image shards through the HIP trainer, each with
+    dloss = 1/B_global (train_vit.rs:288, D15), summed on the host in float64 — what the DP
+    all-reduce produces, without RCCL."""
+    B = px.shape[0]
+    b = B // nshard
+    tot, losses = None, []
+    for s in range(nshard):
+        m = v.ViT.build(cfg, b, prec, params=params)
+        m.set_concurrency(True)
+        m.set_option("microbatch", nmb)
+        m.zero_grad()
+        losses.append(m.forward(px[s * b:(s + 1) * b], lab[s * b:(s + 1) * b], b_global=B))
+        m.backward()
+        g = m.grads().astype(np.float64)
+        tot = g if tot is None else tot + g
+        m.close()
+    return losses, tot
+
+
+@pytest.mark.parametrize("prec_name", ["VIT_FP32", "VIT_BF16"])
+def test_dp_shard_sum_equals_full_batch(gpu, oracle32, prec_name):
+    """The data-parallel identity through the HIP library itself (VERDICT r03 missing #2): two
+    half-batch shards run by the native trainer with b_global = the full batch, their gradients
+    summed on the host, equal (a) the full-batch gradient of the same trainer and (b) the oracle's
+    full-batch gradient.  fp32: (a) within 1e-5 relative per tensor (only fp32 summation order
+    differs), (b) within the fp32 gate; bf16: (a) within 1e-3 max-normalised (bf16 rounding of
+    per-image activations is shard-independent; the weight-gradient GEMMs sum bf16 products over a
+    different token split), (b) within the bf16 gate.  The shard mean losses average to the full
+    mean (the per-rank forward returns its own shard mean, train_vit.rs:264-266)."""
+    import oracle_ctypes as oc
+    v = gpu
+    prec = getattr(v, prec_name)
+    cfg = v.data.CONFIGS["test_h64"]
+    B = 8
+    params = v.data.init_params(cfg, "parity", seed=61)
+    px, lab = v.data.synthetic_batch(cfg, B, seed=62)
+    losses, gsum = _shard_sum(v, cfg, prec, params, px, lab, 2)
+    m = v.ViT.build(cfg, B, prec, params=params)
+    m.zero_grad()
+    loss_full = m.forward(px, lab)
+    m.backward()
+    gfull = m.grads()
+    m.close()
+    assert abs(np.mean(losses) - loss_full) <= 1e-5 * abs(loss_full)
+    tol = 1e-5 if prec == v.VIT_FP32 else 1e-3
+    worst = {}
+    for n, a, b in zip(cfg.split(gsum).keys(), cfg.split(gsum).values(), cfg.split(gfull).values()):
+        worst[n] = float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+    print(f"\n{prec_name} shard-sum vs full-batch HIP: max {max(worst.values()):.2e}")
+    assert max(worst.values()) <= tol, worst
+    loss_r, logits_r, g_r = oracle_step(oc, oracle32, cfg, params, px, lab)
+    rule = parity.FP32 if prec == v.VIT_FP32 else parity.BF16
+    bad, rep = parity.check({n: (a, b) for (n, a), b in zip(cfg.split(gsum.astype(np.float32)).items(),
+                                                           cfg.split(g_r).values())}, rule)
+    print(f"{prec_name} shard-sum vs oracle: {parity.summary(rep)}")
+    assert not bad, bad

@@ -132,3 +132,29 @@ def test_production_bf16_step_is_bitwise_repeatable(gpu, ref):
     assert a[0] == b[0]
     assert np.array_equal(a[1], b[1])
     assert np.array_equal(a[2], b[2])
+
+
+@pytest.mark.parametrize("prec_name", ["VIT_BF16", "VIT_FP32"])
+def test_production_dp_shard_sum(gpu, ref, prec_name):
+    """The DP identity at the production kernel set (VERDICT r03 missing #2): the per-GPU shards
+    of a DP=2 step (B=64 each, b_global = 128, dloss = 1/B_global as train_vit.rs:288 / D15) run
+    through the HIP trainer on the production engines (64 x 197 = 12 608 tokens = 197 x 64: the
+    256x256 epilogues, split-K slab weight gradients, persistent attention backward); their
+    gradients summed on the host equal the full-batch oracle gradient within the mode's gate."""
+    from test_gpu_model import _shard_sum
+    v = gpu
+    prec = getattr(v, prec_name)
+    cfg = ref["cfg"]
+    v.kernel_hits_reset()
+    losses, gsum = _shard_sum(v, cfg, prec, ref["params"], ref["px"], ref["lab"], 2)
+    hits = v.kernel_hits()
+    gate = parity.BF16 if prec == v.VIT_BF16 else parity.FP32
+    lrel = abs(np.mean(losses) - ref["loss"]) / abs(ref["loss"])
+    assert lrel <= gate["loss"], lrel
+    pairs = {n: (a, b) for (n, a), b in zip(cfg.split(gsum.astype(np.float32)).items(), cfg.split(ref["grads"]).values())}
+    bad, rep = parity.check(pairs, gate)
+    print(f"\n{prec_name} DP=2 shard sum vs oracle: loss {lrel:.2e}, {parity.summary(rep)}")
+    assert not bad, bad
+    if prec == v.VIT_BF16:
+        assert hits[v.HIT_GEMM_128:v.HIT_GEMM_128 + 16].sum() == 0, "128x128 fallback ran"
+        assert hits[v.HIT_ATTN_BWD_PERSISTENT] == 2 * cfg.num_layers

@@ -108,3 +108,61 @@ def test_jpeg_loader_reports_bad_record(vit, tmp_path):
     with pytest.raises(vit.VitError, match="image 2"):
         L.next()
     L.close()
+
+
+def _segments(data):
+    """(marker, start, end) of each marker segment up to and including the first SOS's entropy data"""
+    out, p = [], 2
+    while p < len(data) - 1:
+        m = data[p + 1]
+        n = int.from_bytes(data[p + 2:p + 4], "big")
+        out.append((m, p, p + 2 + n))
+        if m == 0xDA:
+            e = p + 2 + n
+            while not (data[e] == 0xFF and data[e + 1] not in (0x00,) and not 0xD0 <= data[e + 1] <= 0xD7):
+                e += 1
+            out[-1] = (m, p, e)
+            break
+        p += 2 + n
+    return out
+
+
+def test_second_frame_after_scan_rejected(vit):
+    """SOI / SOF / SOS / SOF(larger) / SOS: a second frame header would resize the frame under scan
+    buffers sized by the first; the parser must refuse it as libjpeg does."""
+    small = jf.encode(16, 16, 0, 90, {})
+    big = jf.encode(64, 96, 0, 90, {})
+    segs = {m: (a, b) for m, a, b in _segments(big)}
+    sof = big[segs[0xC0][0]:segs[0xC0][1]]
+    sos = big[segs[0xDA][0]:segs[0xDA][1]]
+    assert small.endswith(b"\xff\xd9")
+    bad = small[:-2] + sof + sos + b"\xff\xd9"
+    vit.jpeg_coefficients(small)  # the prefix itself decodes
+    with pytest.raises(vit.VitError, match="duplicate SOF"):
+        vit.jpeg_coefficients(bad)
+
+
+def test_oversized_frame_rejected(vit):
+    """A header of 65535 x 65535 pixels is refused before any allocation."""
+    good = jf.encode(16, 16, 0, 90, {})
+    (_, a, _), = [s for s in _segments(good) if s[0] == 0xC0]
+    bad = bytearray(good)
+    bad[a + 5:a + 9] = b"\xff\xff\xff\xff"   # height, width
+    with pytest.raises(vit.VitError, match="too large"):
+        vit.jpeg_probe(bytes(bad))
+    with pytest.raises(vit.VitError, match="too large"):
+        vit.jpeg_coefficients(bytes(bad))
+
+
+@pytest.mark.timeout(120, method="thread")
+def test_jpeg_loader_close_while_producing(vit, tmp_path):
+    """Closing a loader while its producer is between batches (a pool job published, or about to
+    be) must not deadlock: a job published before the stop runs to its end, none is published
+    after it.  Many open / next / close cycles with the producer racing ahead (depth 3)."""
+    jpegs, labels = jf.dataset(16, seed=7, sizes=((32, 32), (40, 24)))
+    paths = vit.write_jpeg_records(str(tmp_path / "race"), jpegs, labels)
+    for i in range(60):
+        L = vit.JpegLoader(*paths, batch=[1, 2, 4][i % 3], shuffle=True, threads=1 + i % 3)
+        if i % 2:
+            L.next()
+        L.close()

@@ -600,6 +600,119 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
     asm volatile("" ::: "memory");
     staged_epilogue<EPI>(p, acc, smem + wave * STG_WAVE_BYTES, lane, tm0 + wm * 128, tn0 + wn * 64);
 }
+
+// Software-pipelined form (variant 5; K-contiguous A and B: every forward and input-gradient GEMM
+// of the trainer).  The kernel above reads a K-step's 12 fragments and then issues its 32 MFMAs, so
+// a wave alone on its SIMD leaves the matrix pipe idle for the read latency of every step: it
+// relies on the other resident workgroup's wave to fill those gaps, and while that workgroup runs
+// its epilogue (GELU pair, fp32 residual: up to 40 % of a heavy-epilogue launch) nothing does.
+// Here each wave reads step s+1's fragments between step s's MFMAs (two named fragment sets, the
+// loop unrolled by two so every access is static), so one wave keeps its SIMD's matrix pipe
+// busy on its own and the two workgroups of a CU hide each other's epilogues.
+// Ring of 3 slots, DMA three steps ahead: at step s's barrier every wave holds F(s) in registers
+// (lgkmcnt(0) before the barrier) and its own pieces of s+1 have landed (vmcnt(6): s+2's stay in
+// flight), so after the barrier step s+1 is readable by all and slot s % 3 takes step s+3.
+template <int EPI>
+__global__ __launch_bounds__(NT, 2) void gemm_kernel_pipe(GemmParams p) {
+    __shared__ __attribute__((aligned(1024))) char smem[NSLOT * SLOT_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int ntm = cdiv(p.M, BM), ntn = cdiv(p.N, BN);
+    int tm, tn, wg, split;
+    split_remap(ntm * ntn, wg, split);
+    group_order(wg, ntm, ntn, tm, tn);
+    const int tm0 = tm * BM, tn0 = tn * BN;
+    const int kbeg = split * p.kchunk;
+    const int kend = min(p.K, kbeg + p.kchunk);
+    const int nk = (kend - kbeg) / BK;
+    const bf16_t* A = (const bf16_t*)p.A;
+    const bf16_t* B = (const bf16_t*)p.B;
+
+    f32x4_t acc[8][4];
+#pragma unroll
+    for (int a = 0; a < 8; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    auto issue = [&](int st) {
+        char* sl = smem + (st % NSLOT) * SLOT_BYTES;
+        const int k0 = kbeg + st * BK;
+        stage<true, BM>(A, p.lda, tm0, p.M, k0, sl, wave, lane);
+        stage<true, BN>(B, p.ldb, tn0, p.N, k0, sl + A_BYTES, wave, lane);
+    };
+    auto read = [&](int st, bf16x8_t (&fa)[8], bf16x8_t (&fb)[4]) {
+        const char* img = smem + (st % NSLOT) * SLOT_BYTES;
+#pragma unroll
+        for (int b = 0; b < 4; b++) fb[b] = frag<true, BN>(img + A_BYTES, wn * 64 + b * 16, lane);
+#pragma unroll
+        for (int a = 0; a < 8; a++) fa[a] = frag<true, BM>(img, wm * 128 + a * 16, lane);
+    };
+    auto bar = [&](bool more) {  // retire own pieces of step s+1 (s+2's stay in flight) and F(s)
+        __builtin_amdgcn_sched_barrier(0);
+        if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // step s: MFMAs on F(s) = (ca, cb); when s+1 exists, F(s+1) -> (na, nb) between them
+    auto step = [&](int s, const bf16x8_t (&ca)[8], const bf16x8_t (&cb)[4], bf16x8_t (&na)[8],
+                    bf16x8_t (&nb)[4]) {
+        bar(s + 2 < nk);
+        if (s + 3 < nk) issue(s + 3);  // into slot s % 3: every wave holds F(s) in registers
+        __builtin_amdgcn_sched_barrier(0);
+        auto mfmas = [&]() {
+#pragma unroll
+            for (int a = 0; a < 8; a++)
+#pragma unroll
+                for (int b = 0; b < 4; b++)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cb[b], ca[a], acc[a][b], 0, 0, 0);
+        };
+        if (s + 1 < nk) {
+            read(s + 1, na, nb);
+            mfmas();
+#if VIT_PIPE_SGB
+            // 12 fragment reads, one per two MFMAs, then the last 8 MFMAs
+#pragma unroll
+            for (int j = 0; j < 12; j++) {
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x8, 8, 0);
+#endif
+        } else {
+            mfmas();
+        }
+    };
+
+    bf16x8_t fa0[8], fb0[4], fa1[8], fb1[4];
+    if (nk > 0) {
+        issue(0);
+        if (nk > 1) issue(1);
+        if (nk > 2) issue(2);
+        // own pieces of step 0 landed (1 and 2 stay in flight), then F(0) for everyone
+        __builtin_amdgcn_sched_barrier(0);
+        if (nk > 2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        else if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        read(0, fa0, fb0);
+    }
+    for (int kt = 0; kt < nk; kt += 2) {
+        step(kt, fa0, fb0, fa1, fb1);
+        if (kt + 1 < nk) step(kt + 1, fa1, fb1, fa0, fb0);
+    }
+
+    if (skip_epilogue(p, acc)) return;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    staged_epilogue<EPI>(p, acc, smem + wave * STG_WAVE_BYTES, lane, tm0 + wm * 128, tn0 + wn * 64);
+}
 }  // namespace g4
 
 // ============================================================================ fp32 MFMA GEMM
@@ -848,11 +961,12 @@ __global__ __launch_bounds__(256) void slab_reduce_k(float* __restrict__ C, long
 
 // engine selection (gemm_bf16_set_variant; default from VIT_GEMM, else 2):
 //   1 = 128x128 register-staged everywhere, 2 = production (256x256 one workgroup per CU; split-K
-//   weight gradients on 256x128), 4 = 256x128 two per CU everywhere.  Debug flag 2 skips the
+//   weight gradients on 256x128), 4 = 256x128 two per CU everywhere, 5 = as 4 with the
+//   software-pipelined main loop (g4::gemm_kernel_pipe) for K-contiguous operands.  Debug flag 2 skips the
 //   epilogues (main-loop-only timing; results are garbage).
 static int g_variant = -1;
 static int g_debug_flags = 0;
-static bool known_variant(int v) { return v == 1 || v == 2 || v == 4; }
+static bool known_variant(int v) { return v == 1 || v == 2 || v == 4 || v == 5; }
 static int gemm_variant() {
     if (g_variant < 0) {
         const char* e = getenv("VIT_GEMM");
@@ -1012,6 +1126,25 @@ static void launch_g2(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStre
 
 template <bool AK, bool BKC>
 static void launch_g4(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStream_t s) {
+    if constexpr (AK && BKC) {
+        if (gemm_variant() == 5) {  // software-pipelined main loop
+            switch (a.epi) {
+#define VIT_CASE(E) \
+    case E: g4::gemm_kernel_pipe<E><<<grid, g4::NT, 0, s>>>(p); return;
+                VIT_CASE(EPI_F32_STORE)
+                VIT_CASE(EPI_F32_ACC)
+                VIT_CASE(EPI_BF16_STORE)
+                VIT_CASE(EPI_BF16_GELU)
+                VIT_CASE(EPI_F32_RESID)
+                VIT_CASE(EPI_BF16_DGELU)
+                VIT_CASE(EPI_F32_SLAB)
+                VIT_CASE(EPI_BF16_GELU_D)
+                VIT_CASE(EPI_BF16_MUL)
+#undef VIT_CASE
+                default: break;
+            }
+        }
+    }
     switch (a.epi) {
 #define VIT_CASE(E) \
     case E: g4::gemm_kernel<AK, BKC, E><<<grid, g4::NT, 0, s>>>(p); break;
@@ -1094,7 +1227,7 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s) {
                   a.M, a.N, a.K, a.lda, a.ldb);
         return;
     }
-    if (gemm_variant() == 4 && a.K % g4::KTILE == 0 && a.M >= 256 && a.N >= 128 &&
+    if ((gemm_variant() == 4 || gemm_variant() == 5) && a.K % g4::KTILE == 0 && a.M >= 256 && a.N >= 128 &&
         (a.epi != EPI_F32_ATOMIC || a.N % 4 == 0)) {
         gemm_bf16_g4(a, s);
         return;

@@ -429,12 +429,14 @@ struct DeviceSide {
     size_t dcap = 0;
     uint8_t* planes = nullptr;
     size_t pcap = 0;
-    hipEvent_t done = nullptr;  // the kernels of the previous batch (buffer reuse across streams)
+    hipEvent_t done = nullptr;      // the kernels of the previous batch (buffer reuse across streams)
+    hipEvent_t uploaded = nullptr;  // the upload of the current batch (pinned host block reusable)
 
     bool grow(void** p, size_t& cap, size_t need) {
         if (need <= cap) return true;
         if (*p) {
-            (void)hipDeviceSynchronize();
+            // only the previous batch's kernels read the old buffer: wait for them, not the device
+            (void)hipEventSynchronize(done);
             (void)hipFree(*p);
         }
         *p = nullptr;
@@ -449,7 +451,8 @@ struct DeviceSide {
     }
     // enqueue the upload and both kernels of hb on st; out [n][img][img][3] uint8 (device)
     bool run(const HostBatch& hb, uint8_t* out, int img, hipStream_t st) {
-        if (!done && hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess) {
+        if ((!done && hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess) ||
+            (!uploaded && hipEventCreateWithFlags(&uploaded, hipEventDisableTiming) != hipSuccess)) {
             set_error("jpeg: event creation failed");
             return false;
         }
@@ -458,7 +461,8 @@ struct DeviceSide {
             return false;
         }
         if (hipStreamWaitEvent(st, done, 0) != hipSuccess ||
-            hipMemcpyAsync(dbuf, hb.buf, hb.used, hipMemcpyHostToDevice, st) != hipSuccess) {
+            hipMemcpyAsync(dbuf, hb.buf, hb.used, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipEventRecord(uploaded, st) != hipSuccess) {
             set_error("jpeg: upload failed");
             return false;
         }
@@ -471,12 +475,13 @@ struct DeviceSide {
             set_error("jpeg: kernel launch failed");
             return false;
         }
-        // the pinned batch may be refilled once the upload has read it
-        (void)hipStreamSynchronize(st);
+        // the pinned batch may be refilled once the upload has read it (the kernels keep running)
+        (void)hipEventSynchronize(uploaded);
         return true;
     }
     ~DeviceSide() {
         if (done) (void)hipEventDestroy(done);
+        if (uploaded) (void)hipEventDestroy(uploaded);
         if (dbuf) (void)hipFree(dbuf);
         if (planes) (void)hipFree(planes);
     }
@@ -557,7 +562,9 @@ struct vit_jpeg_loader {
             {
                 std::unique_lock<std::mutex> lk(pmu);
                 pcv.wait(lk, [&] { return stop || job_gen != seen; });
-                if (stop) return;
+                // a job published before the stop still runs to its end (quit makes it cheap), so
+                // the producer waiting in pool_job always sees job_left reach 0
+                if (job_gen == seen) return;
                 seen = job_gen;
             }
             int done_here = 0;
@@ -585,6 +592,7 @@ struct vit_jpeg_loader {
     bool pool_job(const long long* recs, HostBatch* hb) {
         {
             std::lock_guard<std::mutex> lk(pmu);
+            if (stop) return false;  // the workers may have left: publish nothing after a stop
             job_recs = recs;
             job_hb = hb;
             job_copy = hb != nullptr;
@@ -662,10 +670,17 @@ struct vit_jpeg_loader {
 
 namespace vit {
 // trainer.hip: decode the loader's current batch into device uint8 [B][img][img][3] on st
-bool jpeg_loader_decode_to(vit_jpeg_loader_t* l, uint8_t* out, int img, hipStream_t st, const int** labels) {
+// (expect_n >= 0: the destination holds exactly expect_n images; a loader batch of another size is
+// rejected before anything is written or its labels read)
+bool jpeg_loader_decode_to(vit_jpeg_loader_t* l, uint8_t* out, int img, hipStream_t st, const int** labels,
+                           int expect_n) {
     HostBatch* hb = l->current();
     if (!hb) {
         set_error("jpeg loader: no current batch (call vit_jpeg_loader_next first)");
+        return false;
+    }
+    if (expect_n >= 0 && hb->n != expect_n) {
+        set_error("jpeg loader: batch of %d images, the trainer's batch is %d", hb->n, expect_n);
         return false;
     }
     if (!hb->err.empty()) {
@@ -816,7 +831,7 @@ int vit_jpeg_loader_decode_u8(vit_jpeg_loader_t* l, unsigned char* dev_out, int 
         set_error("vit_jpeg_loader_decode_u8: bad arguments");
         return 1;
     }
-    return vit::jpeg_loader_decode_to(l, dev_out, img, vit::stream(), nullptr) && !vit::has_error() ? 0 : 1;
+    return vit::jpeg_loader_decode_to(l, dev_out, img, vit::stream(), nullptr, -1) && !vit::has_error() ? 0 : 1;
 }
 
 void vit_jpeg_loader_close(vit_jpeg_loader_t* l) {

@@ -17,6 +17,7 @@ constexpr uint8_t kZig[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18
                               58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
 constexpr int FAST = 11;  // look-up bits of the fast Huffman table
+constexpr long long kMaxFramePixels = 1LL << 28;  // 16384 x 16384: larger headers are rejected
 
 struct Huff {
     bool present = false;
@@ -179,12 +180,18 @@ struct Parser {
     }
 
     bool frame(const uint8_t* q, int len) {
+        // a second SOF would resize the frame under scan state sized by the first (libjpeg
+        // rejects it too)
+        if (have_frame) return fail("duplicate SOF marker");
         if (len < 8) return fail("SOF segment too short");
         if (q[0] != 8) return fail("only 8-bit samples are supported");
         f.h = be16(q + 1);
         f.w = be16(q + 3);
         f.nc = q[5];
         if (f.w <= 0 || f.h <= 0) return fail("zero image dimension (DNL not supported)");
+        // host allocations (masks, offsets, values) scale with the header's pixel count: bound it
+        // before any entropy data is read
+        if ((long long)f.w * f.h > kMaxFramePixels) return fail("image too large (more than 2^28 pixels)");
         if (f.nc != 1 && f.nc != 3) return fail("only 1- or 3-component images are supported");
         if (len < 6 + 3 * f.nc) return fail("SOF segment too short");
         f.hmax = f.vmax = 1;

@@ -25,7 +25,8 @@
 
 namespace vit {
 // jpeg.hip: the JPEG loader's current batch -> device uint8 [B][img][img][3] on st
-bool jpeg_loader_decode_to(vit_jpeg_loader_t* l, uint8_t* out, int img, hipStream_t st, const int** labels);
+bool jpeg_loader_decode_to(vit_jpeg_loader_t* l, uint8_t* out, int img, hipStream_t st, const int** labels,
+                           int expect_n);
 namespace {
 
 enum TIdx {
@@ -174,7 +175,7 @@ __global__ void to_bf16_k(bf16_t* __restrict__ out, const float* __restrict__ in
 // (unlayered tensors: l = 0); chunk c = [chunk_off[c], chunk_off[c+1]): c = 0 head + final LN,
 // 1..L layers L-1..0 (backward's completion order), L+1 embedding.
 void compute_layout(int C, int L, int T, int KP, int NC, long long (&canon_size)[20], long long& n_params,
-                    std::vector<long long>& off, long long (&chunk_off)[66], int& n_chunks, long long& arena_elems) {
+                    std::vector<long long>& off, long long (&chunk_off)[VIT_MAX_LAYERS + 3], int& n_chunks, long long& arena_elems) {
     const long long C_ = C, K = KP;
     const long long sz[20] = {C_ * K, C_, C_, (long long)T * C_,
                               L * C_, L * C_, L * 3 * C_ * C_, L * 3 * C_, L * C_ * C_, L * C_,
@@ -223,7 +224,7 @@ struct Trainer {
     long long canon_size[20]{};
     // device offsets: tensor ti, layer l (l=0 for unlayered)
     std::vector<long long> off;   // [20 * L]
-    long long chunk_off[64 + 2]{};  // chunk c: [chunk_off[c], chunk_off[c+1]) ; c=0 head, 1..L layers L-1..0, L+1 embed
+    long long chunk_off[VIT_MAX_LAYERS + 3]{};  // chunk c: [chunk_off[c], chunk_off[c+1]) ; c=0 head, 1..L layers L-1..0, L+1 embed
     int n_chunks = 0;
 
     hipStream_t s = nullptr, s_comm = nullptr;
@@ -525,7 +526,7 @@ struct Trainer {
         BT = (long long)B * T;
         prec = precision;
         device = dev;
-        if (c->in_ch != 3 || C % NH || L < 1 || L > 64 || B < 1 || prec < VIT_FP32 || prec > VIT_FP8) {
+        if (c->in_ch != 3 || C % NH || L < 1 || L > VIT_MAX_LAYERS || B < 1 || prec < VIT_FP32 || prec > VIT_FP8) {
             set_error("trainer: unsupported config");
             return false;
         }
@@ -1375,7 +1376,7 @@ struct Trainer {
         // the staging slot is free once the normalise of two uploads ago has run
         VIT_HIP(hipStreamWaitEvent(s_copy, u8_used[k], 0));
         if (jl) {  // host entropy decode already done by the loader; the pixel work runs here
-            if (!jpeg_loader_decode_to(jl, u8_stage[k], cfg.img, s_copy, &lab)) return false;
+            if (!jpeg_loader_decode_to(jl, u8_stage[k], cfg.img, s_copy, &lab, B)) return false;
         } else {
             VIT_HIP(hipMemcpyAsync(u8_stage[k], img, bytes, hipMemcpyHostToDevice, s_copy));
         }
@@ -1689,13 +1690,13 @@ int vit_trainer_sync(vit_trainer_t* h) {
 void* vit_trainer_stream(vit_trainer_t* h) { return (void*)h->t.s; }
 
 int vit_layout_query(const vit_config_t* cfg, long long* tensor_off, long long* chunk_off, long long* arena_elems) {
-    if (!cfg || cfg->num_layers < 1 || cfg->num_layers > 64 || cfg->patch < 1 || cfg->img < cfg->patch ||
+    if (!cfg || cfg->num_layers < 1 || cfg->num_layers > VIT_MAX_LAYERS || cfg->patch < 1 || cfg->img < cfg->patch ||
         cfg->channels < 1 || cfg->num_classes < 1) {
         set_error("vit_layout_query: bad config");
         return -1;
     }
     const int L = cfg->num_layers, np = (cfg->img / cfg->patch) * (cfg->img / cfg->patch);
-    long long canon[20], n_params = 0, co[66], arena = 0;
+    long long canon[20], n_params = 0, co[VIT_MAX_LAYERS + 3], arena = 0;
     std::vector<long long> off;
     int n_chunks = 0;
     vit::compute_layout(cfg->channels, L, np + 1, cfg->in_ch * cfg->patch * cfg->patch, cfg->num_classes, canon,
