@@ -234,6 +234,10 @@ void gemm_fp8_fused_mxc(void* C, void* C2, long long ldc, const void* aux, long 
  * diagnostics (flag 2: skip epilogues, main-loop timing only) */
 void gemm_bf16_set_variant(int variant);
 void gemm_bf16_set_debug(int flags);
+/* diagnostic: per-workgroup timestamps of the 256x256 / 256x128 bf16 engines into trace (device,
+ * 4 x u64 per workgroup of the next launches: start, main-loop end, end (100 MHz s_memrealtime),
+ * hardware id = XCC_ID << 32 | HW_ID); NULL turns it off */
+void gemm_bf16_set_trace(unsigned long long* trace);
 void convert_f32_to_bf16(uint16_t* out, const float* inp, long long n);
 void convert_bf16_to_f32(float* out, const uint16_t* inp, long long n);
 

@@ -87,3 +87,31 @@ def check_fp8(pairs_fp8, pairs_bf16):
             if rf[n][k] > fp8_limit(rb[n][k]):
                 bad[f"{n}.{k}"] = (rf[n][k], rb[n][k], fp8_limit(rb[n][k]))
     return bad
+
+
+# ------------------------------------------------------------------ fp8 regression gate (r04)
+# The error model above is a ceiling (9-21 % max-normalised at the measured bf16 errors), far above
+# what the fp8 path actually delivers, so a block-scale layout regression could pass it.  Each
+# tensor's rms-normalised error is therefore also held to FP8_RMS_SLACK x its value recorded at the
+# commit that made tests/golden/fp8_err_baseline.json (VIT_RECORD_FP8_ERR=1 records instead of
+# checking, into gpurun_out/fp8_err_baseline.json; copied into tests/golden and profiles/).
+import json as _json
+import os as _os
+
+FP8_RMS_SLACK = 1.5
+_FP8_BASE = _os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "golden", "fp8_err_baseline.json")
+
+
+def fp8_rms_gate(key, report):
+    """report: fp8_report(pairs) of the fp8 run.  Returns {tensor: (rms, limit)} for failures."""
+    rms = {n: m["rms"] for n, m in report.items()}
+    if _os.environ.get("VIT_RECORD_FP8_ERR"):
+        root = _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__)))
+        out = _os.path.join(root, "gpurun_out", "fp8_err_baseline.json")
+        _os.makedirs(_os.path.dirname(out), exist_ok=True)
+        cur = _json.load(open(out)) if _os.path.exists(out) else {}
+        cur[key] = rms
+        _json.dump(cur, open(out, "w"), indent=1, sort_keys=True)
+        return {}
+    base = _json.load(open(_FP8_BASE))[key]
+    return {n: (r, FP8_RMS_SLACK * base[n]) for n, r in rms.items() if r > FP8_RMS_SLACK * base[n] + 1e-7}

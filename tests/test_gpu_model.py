@@ -414,6 +414,9 @@ def test_fp8_trainer_vs_oracle(gpu, oracle32, name, B):
     assert lf <= parity.fp8_limit(lb), (lf, lb)
     bad = parity.check_fp8(pf, pb)
     assert not bad, bad
+    # regression gate: each tensor's rms error within 1.5x its recorded value (tests/parity.py)
+    reg = parity.fp8_rms_gate(f"trainer_{name}", rf)
+    assert not reg, reg
 
 
 def test_fp8_fused_mx_epilogues_bit_identical(gpu, monkeypatch):

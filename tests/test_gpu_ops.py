@@ -356,10 +356,11 @@ def test_error_channel(gpu):
 
 
 # ------------------------------------------------------------------ generic bf16 GEMM engine
-@pytest.fixture(params=[2, 4])
+@pytest.fixture(params=[2, 4, 5])
 def engine(request, gpu):
     """Run a test under each production GEMM engine (2 = 256x256 one workgroup per CU, with the split-K
-    weight gradients on 256x128; 4 = 256x128 two per CU everywhere), then restore the default."""
+    weight gradients on 256x128; 4 = 256x128 two per CU everywhere; 5 = as 4 with the
+    software-pipelined main loop for K-contiguous operands), then restore the default."""
     gpu.lib().gemm_bf16_set_variant(request.param)
     yield request.param
     gpu.lib().gemm_bf16_set_variant(2)
@@ -393,6 +394,42 @@ def test_gemm_bf16_layouts(gpu, engine, M, N, K, ak, bk):
         assert rel_err(got, want) < (1e-2 if epi == 3 else 2e-3), epi
         if dbias is not None:
             assert rel_err(dbias.numpy(), ar.sum(1)) < 2e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(6304, 3072, 768), (1576, 768, 3072), (520, 384, 256), (776, 1000, 128)])
+def test_gemm_bf16_pipelined_bit_identical(gpu, M, N, K):
+    """The software-pipelined 256x128 main loop (variant 5, g4::gemm_kernel_pipe) issues the same
+    MFMAs in the same K order per accumulator as the 256x128 engine (variant 4): every fused epilogue
+    of the trainer (bf16 store, GELU pair, fp32 residual, x aux + column sums) bit-identical, at the
+    trainer's K (768, 3072) and ragged M / N."""
+    v = gpu
+    L = v.lib()
+    rng = np.random.default_rng(M + 3 * N + K)
+    ab = v.bf16_bits(rng.uniform(-1, 1, size=(M, K)).astype(np.float32))
+    wb = v.bf16_bits((rng.uniform(-1, 1, size=(N, K)) * 0.1).astype(np.float32))
+    A, W = D(v, ab, np.uint16), D(v, wb, np.uint16)
+    bias = D(v, rng.normal(size=N).astype(np.float32))
+    res = D(v, rng.normal(size=(M, N)).astype(np.float32))
+    aux = D(v, v.bf16_bits(rng.normal(size=(M, N)).astype(np.float32)), np.uint16)
+    outs = {}
+    try:
+        for var in (4, 5):
+            L.gemm_bf16_set_variant(var)
+            o = {}
+            for epi in (3, 5, 8, 9):
+                c = Z(v, M * N, np.float32 if epi == 5 else np.uint16)
+                c2 = Z(v, M * N, np.uint16) if epi == 8 else None
+                cs = D(v, np.zeros(N, np.float32)) if epi == 9 else None
+                v.call("gemm_bf16_fused", c, c2, N, res if epi == 5 else (aux if epi == 9 else None), N,
+                       A, K, 1, W, K, 1, bias if epi in (3, 5, 8) else None, cs, M, N, K, epi)
+                o[epi] = [c.numpy()] + ([c2.numpy()] if c2 is not None else []) + ([cs.numpy()] if cs is not None else [])
+            outs[var] = o
+    finally:
+        L.gemm_bf16_set_variant(2)
+    for epi in outs[4]:
+        for x, y in zip(outs[4][epi], outs[5][epi]):
+            assert np.array_equal(x, y), epi
+    assert np.abs(outs[5][5][0]).max() > 0
 
 
 def _gelu64(x):

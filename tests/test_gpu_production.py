@@ -121,6 +121,9 @@ def test_production_fp8_step_vs_oracle(gpu, ref):
     lrel_f = abs(lf - ref["loss"]) / abs(ref["loss"])
     assert lrel_f <= parity.fp8_limit(lrel_b), (lrel_f, lrel_b)
     assert not bad, bad
+    # regression gate: each tensor's rms error within 1.5x its recorded value (tests/parity.py)
+    reg = parity.fp8_rms_gate("production", parity.fp8_report(pf))
+    assert not reg, reg
 
 
 def test_production_bf16_step_is_bitwise_repeatable(gpu, ref):

@@ -111,6 +111,7 @@ _SIGS = {
     "gemm_fp8_fused_mx": (None, [P, P, LL, P, LL, P, P, LL, P, P, LL, P, P, I, I, I, I, P, P]),
     "gemm_fp8_fused_mxc": (None, [P, P, LL, P, LL, P, P, LL, P, P, LL, P, P, I, I, I, I, P, P, P, P, LL, LL]),
     "gemm_bf16_set_variant": (None, [I]), "gemm_bf16_set_debug": (None, [I]),
+    "gemm_bf16_set_trace": (None, [P]),
     "vit_kernel_hits": (I, [P, I]),
     "convert_f32_to_bf16": (None, [P, P, LL]),
     "convert_bf16_to_f32": (None, [P, P, LL]),

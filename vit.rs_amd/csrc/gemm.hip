@@ -328,6 +328,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
+    trace_stamp(p, 0);
     const int ntm = cdiv(p.M, BM), ntn = cdiv(p.N, BN);
     int wg, split;
     split_remap(ntm * ntn, wg, split);
@@ -419,6 +420,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
         bar();
     }
     if (nk > 0 && !lagging) bar();  // balance the stagger barrier
+    trace_stamp(p, 1);
     float bpre[8];  // the epilogue's bias columns, loaded under the trailing DMA wait
     staged_bias_prefetch<EPI>(p, lane, tn0 + wn * 64, bpre);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // retire the trailing re-staged pieces
@@ -440,6 +442,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     staged_epilogue<EPI>(p, acc, smem + wave * STG_WAVE_BYTES, lane, tm0 + wm * 128, tn0 + wn * 64, bpre);
+    trace_stamp(p, 2);
 }
 
 }  // namespace g2
@@ -537,6 +540,7 @@ __device__ __forceinline__ void group_order(int t, int ntm, int ntn, int& tm, in
 template <bool AK, bool BKC, int EPI>
 __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
     __shared__ __attribute__((aligned(1024))) char smem[NSLOT * SLOT_BYTES];
+    first_round_stagger(p.stagger);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 1, wn = wave & 1;
@@ -606,15 +610,21 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p) {
 // a wave alone on its SIMD leaves the matrix pipe idle for the read latency of every step: it
 // relies on the other resident workgroup's wave to fill those gaps, and while that workgroup runs
 // its epilogue (GELU pair, fp32 residual: up to 40 % of a heavy-epilogue launch) nothing does.
-// Here each wave reads step s+1's fragments between step s's MFMAs (two named fragment sets, the
-// loop unrolled by two so every access is static), so one wave keeps its SIMD's matrix pipe
-// busy on its own and the two workgroups of a CU hide each other's epilogues.
-// Ring of 3 slots, DMA three steps ahead: at step s's barrier every wave holds F(s) in registers
-// (lgkmcnt(0) before the barrier) and its own pieces of s+1 have landed (vmcnt(6): s+2's stay in
-// flight), so after the barrier step s+1 is readable by all and slot s % 3 takes step s+3.
+// Here a wave's reads run under its own MFMAs, so one wave keeps its SIMD's matrix pipe busy and
+// the two workgroups of a CU hide each other's epilogues.  Each K-step is two phases of 16 MFMAs:
+//   phase 0: MFMAs of A rows 0-63 (alo) x B (fb)   ||  reads of A rows 64-127 (ahi) of step s
+//   [vmcnt: own pieces of s+1 landed; lgkmcnt(0); barrier; DMA of step s+3 into slot s % 3]
+//   phase 1: MFMAs of ahi x fb                      ||  reads of fb, alo of step s+1
+// so the fragments in flight cost 16 + 16 VGPRs beyond one step's 48 (two named B sets, the loop
+// unrolled by two).  Ring of 3 slots, DMA three steps ahead.  After step s's barrier every wave
+// has read all of slot s (lgkmcnt(0) before it) and its own pieces of s+1 have landed (s+2's stay
+// in flight: vmcnt(6)), so slot s+1 is readable by all and slot s takes step s+3.  The DMA
+// sources are one 32-bit byte offset per piece from the scalar operand base (6 VGPRs).
 template <int EPI>
 __global__ __launch_bounds__(NT, 2) void gemm_kernel_pipe(GemmParams p) {
     __shared__ __attribute__((aligned(1024))) char smem[NSLOT * SLOT_BYTES];
+    first_round_stagger(p.stagger);
+    trace_stamp(p, 0);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 1, wn = wave & 1;
@@ -626,8 +636,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel_pipe(GemmParams p) {
     const int kbeg = split * p.kchunk;
     const int kend = min(p.K, kbeg + p.kchunk);
     const int nk = (kend - kbeg) / BK;
-    const bf16_t* A = (const bf16_t*)p.A;
-    const bf16_t* B = (const bf16_t*)p.B;
+    const char* A = (const char*)p.A;
+    const char* B = (const char*)p.B;
 
     f32x4_t acc[8][4];
 #pragma unroll
@@ -635,64 +645,98 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel_pipe(GemmParams p) {
 #pragma unroll
         for (int b = 0; b < 4; b++) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
+    // per-piece byte offsets of this lane's 16-B DMA source (K-contig image, as stage<true, R>)
+    uint32_t offa[BM / 64], offb[BN / 64];
+#pragma unroll
+    for (int j = 0; j < BM / 64; j++) {
+        const int row = (j * 4 + wave) * 16 + (lane >> 2);
+        const int c = (lane & 3) ^ kc_swz(row);
+        offa[j] = (uint32_t)(((long long)min(tm0 + row, p.M - 1) * p.lda + c * 8) * 2);
+    }
+#pragma unroll
+    for (int j = 0; j < BN / 64; j++) {
+        const int row = (j * 4 + wave) * 16 + (lane >> 2);
+        const int c = (lane & 3) ^ kc_swz(row);
+        offb[j] = (uint32_t)(((long long)min(tn0 + row, p.N - 1) * p.ldb + c * 8) * 2);
+    }
     auto issue = [&](int st) {
         char* sl = smem + (st % NSLOT) * SLOT_BYTES;
-        const int k0 = kbeg + st * BK;
-        stage<true, BM>(A, p.lda, tm0, p.M, k0, sl, wave, lane);
-        stage<true, BN>(B, p.ldb, tn0, p.N, k0, sl + A_BYTES, wave, lane);
-    };
-    auto read = [&](int st, bf16x8_t (&fa)[8], bf16x8_t (&fb)[4]) {
-        const char* img = smem + (st % NSLOT) * SLOT_BYTES;
+        const long long kb = (long long)(kbeg + st * BK) * 2;
+        const char* a0 = A + kb;
+        const char* b0 = B + kb;
 #pragma unroll
-        for (int b = 0; b < 4; b++) fb[b] = frag<true, BN>(img + A_BYTES, wn * 64 + b * 16, lane);
+        for (int j = 0; j < BM / 64; j++)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(a0 + offa[j]),
+                                             (__attribute__((address_space(3))) void*)(sl + (j * 4 + wave) * 1024),
+                                             16, 0, 0);
 #pragma unroll
-        for (int a = 0; a < 8; a++) fa[a] = frag<true, BM>(img, wm * 128 + a * 16, lane);
+        for (int j = 0; j < BN / 64; j++)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(b0 + offb[j]),
+                                             (__attribute__((address_space(3))) void*)(sl + A_BYTES + (j * 4 + wave) * 1024),
+                                             16, 0, 0);
     };
-    auto bar = [&](bool more) {  // retire own pieces of step s+1 (s+2's stay in flight) and F(s)
+    // fragment reads as inline asm (ds_read_b128, immediate offsets): the compiler neither counts
+    // nor waits for them, the phases below do (hipcc's own counting put lgkmcnt(0) in front of
+    // phase 0, waiting for the reads meant to run under its MFMAs).  Lane (i, g) of a 16-row
+    // fragment at rows r0 + i: kc_swz(r0 + i) = (i >> 1) & 3 for r0 % 16 == 0, so one lane address
+    // per operand and slot, the fragments at + 1 KiB each.
+    const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(char, smem);
+    const uint32_t a_lane = lds0 + (wm * 128 + (lane & 15)) * 64 + (((lane >> 4) ^ kc_swz(lane & 15)) << 4);
+    const uint32_t b_lane = lds0 + A_BYTES + (wn * 64 + (lane & 15)) * 64 + (((lane >> 4) ^ kc_swz(lane & 15)) << 4);
+    auto read_b = [&](int st, bf16x8_t (&fb)[4]) {
+        const uint32_t o = b_lane + (st % NSLOT) * SLOT_BYTES;
+        asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:1024\n\t"
+                     "ds_read_b128 %2, %4 offset:2048\n\tds_read_b128 %3, %4 offset:3072"
+                     : "=&v"(fb[0]), "=&v"(fb[1]), "=&v"(fb[2]), "=&v"(fb[3]) : "v"(o));
+    };
+    auto read_a = [&](int st, int half, bf16x8_t (&fa)[4]) {
+        const uint32_t o = a_lane + (st % NSLOT) * SLOT_BYTES + half * 4096;
+        asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:1024\n\t"
+                     "ds_read_b128 %2, %4 offset:2048\n\tds_read_b128 %3, %4 offset:3072"
+                     : "=&v"(fa[0]), "=&v"(fa[1]), "=&v"(fa[2]), "=&v"(fa[3]) : "v"(o));
+    };
+    auto mfma16 = [&](int half, const bf16x8_t (&fa)[4], const bf16x8_t (&fb)[4]) {
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+                acc[half * 4 + a][b] =
+                    __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[b], fa[a], acc[half * 4 + a][b], 0, 0, 0);
+    };
+    bf16x8_t alo[4], ahi[4], fbA[4], fbB[4];
+    // step s with B fragments cb (read in the previous step) and the next step's into nb
+    auto step = [&](int s, const bf16x8_t (&cb)[4], bf16x8_t (&nb)[4]) {
+        // phase 0: alo x cb, ahi of step s read underneath (reads issued first)
         __builtin_amdgcn_sched_barrier(0);
-        if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        read_a(s, 1, ahi);
+        // the 8 reads of the previous phase (cb, alo) are done, this phase's 4 (ahi) stay in flight
+        asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        mfma16(0, alo, cb);
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + 2 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
-    };
-    // step s: MFMAs on F(s) = (ca, cb); when s+1 exists, F(s+1) -> (na, nb) between them
-    auto step = [&](int s, const bf16x8_t (&ca)[8], const bf16x8_t (&cb)[4], bf16x8_t (&na)[8],
-                    bf16x8_t (&nb)[4]) {
-        bar(s + 2 < nk);
-        if (s + 3 < nk) issue(s + 3);  // into slot s % 3: every wave holds F(s) in registers
+        if (s + 3 < nk) issue(s + 3);  // into slot s % 3: every wave has read all of it
         __builtin_amdgcn_sched_barrier(0);
-        auto mfmas = [&]() {
-#pragma unroll
-            for (int a = 0; a < 8; a++)
-#pragma unroll
-                for (int b = 0; b < 4; b++)
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cb[b], ca[a], acc[a][b], 0, 0, 0);
-        };
-        if (s + 1 < nk) {
-            read(s + 1, na, nb);
-            mfmas();
-#if VIT_PIPE_SGB
-            // 12 fragment reads, one per two MFMAs, then the last 8 MFMAs
-#pragma unroll
-            for (int j = 0; j < 12; j++) {
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
-            }
-            __builtin_amdgcn_sched_group_barrier(0x8, 8, 0);
-#endif
-        } else {
-            mfmas();
-        }
+        // phase 1: ahi x cb, step s+1's fb and alo read underneath (unconditionally: past the
+        // last step the slot holds stale data nobody uses and no DMA writes it, and straight-line
+        // reads keep the compiler's lgkmcnt tracking exact)
+        read_b(s + 1, nb);
+        read_a(s + 1, 0, alo);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma16(1, ahi, cb);  // ahi: retired by the lgkmcnt(0) in front of the barrier
+        __builtin_amdgcn_sched_barrier(0);
     };
 
-    bf16x8_t fa0[8], fb0[4], fa1[8], fb1[4];
     if (nk > 0) {
         issue(0);
         if (nk > 1) issue(1);
         if (nk > 2) issue(2);
-        // own pieces of step 0 landed (1 and 2 stay in flight), then F(0) for everyone
+        // own pieces of step 0 landed (1 and 2 stay in flight), then fb, alo of step 0
         __builtin_amdgcn_sched_barrier(0);
         if (nk > 2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
         else if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
@@ -700,18 +744,22 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel_pipe(GemmParams p) {
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
-        read(0, fa0, fb0);
+        read_b(0, fbA);
+        read_a(0, 0, alo);
+        __builtin_amdgcn_sched_barrier(0);
     }
-    for (int kt = 0; kt < nk; kt += 2) {
-        step(kt, fa0, fb0, fa1, fb1);
-        if (kt + 1 < nk) step(kt + 1, fa1, fb1, fa0, fb0);
+    for (int kt = 0; kt < nk; kt += 2) {  // nk is even (host: K and the split chunk % 64 == 0)
+        step(kt, fbA, fbB);
+        step(kt + 1, fbB, fbA);
     }
+    trace_stamp(p, 1);
 
     if (skip_epilogue(p, acc)) return;
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     staged_epilogue<EPI>(p, acc, smem + wave * STG_WAVE_BYTES, lane, tm0 + wm * 128, tn0 + wn * 64);
+    trace_stamp(p, 2);
 }
 }  // namespace g4
 
@@ -977,6 +1025,8 @@ static int gemm_variant() {
 }
 void gemm_set_variant(int v) { g_variant = known_variant(v) ? v : 2; }
 void gemm_set_debug(int flags) { g_debug_flags = flags; }
+static unsigned long long* g_trace = nullptr;
+void gemm_set_trace(unsigned long long* trace) { g_trace = trace; }
 
 GemmParams make_gemm_params(const GemmArgs& a, int kchunk) {
     GemmParams p;
@@ -984,6 +1034,8 @@ GemmParams make_gemm_params(const GemmArgs& a, int kchunk) {
     p.lda = a.lda; p.ldb = a.ldb; p.ldc = a.ldc; p.ldaux = a.ldaux;
     p.M = a.M; p.N = a.N; p.K = a.K; p.kchunk = kchunk;
     p.no_epi = (g_debug_flags & 2) ? 1 : 0;
+    p.stagger = (g_debug_flags >> 8) * 50;  // debug: 0.5 us units
+    p.trace = g_trace;
     p.mx_q = a.mx_q;
     p.mx_s = a.mx_s;
     p.mx_rg = (int)(mx_rows_padded(a.M) / 32);
@@ -1127,7 +1179,10 @@ static void launch_g2(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStre
 template <bool AK, bool BKC>
 static void launch_g4(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStream_t s) {
     if constexpr (AK && BKC) {
-        if (gemm_variant() == 5) {  // software-pipelined main loop
+        // software-pipelined main loop: an even step count per split and 32-bit DMA offsets
+        const bool fits = p.kchunk % 64 == 0 && p.K % 64 == 0 && (long long)p.M * p.lda * 2 < (1LL << 32) &&
+                          (long long)p.N * p.ldb * 2 < (1LL << 32);
+        if (gemm_variant() == 5 && fits) {
             switch (a.epi) {
 #define VIT_CASE(E) \
     case E: g4::gemm_kernel_pipe<E><<<grid, g4::NT, 0, s>>>(p); return;

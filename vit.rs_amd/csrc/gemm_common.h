@@ -18,6 +18,8 @@ struct GemmParams {
     int M, N, K;
     int kchunk;  // K range per split (multiple of the K tile)
     int no_epi;  // diagnostic (gemm_bf16_set_debug): skip the epilogue, keep the accumulators live
+    int stagger;  // two-per-CU engines: first-round delay (100 MHz ticks) of the CU's second workgroup
+    unsigned long long* trace;  // diagnostic: [workgroup][4] start, main-loop end, end, hw id
     int tiles;   // output tiles of the launch (the grid is tiles x K-splits)
     uint8_t* mx_q;  // fused MX output (GemmArgs::mx_q / mx_s); mx_rg = padded rows / 32
     uint8_t* mx_s;
@@ -110,6 +112,33 @@ __device__ __forceinline__ void epi_st16(const GemmParams&, void* q, epi_u32x4 v
 }
 __device__ __forceinline__ epi_u32x4 epi_ld16(const GemmParams&, const void* q) {
     return *reinterpret_cast<const epi_u32x4*>(q);
+}
+
+// Two workgroups per CU (g4 engines): workgroups b and b + 256 of a launch share a CU
+// (tools/probe_placement.hip), and every tile takes the same time, so without help the two start,
+// reach their epilogues and finish together, round after round.  Delaying the second workgroup of
+// each CU in the first round by about half a tile keeps the pair half a tile apart for the whole
+// launch (a finishing workgroup's successor starts at once), so one's epilogue runs beside the
+// other's main loop.
+__device__ __forceinline__ void first_round_stagger(int ticks) {
+    if (ticks <= 0) return;
+    const int lin = blockIdx.y * gridDim.x + blockIdx.x;
+    if (lin < 256 || lin >= 512) return;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+// diagnostic timestamps (gemm_bf16_set_trace): lane 0 of wave 0 writes slot k of its workgroup's
+// record with a vector store; k = 3 also records the hardware id
+__device__ __forceinline__ void trace_stamp(const GemmParams& p, int k) {
+    if (!p.trace || threadIdx.x != 0) return;
+    const long long lin = (long long)blockIdx.y * gridDim.x + blockIdx.x;
+    p.trace[lin * 4 + k] = __builtin_amdgcn_s_memrealtime();
+    if (k == 2) {
+        const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+        const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+        p.trace[lin * 4 + 3] = ((unsigned long long)xcc << 32) | hw;
+    }
 }
 
 // diagnostic: time the main loop alone (the accumulators stay live so nothing is eliminated)

@@ -1059,6 +1059,7 @@ void gemm_bf16_fused(void* C, void* C2, long long ldc, const void* aux, long lon
 }
 void gemm_bf16_set_variant(int variant) { gemm_set_variant(variant); }
 void gemm_bf16_set_debug(int flags) { gemm_set_debug(flags); }
+void gemm_bf16_set_trace(unsigned long long* trace) { gemm_set_trace(trace); }
 void convert_f32_to_bf16(uint16_t* out, const float* inp, long long n) {
     convert_f2bf(out, inp, n, stream());
 }
