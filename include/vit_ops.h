@@ -235,8 +235,9 @@ void gemm_fp8_fused_mxc(void* C, void* C2, long long ldc, const void* aux, long 
 void gemm_bf16_set_variant(int variant);
 void gemm_bf16_set_debug(int flags);
 /* diagnostic: per-workgroup timestamps of the 256x256 / 256x128 bf16 engines into trace (device,
- * 4 x u64 per workgroup of the next launches: start, main-loop end, end (100 MHz s_memrealtime),
- * hardware id = XCC_ID << 32 | HW_ID); NULL turns it off */
+ * 16 x u64 per workgroup of the next launches, 100 MHz s_memrealtime: 0 start, 1 main-loop end,
+ * 2 end of wave 0, 3 hardware id = XCC_ID << 32 | HW_ID, 4 + w end of wave w, 12 first K-step's
+ * operands landed); NULL turns it off */
 void gemm_bf16_set_trace(unsigned long long* trace);
 void convert_f32_to_bf16(uint16_t* out, const float* inp, long long n);
 void convert_bf16_to_f32(float* out, const uint16_t* inp, long long n);

@@ -319,3 +319,15 @@ def test_adamw_matches_torch_adamw(oracle64, tmp_path):
     for t in range(1, steps + 1):
         o.adamw_step(p, o.arr(gs[t - 1]), m, v, 1e-2, 0.9, 0.95, 1e-8, 0.1, t)
     assert np.allclose(p, np.load(tmp_path / "out.npy"), rtol=1e-12, atol=1e-14)
+
+
+def test_fp8_err_baseline_fixture_complete():
+    """tests/golden/fp8_err_baseline.json (the fp8 regression gate's recorded per-tensor rms errors,
+    tests/parity.py fp8_rms_gate) holds every gated case and all 21 tensors (logits + 20 grads)."""
+    import json
+    d = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fp8_err_baseline.json")))
+    want = {"trainer_test_h64", "trainer_vit_h14_l1", "trainer_vit_b16_l2", "production"}
+    assert want <= set(d), set(d)
+    for k in want:
+        assert len(d[k]) == 21 and "logits" in d[k], k
+        assert all(0 < v < 0.5 for v in d[k].values()), (k, d[k])

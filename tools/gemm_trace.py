@@ -22,10 +22,13 @@ SHAPES = {  # name: M, N, K, epi (A, W K-contiguous: forward / input-gradient GE
 }
 
 
-def analyse(tr):
-    t0, t1, t2, hw = tr[:, 0].astype(np.int64), tr[:, 1].astype(np.int64), tr[:, 2].astype(np.int64), tr[:, 3]
+def analyse(tr, nwaves):
+    t0, t1, hw = tr[:, 0].astype(np.int64), tr[:, 1].astype(np.int64), tr[:, 3]
+    t2 = tr[:, 4:4 + nwaves].astype(np.int64).max(1)       # last wave's end
+    t2w0 = tr[:, 2].astype(np.int64)
+    tp = tr[:, 12].astype(np.int64)
     base = t0.min()
-    t0, t1, t2 = t0 - base, t1 - base, t2 - base
+    t0, t1, t2, t2w0, tp = t0 - base, t1 - base, t2 - base, t2w0 - base, tp - base
     cu = (hw >> 32) * 4096 + ((hw & 0xFFFFFFFF) >> 8 & 0xFF)
     by = collections.defaultdict(list)
     for i in range(len(t0)):
@@ -54,6 +57,7 @@ def analyse(tr):
         gaps += [s - e for s, e in zip(starts, ends)]
     us = 0.01  # ticks -> us
     return {"span_us": (t2.max()) * us, "main_us": float(np.mean(t1 - t0)) * us,
+            "prologue_us": float(np.mean(tp - t0)) * us, "wave_skew_us": float(np.mean(t2 - t2w0)) * us,
             "epi_us": float(np.mean(t2 - t1)) * us, "cus": len(by), "wg_per_cu": len(t0) / len(by),
             "max_resident": int(np.max(conc)), "epi_overlap": over / max(epi_tot, 1),
             "turnaround_us": float(np.median(gaps)) * us if gaps else 0.0}
@@ -79,7 +83,7 @@ def main():
     out2 = vit.DeviceArray.zeros(Mx * Nx, np.uint16)
     bias = vit.DeviceArray.from_numpy(rng.uniform(-1, 1, size=Nx).astype(np.float32))
     csum = vit.DeviceArray.zeros(Nx, np.float32)
-    trace = vit.DeviceArray.zeros(4 * 8192, np.uint64)
+    trace = vit.DeviceArray.zeros(16 * 8192, np.uint64)
     for name in args.only.split(","):
         M, N, K, epi = SHAPES[name]
         for var in [int(v) for v in args.variants.split(",")]:
@@ -101,9 +105,10 @@ def main():
             vit.check(name)
             bm, bn = (256, 256) if var == 2 else (256, 128)
             nwg = -(-M // bm) * -(-N // bn)
-            tr = trace.numpy().reshape(-1, 4)[:nwg]
-            r = analyse(tr)
-            print(f"{name:13s} v{var} span {r['span_us']:7.1f} us  main {r['main_us']:6.2f}  epi {r['epi_us']:6.2f}  "
+            tr = trace.numpy().reshape(-1, 16)[:nwg]
+            r = analyse(tr, 8 if var == 2 else 4)
+            print(f"{name:13s} v{var} span {r['span_us']:7.1f} us  prologue {r['prologue_us']:5.2f}  main {r['main_us']:6.2f}  "
+                  f"epi(last wave) {r['epi_us']:6.2f}  wave-end skew {r['wave_skew_us']:5.2f}  "
                   f"CUs {r['cus']}  wg/CU {r['wg_per_cu']:.1f}  resident {r['max_resident']}  "
                   f"epi beside other's main loop {r['epi_overlap']:.2f}  turnaround {r['turnaround_us']:.2f} us",
                   flush=True)

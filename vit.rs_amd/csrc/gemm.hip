@@ -390,6 +390,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
         for (int st = 0; st < DEPTH; st++) { issue_a(st); issue_b(st); }
         wait_vm(4 * (min(DEPTH, nk) - 1));  // own pieces of step 0
         bar();
+        trace_stamp(p, 12);
         if (lagging) {
             __builtin_amdgcn_s_setprio(1);  // static priority for the younger half (T5)
             bar();                          // stagger: one barrier behind waves 0-3
@@ -744,6 +745,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel_pipe(GemmParams p) {
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
+        trace_stamp(p, 12);
         read_b(0, fbA);
         read_a(0, 0, alo);
         __builtin_amdgcn_sched_barrier(0);

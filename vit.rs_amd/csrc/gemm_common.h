@@ -128,17 +128,24 @@ __device__ __forceinline__ void first_round_stagger(int ticks) {
     while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)ticks) __builtin_amdgcn_s_sleep(8);
 }
 
-// diagnostic timestamps (gemm_bf16_set_trace): lane 0 of wave 0 writes slot k of its workgroup's
-// record with a vector store; k = 3 also records the hardware id
+// diagnostic timestamps (gemm_bf16_set_trace): record of 16 u64 per workgroup, written by lane 0
+// of a wave with vector stores: 0 start, 1 main-loop end, 2 end (wave 0), 3 hardware id, 4 + w end
+// of wave w (k = 2 writes both), 12 first K-step's operands landed (wave 0)
+constexpr int TRACE_WORDS = 16;
 __device__ __forceinline__ void trace_stamp(const GemmParams& p, int k) {
-    if (!p.trace || threadIdx.x != 0) return;
-    const long long lin = (long long)blockIdx.y * gridDim.x + blockIdx.x;
-    p.trace[lin * 4 + k] = __builtin_amdgcn_s_memrealtime();
+    if (!p.trace || (threadIdx.x & 63) != 0) return;
+    const int w = threadIdx.x >> 6;
+    if (w != 0 && k != 2) return;
+    const long long rec = ((long long)blockIdx.y * gridDim.x + blockIdx.x) * TRACE_WORDS;
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
     if (k == 2) {
+        p.trace[rec + 4 + w] = t;
+        if (w != 0) return;
         const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
         const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
-        p.trace[lin * 4 + 3] = ((unsigned long long)xcc << 32) | hw;
+        p.trace[rec + 3] = ((unsigned long long)xcc << 32) | hw;
     }
+    p.trace[rec + k] = t;
 }
 
 // diagnostic: time the main loop alone (the accumulators stay live so nothing is eliminated)
