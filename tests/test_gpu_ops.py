@@ -356,7 +356,7 @@ def test_error_channel(gpu):
 
 
 # ------------------------------------------------------------------ generic bf16 GEMM engine
-@pytest.fixture(params=[2, 4, 5])
+@pytest.fixture(params=[2, 4, 5, 7])
 def engine(request, gpu):
     """Run a test under each production GEMM engine (2 = 256x256 one workgroup per CU, with the split-K
     weight gradients on 256x128; 4 = 256x128 two per CU everywhere; 5 = as 4 with the
@@ -396,12 +396,19 @@ def test_gemm_bf16_layouts(gpu, engine, M, N, K, ak, bk):
             assert rel_err(dbias.numpy(), ar.sum(1)) < 2e-3
 
 
-@pytest.mark.parametrize("M,N,K", [(6304, 3072, 768), (1576, 768, 3072), (520, 384, 256), (776, 1000, 128)])
-def test_gemm_bf16_pipelined_bit_identical(gpu, M, N, K):
-    """The software-pipelined 256x128 main loop (variant 5, g4::gemm_kernel_pipe) issues the same
-    MFMAs in the same K order per accumulator as the 256x128 engine (variant 4): every fused epilogue
-    of the trainer (bf16 store, GELU pair, fp32 residual, x aux + column sums) bit-identical, at the
-    trainer's K (768, 3072) and ragged M / N."""
+@pytest.mark.parametrize("pair", [(4, 5), (2, 7)])
+@pytest.mark.parametrize("M,N,K", [(6304, 3072, 768), (1576, 768, 3072), (520, 384, 256), (776, 1000, 128),
+                                   (50432, 768, 768)])
+def test_gemm_bf16_pipelined_bit_identical(gpu, M, N, K, pair):
+    """Engine variants that reorder only the schedule, not the arithmetic: the software-pipelined
+    256x128 main loop (variant 5, g4::gemm_kernel_pipe) against the 256x128 engine (4), and the
+    persistent streaming 256x256 engine (7, g2::gemm_kernel_s: tiles walked per CU, the next tile's
+    first K-steps fetched under the epilogue, 32-row staging) against the one-tile 256x256 engine
+    (2).  Same MFMAs in the same K order per accumulator and the same epilogue arithmetic: every
+    fused epilogue of the trainer (bf16 store, GELU pair, fp32 residual, x aux + column sums)
+    bit-identical, at the trainer's K (768, 3072), its M (50 432 = 197 full 256-row tiles: several
+    tiles per CU) and ragged M / N."""
+    v0, v1 = pair
     v = gpu
     L = v.lib()
     rng = np.random.default_rng(M + 3 * N + K)
@@ -413,7 +420,7 @@ def test_gemm_bf16_pipelined_bit_identical(gpu, M, N, K):
     aux = D(v, v.bf16_bits(rng.normal(size=(M, N)).astype(np.float32)), np.uint16)
     outs = {}
     try:
-        for var in (4, 5):
+        for var in (v0, v1):
             L.gemm_bf16_set_variant(var)
             o = {}
             for epi in (3, 5, 8, 9):
@@ -426,10 +433,10 @@ def test_gemm_bf16_pipelined_bit_identical(gpu, M, N, K):
             outs[var] = o
     finally:
         L.gemm_bf16_set_variant(2)
-    for epi in outs[4]:
-        for x, y in zip(outs[4][epi], outs[5][epi]):
+    for epi in outs[v0]:
+        for x, y in zip(outs[v0][epi], outs[v1][epi]):
             assert np.array_equal(x, y), epi
-    assert np.abs(outs[5][5][0]).max() > 0
+    assert np.abs(outs[v1][5][0]).max() > 0
 
 
 def _gelu64(x):

@@ -103,10 +103,10 @@ def main():
             L.vit_sync()
             L.gemm_bf16_set_trace(None)
             vit.check(name)
-            bm, bn = (256, 256) if var == 2 else (256, 128)
+            bm, bn = (256, 256) if var in (2, 7) else (256, 128)
             nwg = -(-M // bm) * -(-N // bn)
             tr = trace.numpy().reshape(-1, 16)[:nwg]
-            r = analyse(tr, 8 if var == 2 else 4)
+            r = analyse(tr, 8 if var in (2, 7) else 4)
             print(f"{name:13s} v{var} span {r['span_us']:7.1f} us  prologue {r['prologue_us']:5.2f}  main {r['main_us']:6.2f}  "
                   f"epi(last wave) {r['epi_us']:6.2f}  wave-end skew {r['wave_skew_us']:5.2f}  "
                   f"CUs {r['cus']}  wg/CU {r['wg_per_cu']:.1f}  resident {r['max_resident']}  "

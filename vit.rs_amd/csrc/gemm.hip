@@ -328,6 +328,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
+    first_round_stagger(p.stagger, true);
     trace_stamp(p, 0);
     const int ntm = cdiv(p.M, BM), ntn = cdiv(p.N, BN);
     int wg, split;
@@ -444,6 +445,143 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
     asm volatile("" ::: "memory");
     staged_epilogue<EPI>(p, acc, smem + wave * STG_WAVE_BYTES, lane, tm0 + wm * 128, tn0 + wn * 64, bpre);
     trace_stamp(p, 2);
+}
+
+// Persistent streaming form (variant 7; K-contiguous A and B: the forward and input-gradient
+// GEMMs, no split-K).  One workgroup per CU walks its tiles (round j: the tile the one-tile kernel
+// gives block j * 256 + blockIdx.x, so the XCD / L2 placement is unchanged) with the LDS-DMA ring
+// streaming across tile boundaries: the DMA of "step kt + 2" in a tile's last two steps fetches
+// the NEXT tile's steps 0 and 1, which land during this tile's epilogue.  The per-tile trace
+// (tools/gemm_trace.py) of the one-tile kernel showed ~3 us per tile from launch to the first
+// operands (every CU starting a tile at once) and the epilogue running with nothing else on the
+// CU.  The epilogue stages through the tile's last two slots (free once every wave has read them):
+// 8 KiB per wave, four 32-row passes (staged_epilogue_q), while the next tile's first two steps
+// sit in the other two.  Waits: before the epilogue vmcnt(0) retires the next tile's steps 0 and
+// 1 (so the epilogue's own loads and stores are never waited for by a wait meant for a DMA piece,
+// except in phase 1 of the next tile's second step, when those have long completed).  Same MFMA
+// order per accumulator and the same epilogue arithmetic as gemm_kernel: bit-identical outputs.
+template <int EPI>
+__global__ __launch_bounds__(NT, 1) void gemm_kernel_s(GemmParams p) {
+    constexpr int NS = 4;  // DMA two steps ahead
+    __shared__ __attribute__((aligned(1024))) char smem[NS * SLOT_BYTES];
+    static_assert(8 * 8192 <= 2 * SLOT_BYTES, "epilogue staging: two slots");
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int ntm = cdiv(p.M, BM), ntn = cdiv(p.N, BN), tiles = ntm * ntn;
+    const int nblk = gridDim.x;
+    const int my_tiles = (tiles - (int)blockIdx.x + nblk - 1) / nblk;
+    const int nk = p.K / BK;
+    const bf16_t* A = (const bf16_t*)p.A;
+    const bf16_t* B = (const bf16_t*)p.B;
+    auto tile_of = [&](int j, int& tm0, int& tn0, int& t) {
+        t = xcd_remap(j * nblk + (int)blockIdx.x, tiles);
+        tm0 = (t / ntn) * BM;
+        tn0 = (t % ntn) * BN;
+    };
+    f32x4_t acc[8][4];
+    auto zero_acc = [&]() {
+#pragma unroll
+        for (int a = 0; a < 8; a++)
+#pragma unroll
+            for (int b = 0; b < 4; b++) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    };
+    zero_acc();
+    auto slot_of = [&](long long gs) { return smem + (int)(gs % NS) * SLOT_BYTES; };
+    auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto mfma_half = [&](int half, const bf16x8_t (&fa)[4], const bf16x8_t (&fb)[4]) {
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+                acc[half * 4 + a][b] =
+                    __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[b], fa[a], acc[half * 4 + a][b], 0, 0, 0);
+    };
+    if (my_tiles <= 0) return;
+    const long long total = (long long)my_tiles * nk;
+    int tm0, tn0, tcur, tm1 = 0, tn1 = 0, tnext = 0;
+    tile_of(0, tm0, tn0, tcur);
+    if (my_tiles > 1) tile_of(1, tm1, tn1, tnext);
+    // A / B pieces of step kt2 counted from the current tile's start (kt2 >= nk: the next tile's)
+    auto issue_a = [&](long long gs, int kt2) {
+        if (kt2 < nk) stage<true>(A, p.lda, tm0, p.M, kt2 * BK, slot_of(gs), wave, lane);
+        else if (gs < total) stage<true>(A, p.lda, tm1, p.M, (kt2 - nk) * BK, slot_of(gs), wave, lane);
+    };
+    auto issue_b = [&](long long gs, int kt2) {
+        if (kt2 < nk) stage<true>(B, p.ldb, tn0, p.N, kt2 * BK, slot_of(gs) + IMG_BYTES, wave, lane);
+        else if (gs < total) stage<true>(B, p.ldb, tn1, p.N, (kt2 - nk) * BK, slot_of(gs) + IMG_BYTES, wave, lane);
+    };
+    const bool lagging = wave >= 4;
+    issue_a(0, 0); issue_b(0, 0);
+    issue_a(1, 1); issue_b(1, 1);
+    if (total > 1) wait_vm(4);
+    else wait_vm(0);
+    long long gs = 0;
+    bf16x8_t fb[4], alo[4], ahi[4];
+    for (int j = 0; j < my_tiles; j++) {
+        if (p.trace && tid == 0) p.trace[(long long)tcur * TRACE_WORDS] = __builtin_amdgcn_s_memrealtime();
+        bar();
+        if (lagging) {
+            __builtin_amdgcn_s_setprio(1);
+            bar();
+        }
+        for (int kt = 0; kt < nk; kt++, gs++) {
+            const char* img = slot_of(gs);
+            // ---- phase 0
+#pragma unroll
+            for (int b = 0; b < 4; b++) fb[b] = frag<true>(img + IMG_BYTES, wn * 64 + b * 16, lane);
+#pragma unroll
+            for (int a = 0; a < 4; a++) alo[a] = frag<true>(img, wm * 128 + a * 16, lane);
+            issue_a(gs + 2, kt + 2);
+            bar();
+            mfma_half(0, alo, fb);
+            bar();
+            // ---- phase 1
+#pragma unroll
+            for (int a = 0; a < 4; a++) ahi[a] = frag<true>(img, wm * 128 + (4 + a) * 16, lane);
+            // own pieces of step gs+1 landed (the A half of gs+2 stays in flight); in a later
+            // tile's first step they were retired before the previous epilogue
+            if (!(j > 0 && kt == 0)) wait_vm(gs + 2 < total ? 2 : 0);
+            issue_b(gs + 2, kt + 2);
+            bar();
+            mfma_half(1, ahi, fb);
+            bar();
+        }
+        if (!lagging) bar();  // balance the stagger barrier
+        if (p.trace && (tid & 63) == 0 && wave == 0) p.trace[(long long)tcur * TRACE_WORDS + 1] = __builtin_amdgcn_s_memrealtime();
+        float bpre[8];
+        staged_bias_prefetch<EPI>(p, lane, tn0 + wn * 64, bpre);
+        // the next tile's steps 0 and 1 (and the bias) landed; every wave's reads of this tile's
+        // last two slots done before they become staging space
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (!skip_epilogue(p, acc)) {
+            char* stg = (wave < 4 ? slot_of(gs - 2) : slot_of(gs - 1)) + (wave & 3) * 8192;
+            staged_epilogue_q<EPI>(p, acc, reinterpret_cast<float*>(stg), lane, tm0 + wm * 128, tn0 + wn * 64, bpre);
+        }
+        if (p.trace && (tid & 63) == 0) {
+            const long long rec = (long long)tcur * TRACE_WORDS;
+            const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+            p.trace[rec + 4 + wave] = t;
+            if (wave == 0) {
+                p.trace[rec + 2] = t;
+                p.trace[rec + 3] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+                                   __builtin_amdgcn_s_getreg((31 << 11) | 4);
+                p.trace[rec + 12] = p.trace[rec];
+            }
+        }
+        zero_acc();
+        tm0 = tm1; tn0 = tn1; tcur = tnext;
+        if (j + 2 < my_tiles) tile_of(j + 2, tm1, tn1, tnext);
+    }
 }
 
 }  // namespace g2
@@ -1012,11 +1150,12 @@ __global__ __launch_bounds__(256) void slab_reduce_k(float* __restrict__ C, long
 // engine selection (gemm_bf16_set_variant; default from VIT_GEMM, else 2):
 //   1 = 128x128 register-staged everywhere, 2 = production (256x256 one workgroup per CU; split-K
 //   weight gradients on 256x128), 4 = 256x128 two per CU everywhere, 5 = as 4 with the
-//   software-pipelined main loop (g4::gemm_kernel_pipe) for K-contiguous operands.  Debug flag 2 skips the
+//   software-pipelined main loop (g4::gemm_kernel_pipe) for K-contiguous operands, 7 = as 2 with
+//   the persistent streaming 256x256 engine (g2::gemm_kernel_s) for K-contiguous operands.  Debug flag 2 skips the
 //   epilogues (main-loop-only timing; results are garbage).
 static int g_variant = -1;
 static int g_debug_flags = 0;
-static bool known_variant(int v) { return v == 1 || v == 2 || v == 4 || v == 5; }
+static bool known_variant(int v) { return v == 1 || v == 2 || v == 4 || v == 5 || v == 7; }
 static int gemm_variant() {
     if (g_variant < 0) {
         const char* e = getenv("VIT_GEMM");
@@ -1160,6 +1299,26 @@ static void launch_bf16(const GemmArgs& a, const GemmParams& p, dim3 grid, hipSt
 
 template <bool AK, bool BKC>
 static void launch_g2(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStream_t s) {
+    if constexpr (AK && BKC) {
+        // persistent streaming engine: one workgroup per CU (at most one per tile), no split-K
+        if (gemm_variant() == 7 && grid.y == 1) {
+            const dim3 pg(grid.x < 256 ? grid.x : 256);
+            switch (a.epi) {
+#define VIT_CASE(E) \
+    case E: g2::gemm_kernel_s<E><<<pg, g2::NT, 0, s>>>(p); return;
+                VIT_CASE(EPI_F32_STORE)
+                VIT_CASE(EPI_F32_ACC)
+                VIT_CASE(EPI_BF16_STORE)
+                VIT_CASE(EPI_BF16_GELU)
+                VIT_CASE(EPI_F32_RESID)
+                VIT_CASE(EPI_BF16_DGELU)
+                VIT_CASE(EPI_BF16_GELU_D)
+                VIT_CASE(EPI_BF16_MUL)
+#undef VIT_CASE
+                default: break;
+            }
+        }
+    }
     switch (a.epi) {
 #define VIT_CASE(E) \
     case E: g2::gemm_kernel<AK, BKC, E, 2><<<grid, g2::NT, 0, s>>>(p); break;
@@ -1292,7 +1451,7 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s) {
     // split-K weight gradients (M/N-contiguous operands, K = the token count) run on the 256x128
     // two-per-CU engine: 3-9 % faster than 256x256 on every ViT-B/16 wgrad shape (r02,
     // tools/bench_gemm.py), the other GEMMs are faster on 256x256
-    if (gemm_variant() == 2 && a.epi == EPI_F32_ATOMIC && !a.a_kcontig && !a.b_kcontig &&
+    if ((gemm_variant() == 2 || gemm_variant() == 7) && a.epi == EPI_F32_ATOMIC && !a.a_kcontig && !a.b_kcontig &&
         a.K % g4::KTILE == 0 && a.M >= 256 && a.N >= 128 && a.N % 4 == 0 &&
         (a.splitk > 0 || !a.ws ||
          (size_t)choose_split_g4(cdiv(a.M, g4::BM) * cdiv(a.N, g4::BN), a.K / g4::KTILE) * a.M * a.N * sizeof(float) <=

@@ -120,10 +120,12 @@ __device__ __forceinline__ epi_u32x4 epi_ld16(const GemmParams&, const void* q) 
 // each CU in the first round by about half a tile keeps the pair half a tile apart for the whole
 // launch (a finishing workgroup's successor starts at once), so one's epilogue runs beside the
 // other's main loop.
-__device__ __forceinline__ void first_round_stagger(int ticks) {
+// one_per_cu (256x256 engine): delay every other CU of each XCD in the first round instead (the
+// CUs then reach their epilogues' store bursts at different times)
+__device__ __forceinline__ void first_round_stagger(int ticks, bool one_per_cu = false) {
     if (ticks <= 0) return;
     const int lin = blockIdx.y * gridDim.x + blockIdx.x;
-    if (lin < 256 || lin >= 512) return;
+    if (one_per_cu ? (lin >= 256 || !((lin >> 3) & 1)) : (lin < 256 || lin >= 512)) return;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)ticks) __builtin_amdgcn_s_sleep(8);
 }
@@ -583,6 +585,159 @@ __device__ __forceinline__ void staged_epilogue(const GemmParams& p, f32x4_t (&a
         for (int pass = 0; pass < 2; pass++) {
             stage_pass(pass);
             staged_pass<EPI>(p, st, lane, m0, n0, pass, interior, cs, bpre);
+        }
+    }
+    staged_colsum<EPI>(p, lane, m0, n0, cs);
+}
+
+// ------------------------------------------------ 32-row swizzled staging (persistent 256x256 engine)
+// The persistent engine stages a wave's 128 x 64 accumulator tile in four 32-row passes through 8 KiB
+// of LDS (two free ring slots hold the eight waves), 64 fp32 per row with the 16-B chunk index XORed
+// with (row & 15): the accumulator writes (8 rows x one chunk per ds_write_b128 lane group) and the
+// row reads (lane (rr, cc): row 8 it + rr, chunks cc/4 and cc/4 + 1) hit distinct banks.
+__device__ __forceinline__ int sq_off(int r, int col) {
+    return r * 64 + ((((col >> 2) ^ (r & 15)) << 2) | (col & 3));
+}
+template <int EPI>
+struct EpiAuxQ {  // aux operand rows of one interior 32-row pass (rows mrow + 8 it + rr, it < 4)
+    static constexpr bool AUX16 = epi_aux16(EPI);
+    static constexpr bool AUX32 = EPI == EPI_F32_RESID || EPI == EPI_F32_ACC;
+    static constexpr int N = AUX16 ? 4 : (AUX32 ? 8 : 0);
+    epi_u32x4v ax[N > 0 ? N : 1];
+    __device__ __forceinline__ void load(const GemmParams& p, int rr, int mrow, int n) {
+        if constexpr (AUX16) {
+#pragma unroll
+            for (int it = 0; it < 4; it++)
+                ax[it] = epi_ld16(p, (const bf16_t*)p.aux + (long long)(mrow + it * 8 + rr) * p.ldaux + n);
+        } else if constexpr (AUX32) {
+            const float* src = EPI == EPI_F32_RESID ? (const float*)p.aux : (const float*)p.C;
+            const long long ld = EPI == EPI_F32_RESID ? p.ldaux : p.ldc;
+#pragma unroll
+            for (int it = 0; it < 4; it++) {
+                const float* q = src + (long long)(mrow + it * 8 + rr) * ld + n;
+                ax[2 * it] = epi_ld16(p, q);
+                ax[2 * it + 1] = epi_ld16(p, q + 4);
+            }
+        }
+    }
+};
+// one interior 32-row pass (all rows < M, all 64 columns < N): bf16-engine epilogues (no MX outputs)
+template <int EPI>
+__device__ __forceinline__ void staged_pass_interior_q(const GemmParams& p, const float* st, int rr, int cc,
+                                                       int mrow, int n, float (&cs)[8], const float* bv,
+                                                       const EpiAuxQ<EPI>& aux) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    constexpr bool AUX16 = epi_aux16(EPI);
+    constexpr bool AUX32 = EPI == EPI_F32_RESID || EPI == EPI_F32_ACC;
+#pragma unroll
+    for (int it = 0; it < 4; it++) {
+        const int r = it * 8 + rr;
+        const f32x4_t lo = *reinterpret_cast<const f32x4_t*>(st + sq_off(r, cc));
+        const f32x4_t hi = *reinterpret_cast<const f32x4_t*>(st + sq_off(r, cc + 4));
+        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const long long off = (long long)(mrow + r) * p.ldc + n;
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] += bv[j];
+        auto pack8 = [](const float (&w)[8]) {
+            return u32x4{pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3]), pack_bf16x2(w[4], w[5]),
+                         pack_bf16x2(w[6], w[7])};
+        };
+        auto st_f32 = [&](float* q) {
+            epi_st16(p, q, u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])});
+            epi_st16(p, q + 4, u32x4{__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7])});
+        };
+        if constexpr (EPI == EPI_F32_STORE) {
+            st_f32((float*)p.C + off);
+        } else if constexpr (AUX32) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                v[j] += __uint_as_float(aux.ax[2 * it][j]);
+                v[4 + j] += __uint_as_float(aux.ax[2 * it + 1][j]);
+            }
+            st_f32((float*)p.C + off);
+        } else if constexpr (EPI == EPI_BF16_STORE) {
+            epi_st16(p, (bf16_t*)p.C + off, pack8(v));
+        } else if constexpr (EPI == EPI_BF16_GELU) {
+            float gv[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) gv[j] = gelu_fast_f(v[j]);
+            epi_st16(p, (bf16_t*)p.C + off, pack8(v));
+            if (p.C2) epi_st16(p, (bf16_t*)p.C2 + off, pack8(gv));
+        } else if constexpr (EPI == EPI_BF16_GELU_D) {
+            float gv[8], dv[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) gelu_pair_fast_f(v[j], gv[j], dv[j]);
+            epi_st16(p, (bf16_t*)p.C + off, pack8(dv));
+            if (p.C2) epi_st16(p, (bf16_t*)p.C2 + off, pack8(gv));
+        } else if constexpr (AUX16) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const float a0 = __uint_as_float(aux.ax[it][j] << 16), a1 = __uint_as_float(aux.ax[it][j] & 0xffff0000u);
+                if constexpr (EPI == EPI_BF16_DGELU) {
+                    v[2 * j] *= gelu_grad_fast_f(a0);
+                    v[2 * j + 1] *= gelu_grad_fast_f(a1);
+                } else {
+                    v[2 * j] *= a0;
+                    v[2 * j + 1] *= a1;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++) cs[j] += v[j];
+            if (p.C) epi_st16(p, (bf16_t*)p.C + off, pack8(v));
+        }
+    }
+}
+// Epilogue of one wave's 128 x 64 tile through 8 KiB of swizzled staging (four 32-row passes); the
+// interior form loads the next pass's aux rows under the current pass.  Same outputs, bit for bit,
+// as staged_epilogue (same values, same column-sum order: the cs partials add the tile's rows in the
+// same order per lane, rows 8 it + rr of pass 0..3 = rows 8 it' + rr of the 64-row passes).
+template <int EPI>
+__device__ __forceinline__ void staged_epilogue_q(const GemmParams& p, f32x4_t (&acc)[8][4], float* st, int lane,
+                                                  int m0, int n0, const float* bpre) {
+    const int i = lane & 15, g = lane >> 4;
+    const int rr = lane >> 3, cc = (lane & 7) * 8, n = n0 + cc;
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    auto stage_pass = [&](int pass) {
+#pragma unroll
+        for (int a = 0; a < 2; a++)
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+                *reinterpret_cast<f32x4_t*>(st + sq_off(a * 16 + i, b * 16 + 4 * g)) = acc[pass * 2 + a][b];
+    };
+    if (staged_interior<EPI>(p, m0, n0)) {
+        EpiAuxQ<EPI> a0, a1;
+        a0.load(p, rr, m0, n);
+#pragma unroll
+        for (int pass = 0; pass < 4; pass += 2) {
+            a1.load(p, rr, m0 + (pass + 1) * 32, n);
+            stage_pass(pass);
+            staged_pass_interior_q<EPI>(p, st, rr, cc, m0 + pass * 32, n, cs, bpre, a0);
+            if (pass + 2 < 4) a0.load(p, rr, m0 + (pass + 2) * 32, n);
+            stage_pass(pass + 1);
+            staged_pass_interior_q<EPI>(p, st, rr, cc, m0 + (pass + 1) * 32, n, cs, bpre, a1);
+        }
+    } else {
+#pragma unroll
+        for (int pass = 0; pass < 4; pass++) {
+            stage_pass(pass);
+#pragma unroll
+            for (int it = 0; it < 4; it++) {
+                const int r = it * 8 + rr;
+                const f32x4_t lo = *reinterpret_cast<const f32x4_t*>(st + sq_off(r, cc));
+                const f32x4_t hi = *reinterpret_cast<const f32x4_t*>(st + sq_off(r, cc + 4));
+                float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                const int m = m0 + pass * 32 + r;
+                if (m >= p.M) continue;
+                if (n + 8 <= p.N) {
+                    epilogue8<EPI>(p, m, n, v, cs, lane, nullptr);
+                } else if (n + 4 <= p.N) {
+                    f32x4_t t = lo;
+                    epilogue<EPI>(p, m, n, t);
+                    if constexpr (epi_aux16(EPI)) {
+                        cs[0] += t[0]; cs[1] += t[1]; cs[2] += t[2]; cs[3] += t[3];
+                    }
+                }
+            }
         }
     }
     staged_colsum<EPI>(p, lane, m0, n0, cs);
