@@ -472,13 +472,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_s(GemmParams p) {
     const int nblk = gridDim.x;
     const int my_tiles = (tiles - (int)blockIdx.x + nblk - 1) / nblk;
     const int nk = p.K / BK;
-    const bf16_t* A = (const bf16_t*)p.A;
-    const bf16_t* B = (const bf16_t*)p.B;
-    auto tile_of = [&](int j, int& tm0, int& tn0, int& t) {
-        t = xcd_remap(j * nblk + (int)blockIdx.x, tiles);
-        tm0 = (t / ntn) * BM;
-        tn0 = (t % ntn) * BN;
-    };
+    const char* A = (const char*)p.A;
+    const char* B = (const char*)p.B;
     f32x4_t acc[8][4];
     auto zero_acc = [&]() {
 #pragma unroll
@@ -487,7 +482,52 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_s(GemmParams p) {
             for (int b = 0; b < 4; b++) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     };
     zero_acc();
-    auto slot_of = [&](long long gs) { return smem + (int)(gs % NS) * SLOT_BYTES; };
+    if (my_tiles <= 0) return;
+    first_round_stagger(p.stagger, true);
+    // the lane's DMA source of piece j of the A / B image of a tile, as a 32-bit byte offset from
+    // the operand base at k = 0 (K-contiguous image: as stage<true>; host: M*lda, N*ldb < 2^31)
+    struct TileSrc {
+        int tm0, tn0, t;
+        uint32_t a[2], b[2];
+    };
+    auto tile_src = [&](int j, TileSrc& ts) {
+        ts.t = xcd_remap(j * nblk + (int)blockIdx.x, tiles);
+        ts.tm0 = (ts.t / ntn) * BM;
+        ts.tn0 = (ts.t % ntn) * BN;
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const int row = (q * 8 + wave) * 16 + (lane >> 2);
+            const int c = (lane & 3) ^ kc_swz(row);
+            ts.a[q] = (uint32_t)((min(ts.tm0 + row, p.M - 1) * p.lda + c * 8) * 2);
+            ts.b[q] = (uint32_t)((min(ts.tn0 + row, p.N - 1) * p.ldb + c * 8) * 2);
+        }
+    };
+    TileSrc cur, nxt;
+    tile_src(0, cur);
+    nxt = cur;
+    if (my_tiles > 1) tile_src(1, nxt);
+    auto glds = [&](const char* src, char* dst) {
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    };
+    // A / B pieces of step kt2 of the current tile (kt2 >= nk: step kt2 - nk of the next one, if
+    // this workgroup has one) into slot sl
+    auto issue_a = [&](int kt2, int sl, bool more) {
+        if (kt2 >= nk && !more) return;
+        const bool c = kt2 < nk;
+        const char* base = A + (long long)(c ? kt2 : kt2 - nk) * (BK * 2);
+        char* dst = smem + sl * SLOT_BYTES;
+#pragma unroll
+        for (int q = 0; q < 2; q++) glds(base + (c ? cur.a[q] : nxt.a[q]), dst + (q * 8 + wave) * 1024);
+    };
+    auto issue_b = [&](int kt2, int sl, bool more) {
+        if (kt2 >= nk && !more) return;
+        const bool c = kt2 < nk;
+        const char* base = B + (long long)(c ? kt2 : kt2 - nk) * (BK * 2);
+        char* dst = smem + sl * SLOT_BYTES + IMG_BYTES;
+#pragma unroll
+        for (int q = 0; q < 2; q++) glds(base + (c ? cur.b[q] : nxt.b[q]), dst + (q * 8 + wave) * 1024);
+    };
     auto bar = [&]() {
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -502,61 +542,59 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_s(GemmParams p) {
             for (int b = 0; b < 4; b++)
                 acc[half * 4 + a][b] =
                     __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[b], fa[a], acc[half * 4 + a][b], 0, 0, 0);
-    };
-    if (my_tiles <= 0) return;
-    const long long total = (long long)my_tiles * nk;
-    int tm0, tn0, tcur, tm1 = 0, tn1 = 0, tnext = 0;
-    tile_of(0, tm0, tn0, tcur);
-    if (my_tiles > 1) tile_of(1, tm1, tn1, tnext);
-    // A / B pieces of step kt2 counted from the current tile's start (kt2 >= nk: the next tile's)
-    auto issue_a = [&](long long gs, int kt2) {
-        if (kt2 < nk) stage<true>(A, p.lda, tm0, p.M, kt2 * BK, slot_of(gs), wave, lane);
-        else if (gs < total) stage<true>(A, p.lda, tm1, p.M, (kt2 - nk) * BK, slot_of(gs), wave, lane);
-    };
-    auto issue_b = [&](long long gs, int kt2) {
-        if (kt2 < nk) stage<true>(B, p.ldb, tn0, p.N, kt2 * BK, slot_of(gs) + IMG_BYTES, wave, lane);
-        else if (gs < total) stage<true>(B, p.ldb, tn1, p.N, (kt2 - nk) * BK, slot_of(gs) + IMG_BYTES, wave, lane);
+        // the phase's MFMAs stay in front of the barrier that closes it: hipcc's instruction
+        // selection otherwise sank 10 of the 16 past it (the wave then reached the barrier early
+        // and its partner's read phase overlapped its own MFMAs).  An empty asm naming the 16
+        // accumulators orders them; it emits nothing and reads nothing.
+        f32x4_t* q = &acc[half * 4][0];
+        asm volatile("" ::"v"(q[0]), "v"(q[1]), "v"(q[2]), "v"(q[3]), "v"(q[4]), "v"(q[5]), "v"(q[6]), "v"(q[7]),
+                     "v"(q[8]), "v"(q[9]), "v"(q[10]), "v"(q[11]), "v"(q[12]), "v"(q[13]), "v"(q[14]), "v"(q[15]));
     };
     const bool lagging = wave >= 4;
-    issue_a(0, 0); issue_b(0, 0);
-    issue_a(1, 1); issue_b(1, 1);
-    if (total > 1) wait_vm(4);
-    else wait_vm(0);
-    long long gs = 0;
+    issue_a(0, 0, false); issue_b(0, 0, false);
+    issue_a(1, 1, my_tiles > 1); issue_b(1, 1, my_tiles > 1);  // nk >= 2 (K % 64 == 0)
+    wait_vm(4);
+    int sl = 0;  // slot of the step being read (global step % 4)
     bf16x8_t fb[4], alo[4], ahi[4];
     for (int j = 0; j < my_tiles; j++) {
-        if (p.trace && tid == 0) p.trace[(long long)tcur * TRACE_WORDS] = __builtin_amdgcn_s_memrealtime();
+        const bool more = j + 1 < my_tiles;
+        if (p.trace && tid == 0) p.trace[(long long)cur.t * TRACE_WORDS] = __builtin_amdgcn_s_memrealtime();
         bar();
         if (lagging) {
             __builtin_amdgcn_s_setprio(1);
             bar();
         }
-        for (int kt = 0; kt < nk; kt++, gs++) {
-            const char* img = slot_of(gs);
+        for (int kt = 0; kt < nk; kt++) {
+            const char* img = smem + sl * SLOT_BYTES;
+            const int sl2 = (sl + 2) & 3;
             // ---- phase 0
 #pragma unroll
             for (int b = 0; b < 4; b++) fb[b] = frag<true>(img + IMG_BYTES, wn * 64 + b * 16, lane);
 #pragma unroll
             for (int a = 0; a < 4; a++) alo[a] = frag<true>(img, wm * 128 + a * 16, lane);
-            issue_a(gs + 2, kt + 2);
+            issue_a(kt + 2, sl2, more);
             bar();
             mfma_half(0, alo, fb);
             bar();
             // ---- phase 1
 #pragma unroll
             for (int a = 0; a < 4; a++) ahi[a] = frag<true>(img, wm * 128 + (4 + a) * 16, lane);
-            // own pieces of step gs+1 landed (the A half of gs+2 stays in flight); in a later
-            // tile's first step they were retired before the previous epilogue
-            if (!(j > 0 && kt == 0)) wait_vm(gs + 2 < total ? 2 : 0);
-            issue_b(gs + 2, kt + 2);
+            // own pieces of the next step landed (the A half of the one after stays in flight); in a
+            // later tile's first step they were retired before the previous epilogue
+            if (kt > 0 || j == 0) {
+                if (kt + 2 < nk || more) wait_vm(2);
+                else wait_vm(0);
+            }
+            issue_b(kt + 2, sl2, more);
             bar();
             mfma_half(1, ahi, fb);
             bar();
+            sl = (sl + 1) & 3;
         }
         if (!lagging) bar();  // balance the stagger barrier
-        if (p.trace && (tid & 63) == 0 && wave == 0) p.trace[(long long)tcur * TRACE_WORDS + 1] = __builtin_amdgcn_s_memrealtime();
+        if (p.trace && tid == 0) p.trace[(long long)cur.t * TRACE_WORDS + 1] = __builtin_amdgcn_s_memrealtime();
         float bpre[8];
-        staged_bias_prefetch<EPI>(p, lane, tn0 + wn * 64, bpre);
+        staged_bias_prefetch<EPI>(p, lane, cur.tn0 + wn * 64, bpre);
         // the next tile's steps 0 and 1 (and the bias) landed; every wave's reads of this tile's
         // last two slots done before they become staging space
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -564,23 +602,24 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_s(GemmParams p) {
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         if (!skip_epilogue(p, acc)) {
-            char* stg = (wave < 4 ? slot_of(gs - 2) : slot_of(gs - 1)) + (wave & 3) * 8192;
-            staged_epilogue_q<EPI>(p, acc, reinterpret_cast<float*>(stg), lane, tm0 + wm * 128, tn0 + wn * 64, bpre);
+            // this tile's last two steps were in slots sl - 1, sl - 2 (mod 4)
+            char* stg = smem + ((wave < 4 ? sl + 2 : sl + 3) & 3) * SLOT_BYTES + (wave & 3) * 8192;
+            staged_epilogue_q<EPI>(p, acc, reinterpret_cast<float*>(stg), lane, cur.tm0 + wm * 128,
+                                   cur.tn0 + wn * 64, bpre);
         }
         if (p.trace && (tid & 63) == 0) {
-            const long long rec = (long long)tcur * TRACE_WORDS;
+            const long long rec = (long long)cur.t * TRACE_WORDS;
             const unsigned long long t = __builtin_amdgcn_s_memrealtime();
             p.trace[rec + 4 + wave] = t;
             if (wave == 0) {
                 p.trace[rec + 2] = t;
                 p.trace[rec + 3] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
                                    __builtin_amdgcn_s_getreg((31 << 11) | 4);
-                p.trace[rec + 12] = p.trace[rec];
             }
         }
         zero_acc();
-        tm0 = tm1; tn0 = tn1; tcur = tnext;
-        if (j + 2 < my_tiles) tile_of(j + 2, tm1, tn1, tnext);
+        cur = nxt;
+        if (j + 2 < my_tiles) tile_src(j + 2, nxt);
     }
 }
 
@@ -1301,7 +1340,8 @@ template <bool AK, bool BKC>
 static void launch_g2(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStream_t s) {
     if constexpr (AK && BKC) {
         // persistent streaming engine: one workgroup per CU (at most one per tile), no split-K
-        if (gemm_variant() == 7 && grid.y == 1) {
+        if (gemm_variant() == 7 && grid.y == 1 && (long long)p.M * p.lda * 2 < (1LL << 31) &&
+            (long long)p.N * p.ldb * 2 < (1LL << 31)) {
             const dim3 pg(grid.x < 256 ? grid.x : 256);
             switch (a.epi) {
 #define VIT_CASE(E) \
