@@ -229,9 +229,11 @@ void gemm_fp8_fused_mxc(void* C, void* C2, long long ldc, const void* aux, long 
                         long long ldb, const float* bias, float* colsum_out, int M, int N, int K, int epi,
                         uint8_t* mx_q, uint8_t* mx_s, uint8_t* mxc_q, uint8_t* mxc_s, long long mxc_ld,
                         long long mxc_off);
-/* tools: GEMM engine selection (1 = 128x128 everywhere, 2 = production: 256x256 one workgroup per
- * CU with the split-K weight gradients on 256x128, 4 = 256x128 two per CU everywhere) and
- * diagnostics (flag 2: skip epilogues, main-loop timing only) */
+/* tools: GEMM engine selection (0 = the default; 1 = 128x128 everywhere, 2 = 256x256 one tile per
+ * workgroup with the split-K weight gradients on 256x128, 4 = 256x128 two per CU everywhere,
+ * 5 = 4 with a software-pipelined main loop, 7 = production: 2 with the persistent streaming
+ * 256x256 engine for the K-contiguous GEMMs) and diagnostics (flag 2: skip epilogues, main-loop
+ * timing only; flags >> 8: first-round stagger in 0.5 us units) */
 void gemm_bf16_set_variant(int variant);
 void gemm_bf16_set_debug(int flags);
 /* diagnostic: per-workgroup timestamps of the 256x256 / 256x128 bf16 engines into trace (device,

@@ -363,7 +363,7 @@ def engine(request, gpu):
     software-pipelined main loop for K-contiguous operands), then restore the default."""
     gpu.lib().gemm_bf16_set_variant(request.param)
     yield request.param
-    gpu.lib().gemm_bf16_set_variant(2)
+    gpu.lib().gemm_bf16_set_variant(0)
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (304, 520, 128), (776, 1000, 192), (512, 264, 640),
@@ -432,7 +432,7 @@ def test_gemm_bf16_pipelined_bit_identical(gpu, M, N, K, pair):
                 o[epi] = [c.numpy()] + ([c2.numpy()] if c2 is not None else []) + ([cs.numpy()] if cs is not None else [])
             outs[var] = o
     finally:
-        L.gemm_bf16_set_variant(2)
+        L.gemm_bf16_set_variant(0)
     for epi in outs[v0]:
         for x, y in zip(outs[v0][epi], outs[v1][epi]):
             assert np.array_equal(x, y), epi

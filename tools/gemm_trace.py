@@ -113,7 +113,7 @@ def main():
                   f"epi beside other's main loop {r['epi_overlap']:.2f}  turnaround {r['turnaround_us']:.2f} us",
                   flush=True)
     L.gemm_bf16_set_debug(0)
-    L.gemm_bf16_set_variant(2)
+    L.gemm_bf16_set_variant(0)
 
 
 if __name__ == "__main__":

@@ -1186,24 +1186,27 @@ __global__ __launch_bounds__(256) void slab_reduce_k(float* __restrict__ C, long
     }
 }
 
-// engine selection (gemm_bf16_set_variant; default from VIT_GEMM, else 2):
-//   1 = 128x128 register-staged everywhere, 2 = production (256x256 one workgroup per CU; split-K
-//   weight gradients on 256x128), 4 = 256x128 two per CU everywhere, 5 = as 4 with the
-//   software-pipelined main loop (g4::gemm_kernel_pipe) for K-contiguous operands, 7 = as 2 with
-//   the persistent streaming 256x256 engine (g2::gemm_kernel_s) for K-contiguous operands.  Debug flag 2 skips the
+// engine selection (gemm_bf16_set_variant; default from VIT_GEMM, else 7):
+//   1 = 128x128 register-staged everywhere, 2 = 256x256 one workgroup per CU (one tile per
+//   workgroup; split-K weight gradients on 256x128), 4 = 256x128 two per CU everywhere, 5 = as 4
+//   with the software-pipelined main loop (g4::gemm_kernel_pipe) for K-contiguous operands,
+//   7 = production: as 2 with the persistent streaming 256x256 engine (g2::gemm_kernel_s) for the
+//   K-contiguous GEMMs without split-K.  Debug flag 2 skips the
 //   epilogues (main-loop-only timing; results are garbage).
 static int g_variant = -1;
 static int g_debug_flags = 0;
 static bool known_variant(int v) { return v == 1 || v == 2 || v == 4 || v == 5 || v == 7; }
+static constexpr int kDefaultVariant = 7;
 static int gemm_variant() {
     if (g_variant < 0) {
         const char* e = getenv("VIT_GEMM");
-        g_variant = e ? atoi(e) : 2;
-        if (!known_variant(g_variant)) g_variant = 2;
+        g_variant = e ? atoi(e) : kDefaultVariant;
+        if (!known_variant(g_variant)) g_variant = kDefaultVariant;
     }
     return g_variant;
 }
-void gemm_set_variant(int v) { g_variant = known_variant(v) ? v : 2; }
+// 0 (or any unknown value) restores the default
+void gemm_set_variant(int v) { g_variant = known_variant(v) ? v : kDefaultVariant; }
 void gemm_set_debug(int flags) { g_debug_flags = flags; }
 static unsigned long long* g_trace = nullptr;
 void gemm_set_trace(unsigned long long* trace) { g_trace = trace; }
