@@ -161,3 +161,24 @@ def test_production_dp_shard_sum(gpu, ref, prec_name):
     if prec == v.VIT_BF16:
         assert hits[v.HIT_GEMM_128:v.HIT_GEMM_128 + 16].sum() == 0, "128x128 fallback ran"
         assert hits[v.HIT_ATTN_BWD_PERSISTENT] == 2 * cfg.num_layers
+
+
+@pytest.mark.parametrize("prec_name", ["VIT_BF16", "VIT_FP8"])
+def test_production_streaming_engines_bit_identical(gpu, ref, prec_name):
+    """The persistent streaming GEMM engines (the production variant 7: g2::gemm_kernel_s for bf16,
+    f8::gemm_kernel_s for MXFP8 with its fused row / column MX outputs) against the one-tile engines
+    (variant 2) on the whole production step (2 micro-batch streams): loss, logits and every gradient
+    bit-identical — same MFMAs in the same order, same epilogue arithmetic."""
+    v = gpu
+    prec = getattr(v, prec_name)
+    out = {}
+    try:
+        for var in (2, 0):
+            v.lib().gemm_bf16_set_variant(var)
+            out[var] = _run(v, ref, prec, 2)
+    finally:
+        v.lib().gemm_bf16_set_variant(0)
+    (l2, z2, g2, _), (l7, z7, g7, _) = out[2], out[0]
+    assert l2 == l7
+    assert np.array_equal(z2, z7)
+    assert np.array_equal(g2, g7)

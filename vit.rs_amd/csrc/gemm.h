@@ -95,6 +95,7 @@ bool gemm_bf16_supported(const GemmArgs& a);
 void gemm_set_variant(int v);
 void gemm_set_debug(int flags);
 void gemm_set_trace(unsigned long long* trace);
+bool gemm_streaming();  // the production variant: persistent streaming engines (bf16 and fp8)
 
 // fp8 (OCP e4m3) operands with MX block scales (one E8M0 per 32 k-elements), fp32 accumulate
 // (v_mfma_scale_f32_32x32x64_f8f6f4): A [M][K], B [N][K] K-contiguous byte rows (lda/ldb in

@@ -618,7 +618,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_s(GemmParams p) {
             }
         }
         zero_acc();
-        cur = nxt;
+        // recomputed rather than carried: nothing of the next tiles' sources stays live through the epilogue
+        if (more) tile_src(j + 1, cur);
         if (j + 2 < my_tiles) tile_src(j + 2, nxt);
     }
 }
@@ -1207,6 +1208,7 @@ static int gemm_variant() {
 }
 // 0 (or any unknown value) restores the default
 void gemm_set_variant(int v) { g_variant = known_variant(v) ? v : kDefaultVariant; }
+bool gemm_streaming() { return gemm_variant() == 7; }
 void gemm_set_debug(int flags) { g_debug_flags = flags; }
 static unsigned long long* g_trace = nullptr;
 void gemm_set_trace(unsigned long long* trace) { g_trace = trace; }

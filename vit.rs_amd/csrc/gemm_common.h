@@ -621,14 +621,54 @@ struct EpiAuxQ {  // aux operand rows of one interior 32-row pass (rows mrow + 8
         }
     }
 };
-// one interior 32-row pass (all rows < M, all 64 columns < N): bf16-engine epilogues (no MX outputs)
-template <int EPI>
-__device__ __forceinline__ void staged_pass_interior_q(const GemmParams& p, const float* st, int rr, int cc,
+// the 8 bf16 values (packed as stored) back into swizzled staging row r, columns cc..cc+7, as fp32
+// (the column-wise MX pass of the fp8 engine reads them)
+__device__ __forceinline__ void stage_back8_q(float* st, int r, int cc, uint32_t w0, uint32_t w1, uint32_t w2,
+                                              uint32_t w3) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<f4*>(st + sq_off(r, cc)) = f4{__uint_as_float(w0 << 16), __uint_as_float(w0 & 0xffff0000u),
+                                                    __uint_as_float(w1 << 16), __uint_as_float(w1 & 0xffff0000u)};
+    *reinterpret_cast<f4*>(st + sq_off(r, cc + 4)) = f4{__uint_as_float(w2 << 16), __uint_as_float(w2 & 0xffff0000u),
+                                                        __uint_as_float(w3 << 16), __uint_as_float(w3 & 0xffff0000u)};
+}
+// column-wise MX of one 32-row pass (one MX block per column) whose bf16 outputs stage_back8_q left in
+// the swizzled staging: lane c takes column n0 + c (as mx_cols_pass, one block instead of two)
+__device__ __forceinline__ void mx_cols_pass_q(const GemmParams& p, const float* st, int lane, int mrow, int n0) {
+    if (mrow >= p.M) return;
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const int c = n0 + lane;
+    // two sweeps over the column (amax, then quantize) instead of 32 values held in registers:
+    // the persistent engine keeps the next tile's DMA state live through the epilogue
+    float amax = 0.f;
+#pragma unroll
+    for (int i = 0; i < 32; i++) amax = fmaxf(amax, fabsf(st[sq_off(i, lane)]));
+    const int sb = mx_scale_byte(amax);
+    const int tok = p.mxc_off + mrow, kb = tok >> 5;
+    p.mxc_s[((long long)(kb >> 1) * p.mxc_rg + (c >> 5)) * 64 + (kb & 1) * 32 + (c & 31)] = (uint8_t)sb;
+    const float inv = __uint_as_float((uint32_t)(254 - sb) << 23);
+    uint32_t w[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const float v0 = st[sq_off(4 * j, lane)], v1 = st[sq_off(4 * j + 1, lane)];
+        const float v2 = st[sq_off(4 * j + 2, lane)], v3 = st[sq_off(4 * j + 3, lane)];
+        int t = __builtin_amdgcn_cvt_pk_fp8_f32(v0 * inv, v1 * inv, 0, false);
+        t = __builtin_amdgcn_cvt_pk_fp8_f32(v2 * inv, v3 * inv, t, true);
+        w[j] = (uint32_t)t;
+    }
+    uint8_t* dst = p.mxc_q + (long long)c * p.mxc_ld + tok;
+    *reinterpret_cast<u32x4*>(dst) = u32x4{w[0], w[1], w[2], w[3]};
+    *reinterpret_cast<u32x4*>(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
+}
+// one interior 32-row pass (all rows < M, all 64 columns < N); the MX outputs (mx_q row form,
+// mxc_q column form via stage_back8_q) are the fp8 engine's
+template <int EPI, bool MX>
+__device__ __forceinline__ void staged_pass_interior_q(const GemmParams& p, float* st, int rr, int cc,
                                                        int mrow, int n, float (&cs)[8], const float* bv,
                                                        const EpiAuxQ<EPI>& aux) {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     constexpr bool AUX16 = epi_aux16(EPI);
     constexpr bool AUX32 = EPI == EPI_F32_RESID || EPI == EPI_F32_ACC;
+    const int cc_lane = cc >> 3;
 #pragma unroll
     for (int it = 0; it < 4; it++) {
         const int r = it * 8 + rr;
@@ -662,13 +702,23 @@ __device__ __forceinline__ void staged_pass_interior_q(const GemmParams& p, cons
 #pragma unroll
             for (int j = 0; j < 8; j++) gv[j] = gelu_fast_f(v[j]);
             epi_st16(p, (bf16_t*)p.C + off, pack8(v));
-            if (p.C2) epi_st16(p, (bf16_t*)p.C2 + off, pack8(gv));
+            const u32x4 g8 = pack8(gv);
+            if (p.C2) epi_st16(p, (bf16_t*)p.C2 + off, g8);
+            if constexpr (MX) {
+                if (p.mx_q) mx_out8(p, mrow + r, n, g8[0], g8[1], g8[2], g8[3], cc_lane);
+                if (p.mxc_q) stage_back8_q(st, r, cc, g8[0], g8[1], g8[2], g8[3]);
+            }
         } else if constexpr (EPI == EPI_BF16_GELU_D) {
             float gv[8], dv[8];
 #pragma unroll
             for (int j = 0; j < 8; j++) gelu_pair_fast_f(v[j], gv[j], dv[j]);
             epi_st16(p, (bf16_t*)p.C + off, pack8(dv));
-            if (p.C2) epi_st16(p, (bf16_t*)p.C2 + off, pack8(gv));
+            const u32x4 g8 = pack8(gv);
+            if (p.C2) epi_st16(p, (bf16_t*)p.C2 + off, g8);
+            if constexpr (MX) {
+                if (p.mx_q) mx_out8(p, mrow + r, n, g8[0], g8[1], g8[2], g8[3], cc_lane);
+                if (p.mxc_q) stage_back8_q(st, r, cc, g8[0], g8[1], g8[2], g8[3]);
+            }
         } else if constexpr (AUX16) {
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -683,7 +733,12 @@ __device__ __forceinline__ void staged_pass_interior_q(const GemmParams& p, cons
             }
 #pragma unroll
             for (int j = 0; j < 8; j++) cs[j] += v[j];
-            if (p.C) epi_st16(p, (bf16_t*)p.C + off, pack8(v));
+            const u32x4 d8 = pack8(v);
+            if (p.C) epi_st16(p, (bf16_t*)p.C + off, d8);
+            if constexpr (MX) {
+                if (p.mx_q) mx_out8(p, mrow + r, n, d8[0], d8[1], d8[2], d8[3], cc_lane);
+                if (p.mxc_q) stage_back8_q(st, r, cc, d8[0], d8[1], d8[2], d8[3]);
+            }
         }
     }
 }
@@ -691,30 +746,42 @@ __device__ __forceinline__ void staged_pass_interior_q(const GemmParams& p, cons
 // interior form loads the next pass's aux rows under the current pass.  Same outputs, bit for bit,
 // as staged_epilogue (same values, same column-sum order: the cs partials add the tile's rows in the
 // same order per lane, rows 8 it + rr of pass 0..3 = rows 8 it' + rr of the 64-row passes).
-template <int EPI>
-__device__ __forceinline__ void staged_epilogue_q(const GemmParams& p, f32x4_t (&acc)[8][4], float* st, int lane,
-                                                  int m0, int n0, const float* bpre) {
-    const int i = lane & 15, g = lane >> 4;
+// stage_pass(pass) writes rows 32 pass .. 32 pass + 31 of the wave tile into st (sq_off layout)
+template <int EPI, bool MX, typename StagePass>
+__device__ __forceinline__ void staged_epilogue_q_any(const GemmParams& p, StagePass stage_pass, float* st, int lane,
+                                                      int m0, int n0, const float* bpre) {
     const int rr = lane >> 3, cc = (lane & 7) * 8, n = n0 + cc;
     float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    auto stage_pass = [&](int pass) {
-#pragma unroll
-        for (int a = 0; a < 2; a++)
-#pragma unroll
-            for (int b = 0; b < 4; b++)
-                *reinterpret_cast<f32x4_t*>(st + sq_off(a * 16 + i, b * 16 + 4 * g)) = acc[pass * 2 + a][b];
+    auto mx_cols = [&](int pass) {
+        if constexpr (MX && epi_mx(EPI)) {
+            if (p.mxc_q) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                mx_cols_pass_q(p, st, lane, m0 + pass * 32, n0);
+            }
+        }
     };
     if (staged_interior<EPI>(p, m0, n0)) {
-        EpiAuxQ<EPI> a0, a1;
-        a0.load(p, rr, m0, n);
+        if constexpr (!MX) {  // the next pass's aux rows load under the current pass
+            EpiAuxQ<EPI> a0, a1;
+            a0.load(p, rr, m0, n);
 #pragma unroll
-        for (int pass = 0; pass < 4; pass += 2) {
-            a1.load(p, rr, m0 + (pass + 1) * 32, n);
-            stage_pass(pass);
-            staged_pass_interior_q<EPI>(p, st, rr, cc, m0 + pass * 32, n, cs, bpre, a0);
-            if (pass + 2 < 4) a0.load(p, rr, m0 + (pass + 2) * 32, n);
-            stage_pass(pass + 1);
-            staged_pass_interior_q<EPI>(p, st, rr, cc, m0 + (pass + 1) * 32, n, cs, bpre, a1);
+            for (int pass = 0; pass < 4; pass += 2) {
+                a1.load(p, rr, m0 + (pass + 1) * 32, n);
+                stage_pass(pass);
+                staged_pass_interior_q<EPI, MX>(p, st, rr, cc, m0 + pass * 32, n, cs, bpre, a0);
+                if (pass + 2 < 4) a0.load(p, rr, m0 + (pass + 2) * 32, n);
+                stage_pass(pass + 1);
+                staged_pass_interior_q<EPI, MX>(p, st, rr, cc, m0 + (pass + 1) * 32, n, cs, bpre, a1);
+            }
+        } else {  // fp8 engine (MX outputs): one set of aux registers, loaded ahead of the staging writes
+#pragma unroll
+            for (int pass = 0; pass < 4; pass++) {
+                EpiAuxQ<EPI> a0;
+                a0.load(p, rr, m0 + pass * 32, n);
+                stage_pass(pass);
+                staged_pass_interior_q<EPI, MX>(p, st, rr, cc, m0 + pass * 32, n, cs, bpre, a0);
+                mx_cols(pass);
+            }
         }
     } else {
 #pragma unroll
@@ -729,7 +796,17 @@ __device__ __forceinline__ void staged_epilogue_q(const GemmParams& p, f32x4_t (
                 const int m = m0 + pass * 32 + r;
                 if (m >= p.M) continue;
                 if (n + 8 <= p.N) {
-                    epilogue8<EPI>(p, m, n, v, cs, lane, nullptr);
+                    if constexpr (MX && epi_mx(EPI)) {
+                        float wb[8];
+                        epilogue8<EPI>(p, m, n, v, cs, lane, p.mxc_q ? wb : nullptr);
+                        if (p.mxc_q) {
+                            typedef float f4 __attribute__((ext_vector_type(4)));
+                            *reinterpret_cast<f4*>(st + sq_off(r, cc)) = f4{wb[0], wb[1], wb[2], wb[3]};
+                            *reinterpret_cast<f4*>(st + sq_off(r, cc + 4)) = f4{wb[4], wb[5], wb[6], wb[7]};
+                        }
+                    } else {
+                        epilogue8<EPI>(p, m, n, v, cs, lane, nullptr);
+                    }
                 } else if (n + 4 <= p.N) {
                     f32x4_t t = lo;
                     epilogue<EPI>(p, m, n, t);
@@ -738,9 +815,25 @@ __device__ __forceinline__ void staged_epilogue_q(const GemmParams& p, f32x4_t (
                     }
                 }
             }
+            mx_cols(pass);
         }
     }
     staged_colsum<EPI>(p, lane, m0, n0, cs);
+}
+// the bf16 engines' 16x16 accumulator tiles: lane (i,g) of tile (a,b) holds row 16a+i, columns
+// 16b+4g..+3
+template <int EPI>
+__device__ __forceinline__ void staged_epilogue_q(const GemmParams& p, f32x4_t (&acc)[8][4], float* st, int lane,
+                                                  int m0, int n0, const float* bpre) {
+    const int i = lane & 15, g = lane >> 4;
+    auto stage_pass = [&](int pass) {
+#pragma unroll
+        for (int a = 0; a < 2; a++)
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+                *reinterpret_cast<f32x4_t*>(st + sq_off(a * 16 + i, b * 16 + 4 * g)) = acc[pass * 2 + a][b];
+    };
+    staged_epilogue_q_any<EPI, false>(p, stage_pass, st, lane, m0, n0, bpre);
 }
 
 }  // namespace vit

@@ -247,6 +247,181 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(F8Params fp) {
     staged_colsum<EPI>(p, lane, m0, n0, cs);
 }
 
+// Persistent streaming form (as g2::gemm_kernel_s): one workgroup per CU walks its
+// tiles with the LDS-DMA ring (data and scale pieces) streaming across tile boundaries, the next
+// tile's first two K-steps landing under the epilogue, which stages through the tile's last two
+// slots in 32-row passes (8 KiB per wave; the column-wise MX pass quantizes one 32-token block per
+// pass).  Same MFMAs in the same order and the same epilogue arithmetic: bit-identical outputs.
+template <int EPI>
+__global__ __launch_bounds__(NT, 1) void gemm_kernel_s(F8Params fp) {
+    const GemmParams& p = fp.p;
+    __shared__ __attribute__((aligned(1024))) char smem[NS * SLOT_BYTES];
+    static_assert(4 * 8192 <= SLOT_BYTES, "epilogue staging: four waves per slot");
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int ntn = cdiv(p.N, BN), tiles = p.tiles;
+    const int nblk = gridDim.x;
+    const int my_tiles = (tiles - (int)blockIdx.x + nblk - 1) / nblk;
+    const int nk = p.K / KB;
+    const char* A = (const char*)p.A;
+    const char* B = (const char*)p.B;
+    const bool isb = wave >= 4;
+    const int w4 = wave & 3;
+    const char* S = (const char*)(isb ? fp.sb : fp.sa);
+    const int rg_tot = isb ? fp.rgb_tot : fp.rga_tot;
+    v16f acc[4][2];
+    auto zero_acc = [&]() {
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+#pragma unroll
+            for (int b = 0; b < 2; b++) acc[a][b] = v16f{};
+    };
+    zero_acc();
+    if (my_tiles <= 0) return;
+    struct TileSrc {
+        int tm0, tn0;
+        uint32_t a[2], b[2], sc;
+    };
+    auto tile_src = [&](int j, TileSrc& ts) {
+        const int t = xcd_remap(j * nblk + (int)blockIdx.x, tiles);
+        ts.tm0 = (t / ntn) * BM;
+        ts.tn0 = (t % ntn) * BN;
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const int row = (q * 8 + wave) * 16 + (lane >> 2);
+            const int c = (lane & 3) ^ swz(row);
+            ts.a[q] = (uint32_t)((long long)min(ts.tm0 + row, p.M - 1) * p.lda + c * 16);
+            ts.b[q] = (uint32_t)((long long)min(ts.tn0 + row, p.N - 1) * p.ldb + c * 16);
+        }
+        ts.sc = (uint32_t)((((isb ? ts.tn0 : ts.tm0) / 32) + 2 * w4) * 64 + 4 * lane);
+    };
+    TileSrc cur, nxt;
+    tile_src(0, cur);
+    nxt = cur;
+    if (my_tiles > 1) tile_src(1, nxt);
+    auto glds16 = [&](const char* src, char* dst) {
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    };
+    // A pieces + this wave's scale piece of step kt2 of the current tile (kt2 >= nk: the next one's)
+    auto issue_a = [&](int kt2, int sl, bool more) {
+        if (kt2 >= nk && !more) return;
+        const bool c = kt2 < nk;
+        const int k = c ? kt2 : kt2 - nk;
+        char* dst = smem + sl * SLOT_BYTES;
+#pragma unroll
+        for (int q = 0; q < 2; q++) glds16(A + (long long)k * KB + (c ? cur.a[q] : nxt.a[q]), dst + (q * 8 + wave) * 1024);
+        if (lane < 32)
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void*)(S + (long long)k * rg_tot * 64 + (c ? cur.sc : nxt.sc)),
+                (__attribute__((address_space(3))) void*)(dst + 2 * IMG_BYTES + (isb ? 512 : 0) + w4 * 128), 4, 0, 0);
+    };
+    auto issue_b = [&](int kt2, int sl, bool more) {
+        if (kt2 >= nk && !more) return;
+        const bool c = kt2 < nk;
+        const int k = c ? kt2 : kt2 - nk;
+        char* dst = smem + sl * SLOT_BYTES + IMG_BYTES;
+#pragma unroll
+        for (int q = 0; q < 2; q++) glds16(B + (long long)k * KB + (c ? cur.b[q] : nxt.b[q]), dst + (q * 8 + wave) * 1024);
+    };
+    auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto mfma_half = [&](int half, const v8i (&fa)[2], const int (&sa)[2], const v8i (&fb)[2], const int (&sb)[2]) {
+#pragma unroll
+        for (int a = 0; a < 2; a++)
+#pragma unroll
+            for (int b = 0; b < 2; b++)
+                acc[half * 2 + a][b] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+                    fb[b], fa[a], acc[half * 2 + a][b], 0, 0, 0, sb[b], 0, sa[a]);
+        // keep the phase's MFMAs in front of the barrier that closes it (as g2::gemm_kernel_s)
+        asm volatile("" ::"v"(acc[half * 2][0]), "v"(acc[half * 2][1]), "v"(acc[half * 2 + 1][0]),
+                     "v"(acc[half * 2 + 1][1]));
+    };
+    const bool lagging = wave >= 4;
+    issue_a(0, 0, false); issue_b(0, 0, false);
+    issue_a(1, 1, my_tiles > 1); issue_b(1, 1, my_tiles > 1);  // nk >= 1; a missing step 1 issues nothing
+    if (nk > 1 || my_tiles > 1) wait_vm(5);
+    else wait_vm(0);
+    int sl = 0;
+    v8i fb[2], fa0[2], fa1[2];
+    int sb_[2], sa0[2], sa1[2];
+    for (int j = 0; j < my_tiles; j++) {
+        const bool more = j + 1 < my_tiles;
+        bar();
+        if (lagging) {
+            __builtin_amdgcn_s_setprio(1);
+            bar();
+        }
+        for (int kt = 0; kt < nk; kt++) {
+            const char* img = smem + sl * SLOT_BYTES;
+            const char* sc = img + 2 * IMG_BYTES;
+            const int sl2 = (sl + 2) & 3;
+#pragma unroll
+            for (int b = 0; b < 2; b++) {
+                fb[b] = frag(img + IMG_BYTES, wn * 64 + b * 32, lane);
+                sb_[b] = scale_of(sc + 512, wn * 2 + b, lane);
+            }
+#pragma unroll
+            for (int a = 0; a < 2; a++) {
+                fa0[a] = frag(img, wm * 128 + a * 32, lane);
+                sa0[a] = scale_of(sc, wm * 4 + a, lane);
+            }
+            issue_a(kt + 2, sl2, more);
+            bar();
+            mfma_half(0, fa0, sa0, fb, sb_);
+            bar();
+#pragma unroll
+            for (int a = 0; a < 2; a++) {
+                fa1[a] = frag(img, wm * 128 + (2 + a) * 32, lane);
+                sa1[a] = scale_of(sc, wm * 4 + 2 + a, lane);
+            }
+            // own pieces of the next step landed (the A half of the one after, 3 pieces, in flight);
+            // in a later tile's first step they were retired before the previous epilogue
+            if (kt > 0 || j == 0) {
+                if (kt + 2 < nk || more) wait_vm(3);
+                else wait_vm(0);
+            }
+            issue_b(kt + 2, sl2, more);
+            bar();
+            mfma_half(1, fa1, sa1, fb, sb_);
+            bar();
+            sl = (sl + 1) & 3;
+        }
+        if (!lagging) bar();  // balance the stagger barrier
+        float bpre[8];
+        staged_bias_prefetch<EPI>(p, lane, cur.tn0 + wn * 64, bpre);
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        // this tile's last two steps were in slots sl - 1, sl - 2 (mod 4); nk == 1: slot sl - 1 and
+        // slot sl + 2, the next tile's step 2 slot, which nothing fills before the next barrier
+        float* st = reinterpret_cast<float*>(smem + ((wave < 4 ? sl + 2 : sl + 3) & 3) * SLOT_BYTES + (wave & 3) * 8192);
+        const int r = lane & 31, h = lane >> 5;
+        auto stage_pass = [&](int pass) {
+#pragma unroll
+            for (int b = 0; b < 2; b++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const v16f& v = acc[pass][b];
+                    *reinterpret_cast<f32x4_t*>(st + sq_off(r, b * 32 + 8 * q + 4 * h)) =
+                        f32x4_t{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+                }
+        };
+        staged_epilogue_q_any<EPI, true>(p, stage_pass, st, lane, cur.tm0 + wm * 128, cur.tn0 + wn * 64, bpre);
+        zero_acc();
+        // recomputed rather than carried: nothing of the next tiles' sources stays live through the epilogue
+        if (more) tile_src(j + 1, cur);
+        if (j + 2 < my_tiles) tile_src(j + 2, nxt);
+    }
+}
+
 // ------------------------------------------------------------------------------- quantizer
 // MX block quantization of a [R][K] fp32 / bf16 matrix (row stride ldx elements) into fp8 e4m3
 // rows (stride ldq bytes) + lane-native scales.  One wave per (32-row group, 64-deep k-step):
@@ -505,6 +680,32 @@ void gemm_fp8(const GemmArgs& a, hipStream_t s) {
     fp.sb = (const uint8_t*)a.b_scale;
     fp.rga_tot = (int)(mx_rows_padded(a.M) / 32);
     fp.rgb_tot = (int)(mx_rows_padded(a.N) / 32);
+    // persistent streaming engine (production GEMM variant, gemm_streaming()): no split-K, 32-bit
+    // DMA offsets; not for the aux x product epilogues (6 / 9: with both MX outputs their epilogue
+    // outgrows the registers the streaming state leaves and spills; measured 8 % slower than the
+    // one-tile kernel on the ViT-H/14 fcproj input gradient)
+    if (split == 1 && gemm_streaming() && b.epi != EPI_F32_ACC && !epi_aux16(b.epi) &&
+        (long long)a.M * a.lda < (1LL << 31) &&
+        (long long)a.N * a.ldb < (1LL << 31)) {
+        const dim3 pg(tiles < 256 ? tiles : 256);
+        switch (b.epi) {
+#define VIT_CASE(E) \
+    case E: f8::gemm_kernel_s<E><<<pg, f8::NT, 0, s>>>(fp); break;
+            VIT_CASE(EPI_F32_STORE)
+            VIT_CASE(EPI_BF16_STORE)
+            VIT_CASE(EPI_BF16_GELU)
+            VIT_CASE(EPI_F32_RESID)
+            VIT_CASE(EPI_BF16_DGELU)
+            VIT_CASE(EPI_BF16_GELU_D)
+            VIT_CASE(EPI_BF16_MUL)
+#undef VIT_CASE
+            default: set_error("gemm_fp8: unsupported epilogue %d", b.epi); return;
+        }
+        after_launch("gemm_fp8");
+        count_hit(VIT_HIT_GEMM_FP8 + b.epi);
+        colsum_rows_end(a, cs_rows, s);
+        return;
+    }
     switch (b.epi) {
 #define VIT_CASE(E) \
     case E: f8::gemm_kernel<E><<<dim3(tiles, split), f8::NT, 0, s>>>(fp); break;
