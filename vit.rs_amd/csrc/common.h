@@ -118,30 +118,34 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
 // in range-reduction and correctly-rounded refinement sequences (~12 VALU per element, the bulk of
 // the GELU / GELU' epilogues); the results are rounded to bf16, so 1-ulp fp32 terms do not show.
 // x -> -inf: exp2 -> inf, rcp -> 0, product -> -0; x -> +inf: sigmoid -> 1.
+// (r04) The tanh argument in Horner form: z = k (x + c x^3) = x * fma(k c, x^2, k), and the
+// derivative as sg + [x sg (1 - sg)] * [2 s (1 + 3 c x^2)] = fma(fma(-g, sg, g), w, sg) with
+// g = x sg: 8 VALU + 2 transcendentals per element for the pair (was 11 + 2).  The fc forward's
+// GELU-pair epilogue is vector-issue bound, so the count is its cost.
+constexpr float GELU_K = -2.0f * 0.7978845608028654f * 1.4426950408889634f;  // -2 sqrt(2/pi) log2(e)
+constexpr float GELU_KC = GELU_K * 0.044715f;
+constexpr float GELU_W0 = 2.0f * 0.7978845608028654f;                       // 2 s
+constexpr float GELU_W2 = 2.0f * 0.7978845608028654f * 3.0f * 0.044715f;    // 2 s 3 c
+__device__ __forceinline__ float gelu_sigmoid_f(float x, float x2) {       // 0.5 (1 + tanh a)
+    return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * fmaf(GELU_KC, x2, GELU_K)));
+}
 __device__ __forceinline__ float gelu_fast_f(float x) {
-    const float k = -2.0f * 0.7978845608028654f * 1.4426950408889634f;  // -2 sqrt(2/pi) log2(e)
-    const float t = k * fmaf(0.044715f * x, x * x, x);
-    return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(t));
+    return x * gelu_sigmoid_f(x, x * x);
 }
 // derivative with sech^2 of the tanh argument (D4): sg + 2 s x sg (1 - sg) (1 + 3 * 0.044715 x^2)
 __device__ __forceinline__ float gelu_grad_fast_f(float x) {
-    const float s = 0.7978845608028654f;
-    const float k = -2.0f * s * 1.4426950408889634f;
     const float x2 = x * x;
-    const float sg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(k * fmaf(0.044715f * x, x2, x)));  // 0.5(1 + tanh a)
-    const float u = fmaf(-sg, sg, sg);                                // sg (1 - sg)
-    return fmaf((2.0f * s) * x * u, fmaf(3.0f * 0.044715f, x2, 1.0f), sg);
+    const float sg = gelu_sigmoid_f(x, x2);
+    const float g = x * sg;
+    return fmaf(fmaf(-g, sg, g), fmaf(GELU_W2, x2, GELU_W0), sg);
 }
 
 // gelu_fast_f(x) and gelu_grad_fast_f(x) from one sigmoid (bit-identical to the two calls)
 __device__ __forceinline__ void gelu_pair_fast_f(float x, float& g, float& d) {
-    const float s = 0.7978845608028654f;
-    const float k = -2.0f * s * 1.4426950408889634f;
     const float x2 = x * x;
-    const float sg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(k * fmaf(0.044715f * x, x2, x)));
+    const float sg = gelu_sigmoid_f(x, x2);
     g = x * sg;
-    const float u = fmaf(-sg, sg, sg);
-    d = fmaf((2.0f * s) * x * u, fmaf(3.0f * 0.044715f, x2, 1.0f), sg);
+    d = fmaf(fmaf(-g, sg, g), fmaf(GELU_W2, x2, GELU_W0), sg);
 }
 
 // optimizer_step (train_vit.rs:740): p -= lr*g with two roundings like the Rust reference
