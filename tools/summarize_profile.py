@@ -27,10 +27,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # bench timing class -> (kernel-name regex, grid x of the launch at ViT-B/16 B=256 or None).
 # g2::gemm_kernel<a_kcontig, b_kcontig, epi, ...>; epi numbers from vit.rs_amd/csrc/gemm.h.
 CLASS_KERNELS = {
-    # epi 9 / 8 (stored gelu' x product, gelu' / gelu pair) since r02b; 6 / 4 before
-    "gemm_fcproj_dgrad": (r"g2::gemm_kernel<true, (true|false), (6|9)\b", None),  # dgrad B = transposed weight copy since dd2b73c
-    "gemm_fc_fwd": (r"g2::gemm_kernel<true, true, (4|8)\b", None),
-    "gemm_qkv_fwd": (r"g2::gemm_kernel<true, true, 3\b", None),
+    # epi 9 / 8 (stored gelu' x product, gelu' / gelu pair) since r02b; 6 / 4 before; the persistent
+    # streaming engine g2::gemm_kernel_s<epi> since r04
+    "gemm_fcproj_dgrad": (r"g2::gemm_kernel(<true, (true|false), |_s<)(6|9)\b", None),  # dgrad B = transposed weight copy since dd2b73c
+    "gemm_fc_fwd": (r"g2::gemm_kernel(<true, true, |_s<)(4|8)\b", None),
+    "gemm_qkv_fwd": (r"g2::gemm_kernel(<true, true, |_s<)3\b", None),
     "gemm_proj_dgrad": (r"g2::gemm_kernel<true, false, 3\b", None),
     "attention_bwd": (r"attn_bwd(p|1|_pair)_k", None),
     "attention_fwd": (r"attn_fwd_k", None),
@@ -41,7 +42,7 @@ CLASS_KERNELS = {
 # epilogue runs proj fwd (A 1 x C wide) and fcproj fwd (A 4 x C wide) alternately in every layer;
 # the smaller half of its dispatches (by bytes) is proj fwd, the larger fcproj fwd
 SPLIT_KERNELS = {
-    r"g2::gemm_kernel<true, true, 5\b": ("gemm_proj_fwd", "gemm_fcproj_fwd"),
+    r"g2::gemm_kernel(<true, true, |_s<)5\b": ("gemm_proj_fwd", "gemm_fcproj_fwd"),
 }
 
 
