@@ -652,6 +652,25 @@ constexpr int ATTN_PART_ROWS = 16;   // column-sum partial rows per (b,h) a back
 #ifndef VIT_ATTN_SW_SLICE
 #define VIT_ATTN_SW_SLICE 1
 #endif
+// diagnostic builds only (tools/bench_attn.py on a -DVIT_ATTN_DIAG=n library; outputs wrong):
+// bit 0 = the persistent backward issues no global loads inside its item loop, bit 1 = no dQ / dK / dV stores
+#ifndef VIT_ATTN_DIAG
+#define VIT_ATTN_DIAG 0
+#endif
+// bit 2: per-wave s_memtime stamps of the persistent backward's slice loop (blocks < 8, the first 16
+// slices) into attn_trace (read with vit_attn_trace_read, attn_h64.hip)
+#if VIT_ATTN_DIAG & 4
+static __device__ unsigned long long attn_trace[8 * 16 * 16 * 16];
+#define ATTN_STAMP(k)                                                                                   \
+    do {                                                                                                \
+        if (blockIdx.x < 8 && it < 16 && lane == 0)                                                     \
+            attn_trace[((blockIdx.x * 16 + it) * 16 + w) * 16 + (k)] = __builtin_amdgcn_s_memtime();   \
+    } while (0)
+#else
+#define ATTN_STAMP(k) \
+    do {              \
+    } while (0)
+#endif
 template <int HS>
 constexpr bool sw_slice() { return HS == 64 && VIT_ATTN_SW_SLICE; }
 #ifndef VIT_ATTN_SW_DS
@@ -822,25 +841,51 @@ __device__ __forceinline__ void bwd_slice_b(const bf16_t* Ks, const bf16_t* dSs,
 #pragma unroll
             for (int r = 0; r < 4; r++) acc[r] += e * xk_k[16 * dt + 4 * g + r];
         }
-        if (q < T) store4(dq + (long long)q * C3 + 16 * dt + 4 * g, acc, scale);
+        if constexpr (VIT_ATTN_DIAG & 2) asm volatile("" ::"v"(acc));
+        else if (q < T) store4(dq + (long long)q * C3 + 16 * dt + 4 * g, acc, scale);
     };
     constexpr bool BAL = NW == 7 && 2 * DT == 8;  // one loop body (two inlined copies spill)
     const int jlast = BAL ? (w == 3 ? 7 : w) : 2 * DT - 1, jstep = BAL ? 4 : NW;
     for (int j = w; j <= jlast; j += jstep) tile(j);
 }
 
+// Σ over the 16 lanes of a DPP row of v[0..15], transposed: lane i of the row gets Σ_lanes v[i].
+// Butterfly over the partners i ^ 15 (row_mirror), i ^ 7 (row_half_mirror), i ^ 2, i ^ 1 (quad_perm),
+// each step keeping the half of the values selected by bit 3, 2, 1, 0 of i: 15 DPP adds instead of
+// the 64 of sixteen row_sum16 reductions, and every lane ends up holding a result.
+template <int CTRL>
+__device__ __forceinline__ float dpp_c(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row_transpose_sum16(const float (&v)[16], int i) {
+    const bool b3 = i & 8, b2 = i & 4, b1 = i & 2, b0 = i & 1;
+    float w[8], x[4], y[2];
+#pragma unroll
+    for (int k = 0; k < 8; k++) w[k] = (b3 ? v[k + 8] : v[k]) + dpp_c<0x140>(b3 ? v[k] : v[k + 8]);
+#pragma unroll
+    for (int k = 0; k < 4; k++) x[k] = (b2 ? w[k + 4] : w[k]) + dpp_c<0x141>(b2 ? w[k] : w[k + 4]);
+#pragma unroll
+    for (int k = 0; k < 2; k++) y[k] = (b1 ? x[k + 2] : x[k]) + dpp_c<0x4E>(b1 ? x[k] : x[k + 2]);
+    return (b0 ? y[1] : y[0]) + dpp_c<0xB1>(b0 ? y[0] : y[1]);
+}
+
 // end of an item: dK, dV of the wave's keys; the wave's column sums of dQ | dK | dV into its own
-// partial row part[3 HS] (attn_colsum_reduce_k sums the rows: no barrier, no LDS)
+// partial row part[3 HS] (attn_colsum_reduce_k sums the rows: no barrier, no LDS).  The sums go
+// through row_transpose_sum16, sixteen columns per reduction, each lane storing one column (at head
+// size 64 three dword stores of 256 contiguous bytes); the row_sum16 form (4 DPP adds per column, the
+// sum in lane 15, 4-B stores by 4 lanes) measured 5.3k + 1k cycles per item at ViT-B/16, 7.1k at
+// ViT-H/14 (tools/attn_trace.py)
 template <int HS, int KK = 2>
 __device__ __forceinline__ void bwd_item_end(BwdRegs<HS, KK>& R, bf16_t* dq, long long C, int key0, int T, float scale,
-                                             float* part, int lane) {
+                                             float* part, int lane, int it = 99) {
     constexpr int KS = Geo<HS>::KS, DT = Geo<HS>::DT;
     const int i = lane & 15, g = lane >> 4;
+    [[maybe_unused]] const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // ATTN_STAMP
     const long long C3 = 3 * C;
 #pragma unroll
     for (int kk = 0; kk < KK; kk++) {
         const int key = key0 + 16 * kk + i;
-        if (key >= T) continue;
+        if (key >= T || (VIT_ATTN_DIAG & 2)) continue;
         bf16_t* dst = dq + (long long)key * C3 + 4 * g;
 #pragma unroll
         for (int dt = 0; dt < DT; dt++) {
@@ -848,27 +893,8 @@ __device__ __forceinline__ void bwd_item_end(BwdRegs<HS, KK>& R, bf16_t* dq, lon
             store4(dst + 2 * C + 16 * dt, R.dv[kk][dt], 1.0f);
         }
     }
+    ATTN_STAMP(8);
     if (!part) return;
-    // reductions over the 16 key lanes of a DPP row (row_shr 1, 2, 4, 8: the sum lands in lane
-    // 15 of the row), written by lanes i == 15 straight to the wave's partial row in global memory
-#pragma unroll
-    for (int dt = 0; dt < DT; dt++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            float tk = 0.f, tv = 0.f;
-#pragma unroll
-            for (int kk = 0; kk < KK; kk++)
-                if (key0 + 16 * kk + i < T) {
-                    tk += R.dk[kk][dt][r] * scale;
-                    tv += R.dv[kk][dt][r];
-                }
-            tk = row_sum16(tk);
-            tv = row_sum16(tv);
-            if (i == 15) {
-                part[HS + 16 * dt + 4 * g + r] = tk;
-                part[2 * HS + 16 * dt + 4 * g + r] = tv;
-            }
-        }
     // dQ: lane (i,g) sums over the 4 g-groups' queries, then over its key column i
     float sd[KK];
 #pragma unroll
@@ -876,18 +902,66 @@ __device__ __forceinline__ void bwd_item_end(BwdRegs<HS, KK>& R, bf16_t* dq, lon
         sd[kk] = R.sds[kk] + __shfl_xor(R.sds[kk], 16, 64);
         sd[kk] += __shfl_xor(sd[kk], 32, 64);
     }
+    // per-lane values: dK / dV index 4 dt + r (d = 16 dt + 4 g + r); dQ index 8 s + j over the valid
+    // (s, j) of the k-steps (the last one of HS % 32 == 16 has j < 4 only)
+    constexpr int NKV = 4 * DT, NQ = 8 * KS - (Geo<HS>::HALF ? 4 : 0);
+    constexpr int PKV = (NKV + 15) / 16 * 16, PQ = (NQ + 15) / 16 * 16;  // padded to whole reductions
+    float vk[PKV], vv[PKV], vq[PQ];
 #pragma unroll
-    for (int s = 0; s < KS; s++)
+    for (int k = 0; k < PKV; k++) vk[k] = vv[k] = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const int d = 32 * s + (j < 4 ? 4 * g + j : 16 + 4 * g + j - 4);
-            if (d >= HS) continue;  // zero half of the last k-step (HS % 32 == 16)
-            float t = 0.f;
+    for (int k = 0; k < PQ; k++) vq[k] = 0.f;
 #pragma unroll
-            for (int kk = 0; kk < KK; kk++) t += sd[kk] * (float)R.kf[kk][s][j];
-            t = row_sum16(t);
-            if (i == 15) part[d] = t * scale;
+    for (int dt = 0; dt < DT; dt++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+#pragma unroll
+            for (int kk = 0; kk < KK; kk++)
+                if (key0 + 16 * kk + i < T) {
+                    vk[4 * dt + r] += R.dk[kk][dt][r] * scale;
+                    vv[4 * dt + r] += R.dv[kk][dt][r];
+                }
         }
+#pragma unroll
+    for (int k = 0; k < NQ; k++) {
+        const int s = k >> 3, j = k & 7;
+        float t = 0.f;
+#pragma unroll
+        for (int kk = 0; kk < KK; kk++) t += sd[kk] * (float)R.kf[kk][s][j];
+        vq[k] = t;
+    }
+    auto dq_col = [&](int k) {
+        const int s = k >> 3, j = k & 7;
+        return 32 * s + (j < 4 ? 4 * g + j : 16 + 4 * g + j - 4);
+    };
+    // sixteen values at a time: lane i of each DPP row gets the sum of value base + i
+#pragma unroll
+    for (int base = 0; base < PKV; base += 16) {
+        float tk[16], tv[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            tk[k] = vk[base + k];
+            tv[k] = vv[base + k];
+        }
+        const float sk = row_transpose_sum16(tk, i), sv = row_transpose_sum16(tv, i);
+        const int k = base + i;
+        if (k < NKV) {
+            const int d = 16 * (k >> 2) + 4 * g + (k & 3);
+            part[HS + d] = sk;
+            part[2 * HS + d] = sv;
+        }
+    }
+    ATTN_STAMP(9);
+#pragma unroll
+    for (int base = 0; base < PQ; base += 16) {
+        float tq[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) tq[k] = vq[base + k];
+        const float sq = row_transpose_sum16(tq, i);
+        const int k = base + i;
+        if (k < NQ) part[dq_col(k)] = sq * scale;
+    }
+    ATTN_STAMP(10);
 }
 
 // XK: T = TP + 1 (ViT-H/14, ViT-L/14 at 224^2: T = 257 = 8 x 32 + 1): the waves own keys 0 .. TP-1
@@ -956,15 +1030,14 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
     bf16_t* dq = dqkv + (long long)b * T * C3 + h * HS;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, i = lane & 15;
     const int key0 = w * 32;
+    int it = 15;  // ATTN_STAMP record: kernel-level stamps in record 15, slice sl in record sl
+    ATTN_STAMP(0);
     BwdRegs<HS> R;
-    // the wave's K, V fragments (rows >= T -> 0), requested first so their latency hides
+    // the wave's V fragments (rows >= T -> 0), requested first so their latency hides
 #pragma unroll
     for (int kk = 0; kk < 2; kk++)
 #pragma unroll
-        for (int s = 0; s < KS; s++) {
-            R.kf[kk][s] = frag_glb<HS>(base + C, C3, key0 + 16 * kk + i, T, s, lane);
-            R.vf[kk][s] = frag_glb<HS>(base + 2 * C, C3, key0 + 16 * kk + i, T, s, lane);
-        }
+        for (int s = 0; s < KS; s++) R.vf[kk][s] = frag_glb<HS>(base + 2 * C, C3, key0 + 16 * kk + i, T, s, lane);
     // one slice (32 rows) of Q and dO: PER 16-B pieces per thread and operand
     uint4 pq[PER], pd[PER];
     auto fetch_slice = [&](int q0) {
@@ -1017,6 +1090,11 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
         }
     }
     __syncthreads();
+    // the wave's K fragments from the image (one global read of K per item, not two)
+#pragma unroll
+    for (int kk = 0; kk < 2; kk++)
+#pragma unroll
+        for (int s = 0; s < KS; s++) R.kf[kk][s] = frag_row<HS>(Ks, SV, key0 + 16 * kk, s, lane);
     float xacc = 0.f, xsds = 0.f;  // XK: this thread's dK / dV element of key T-1; sum of its dS
     // XK: the 8 dims 8p .. 8p+7 (p = tid & 15 < HS / 8) of key T-1's K and V rows, in registers for
     // the item: each query's s = q . k and dP = do . v is 16 lanes x one 16-B slice read
@@ -1032,11 +1110,15 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
     const float scale = 1.0f / sqrtf((float)HS);
     const float c = LOG2E * scale;
     R.zero();
+    ATTN_STAMP(1);
 #pragma unroll 1
     for (int sl = 0; sl < NSLQ; sl++) {
         const int q0 = sl * 32, cur = sl & 1;
+        it = sl;
+        ATTN_STAMP(0);
         if (sl + 1 < NSLQ) fetch_slice(q0 + 32);  // lands in registers during phase A
         bwd_slice_a<HS>(R, Qs + cur * 32 * SK, Ds + cur * 32 * SK, lse_s + q0, del_s + q0, dSs + key0 * Z::SDS, c, lane);
+        ATTN_STAMP(1);
         if constexpr (XK) {  // key T-1 against the slice's 32 queries: 16 lanes per query
             const bf16_t* Qc = Qs + cur * 32 * SK;
             const bf16_t* Dc = Ds + cur * 32 * SK;
@@ -1062,6 +1144,7 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
             }
         }
         __syncthreads();
+        ATTN_STAMP(2);
         if constexpr (XK) {
             if (tid < 2 * HS) {
                 const bf16_t* img = (tid < HS ? Qs : Ds) + cur * 32 * SK;
@@ -1075,13 +1158,19 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
             }
         }
         if (sl + 1 < NSLQ) put_slice(cur ^ 1);  // its buffer was last read in the previous slice
+        ATTN_STAMP(3);
         bwd_slice_b<HS, NSL, NW, XK>(Ks, dSs, dq, C3, q0, T, scale, w, lane, xds_s, xk_s);
+        ATTN_STAMP(4);
         __syncthreads();
+        ATTN_STAMP(5);
     }
+    it = 15;
+    ATTN_STAMP(6);
     // per-wave column-sum rows: dsum[((b NWR + w) NH + h)][3 HS], NWR = NW (+ 1: the last key's row, XK)
     constexpr int NWR = NW + (XK ? 1 : 0);
     bwd_item_end<HS>(R, dq, C, key0, T, scale,
-                     dsum ? dsum + ((long long)(b * NWR + w) * NH + h) * 3 * HS : nullptr, lane);
+                     dsum ? dsum + ((long long)(b * NWR + w) * NH + h) * 3 * HS : nullptr, lane, it);
+    ATTN_STAMP(7);
     if constexpr (XK) {  // key T-1's dK, dV and its column-sum row (index NW of the item)
         if (tid < 2 * HS) {
             const int o = tid, d = o < HS ? o : o - HS;
@@ -1103,6 +1192,7 @@ template <int HS, int NKT, int KK = 2>
 #ifndef VIT_ATTN_SKEW
 #define VIT_ATTN_SKEW 1
 #endif
+
 struct Bwdp {
     using G = Geo<HS>;
     static constexpr int TP = NKT * 16, NW = NKT / KK, NT = NW * 64, NSL = TP / 32, CH = G::CH;
@@ -1228,6 +1318,9 @@ __global__ __launch_bounds__(NKT / KK * 64, 1) void attn_bwdp_k(bf16_t* __restri
     };
     int bh = blockIdx.x;
     if (bh >= BH) return;
+    // (measured, not kept: s_setprio 1 for waves 4-6, 263.6 vs 254.5 us — their phase A sped up by what
+    // waves 0-2's slowed down; waves 4-6 running phase B before phase A, 262 us: the SIMD's issue is
+    // shared, not idle)
     // prologue (first item): K image, V rows, lse, slice 0 — one blocking round trip
     fetch_slice(src_of(bh), 0);
     {
@@ -1239,6 +1332,7 @@ __global__ __launch_bounds__(NKT / KK * 64, 1) void attn_bwdp_k(bf16_t* __restri
     }
     for (int t = tid; t < TP; t += NT) lse_s[t] = t < T ? lse[(long long)bh * T + t] : INFINITY;
     put_slice(0);
+    if constexpr ((VIT_ATTN_DIAG & 1) != 0) fetch_side(src_of(bh), 0);
     __syncthreads();
     BwdRegs<HS, KK> R;
     load_kv(R, 0);
@@ -1255,31 +1349,39 @@ __global__ __launch_bounds__(NKT / KK * 64, 1) void attn_bwdp_k(bf16_t* __restri
 #pragma unroll 1
         for (int sl = 0; sl < NSL; sl++, it++) {
             const int cur = it & 1, q0 = sl * 32;
+            ATTN_STAMP(0);
             // one step ahead: the next slice (this item's or the next item's first), the next
             // item's K / V row block sl and, with its first block, its lse
             // (unconditional: past the last item / slice a valid item is re-read into buffers no one
             // reads again, so the compiler sees every prefetch register consumed on every path and
             // does not drain vmcnt before re-using them)
-            if (sl + 1 < NSL) fetch_slice(s_cur, q0 + 32);
-            else fetch_slice(s_nxt, 0);
-            fetch_side(s_nxt, sl);
-            // unconditional load (past T: 0); padded keys get +inf when it is put
-            if (sl == 0) lse_n = buf_ldf(s_nxt.l, 4 * tid);
+            if constexpr (!(VIT_ATTN_DIAG & 1)) {
+                if (sl + 1 < NSL) fetch_slice(s_cur, q0 + 32);
+                else fetch_slice(s_nxt, 0);
+                fetch_side(s_nxt, sl);
+                // unconditional load (past T: 0); padded keys get +inf when it is put
+                if (sl == 0) lse_n = buf_ldf(s_nxt.l, 4 * tid);
+            }
             if constexpr (VIT_ATTN_SKEW) {
                 // A(sl) -> dS^T buffer sl&1; B(sl-1) from buffer (sl-1)&1 (complete since the last
                 // barrier); the slice buffers cur^1 were last read by A(sl-1), before that barrier
                 bf16_t* dS_a = dSs + (sl & 1) * TP * Z::SDS;
                 bwd_slice_a<HS, KK>(R, Qs + cur * 32 * SL, Ds + cur * 32 * SL, lse_cur + q0, del_s + cur * 32,
                                     dS_a + key0 * Z::SDS, c, lane);
+                ATTN_STAMP(1);
                 if (sl > 0)
                     bwd_slice_b<HS, NSL, NW>(Kimg + kb * TP * SV, dSs + ((sl - 1) & 1) * TP * Z::SDS, dq, C3,
                                              q0 - 32, T, scale, w, lane);
+                ATTN_STAMP(2);
                 put_slice(cur ^ 1);
                 if (sl == 0 && tid < TP) lse_s[((n + 1) & 1) * TP + tid] = tid < T ? lse_n : INFINITY;
+                ATTN_STAMP(3);
                 __syncthreads();
+                ATTN_STAMP(4);
                 // the next item's K image / V rows: after the barrier, so every wave has finished
                 // this item's load_kv reads of the V rows (item start) before any block is replaced
                 put_side(kb ^ 1, sl);
+                ATTN_STAMP(5);
             } else {
                 bwd_slice_a<HS, KK>(R, Qs + cur * 32 * SL, Ds + cur * 32 * SL, lse_cur + q0, del_s + cur * 32,
                                     dSs + key0 * Z::SDS, c, lane);
@@ -1298,8 +1400,11 @@ __global__ __launch_bounds__(NKT / KK * 64, 1) void attn_bwdp_k(bf16_t* __restri
                                      (NSL - 1) * 32, T, scale, w, lane);
             __syncthreads();
         }
+        ATTN_STAMP(6);
         bwd_item_end<HS, KK>(R, dq, C, key0, T, scale,
-                         dsum ? dsum + ((long long)((bh / NH) * NW + w) * NH + bh % NH) * 3 * HS : nullptr, lane);
+                             dsum ? dsum + ((long long)((bh / NH) * NW + w) * NH + bh % NH) * 3 * HS : nullptr, lane,
+                             it);
+        ATTN_STAMP(7);
         if (has_next) {
             kb ^= 1;
             load_kv(R, kb);  // every block was put before the item's last barrier

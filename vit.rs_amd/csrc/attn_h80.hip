@@ -5,3 +5,9 @@
 namespace vit {
 VIT_FA_DEFINE(80)
 }  // namespace vit
+
+#if VIT_ATTN_DIAG & 4
+extern "C" int vit_attn_trace_read_h80(void* host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(vit::fa::attn_trace), sizeof(vit::fa::attn_trace));
+}
+#endif
