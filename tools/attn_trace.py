@@ -68,12 +68,33 @@ def show_bwd1(tr, nsl):
         print(f"  w{w} " + " ".join(f"{x:9.0f}" for x in d))
 
 
+def show_fwd(tr, nqt):
+    nw = 4
+    k = tr[:, 15, :nw]
+    print(f"forward, cycles (mean over blocks 0-7): K/V staging {(k[..., 1] - k[..., 0]).mean():.0f}, "
+          f"barrier {(k[..., 2] - k[..., 1]).mean():.0f}, tile loop {(k[..., 3] - k[..., 2]).mean():.0f}, "
+          f"workgroup {(k[..., 3] - k[..., 0]).mean():.0f}")
+    names = ["S", "softmax", "PV", "store", "to next"]
+    print("tile " + " ".join(f"{n:>9s}" for n in names))
+    for r in range((nqt + 3) // 4):
+        rows = []
+        for w in range(nw):
+            if w + 4 * r >= nqt:
+                continue
+            d = [tr[:, r, w, j + 1] - tr[:, r, w, j] for j in range(4)]
+            nxt = tr[:, r + 1, w, 0] if w + 4 * (r + 1) < nqt else k[:, w, 3]
+            d.append(nxt - tr[:, r, w, 4])
+            rows.append([np.mean(x) for x in d])
+        print(f"{r:4d} " + " ".join(f"{x:9.0f}" for x in np.mean(rows, axis=0)))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--T", type=int, default=197)
     ap.add_argument("--NH", type=int, default=12)
     ap.add_argument("--hs", type=int, default=64)
+    ap.add_argument("--fwd", action="store_true", help="trace the forward kernel instead")
     args = ap.parse_args()
     B, T, NH, hs = args.batch, args.T, args.NH, args.hs
     C = hs * NH
@@ -87,15 +108,18 @@ def main():
     lse = vit.DeviceArray.zeros(B * NH * T, np.float32)
     dqkv = vit.DeviceArray.zeros(B * T * 3 * C, np.uint16)
     dbias = vit.DeviceArray.zeros(3 * C, np.float32)
-    L.attention_forward_fused_bf16(out.ptr, lse.ptr, qkv.ptr, B, T, C, NH)
-    for _ in range(3):
+    for _ in range(3 if args.fwd else 1):
+        L.attention_forward_fused_bf16(out.ptr, lse.ptr, qkv.ptr, B, T, C, NH)
+    for _ in range(0 if args.fwd else 3):
         L.attention_backward_fused_bf16_ex(dqkv.ptr, dout.ptr, qkv.ptr, out.ptr, lse.ptr, B, T, C, NH, dbias.ptr)
     L.vit_sync()
     tr = np.zeros(8 * 16 * 16 * 16, np.uint64)
     fn = getattr(raw, f"vit_attn_trace_read_h{hs}")
     assert fn(tr.ctypes.data_as(ctypes.c_void_p)) == 0
     tr = tr.reshape(8, 16, 16, 16).astype(np.int64)  # [block][record][wave][stamp]
-    if tr[0, 15, 0, 1] != 0 and tr[0, 15, 0, 6] != 0:
+    if args.fwd:
+        show_fwd(tr, (T + 15) // 16)
+    elif tr[0, 15, 0, 1] != 0 and tr[0, 15, 0, 6] != 0:
         show_bwd1(tr, (T + 31) // 32)
     else:
         show_bwdp(tr)

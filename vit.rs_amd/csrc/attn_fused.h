@@ -23,6 +23,26 @@
 namespace vit {
 namespace fa {
 
+// diagnostic builds only (tools/bench_attn.py on a -DVIT_ATTN_DIAG=n library; outputs wrong):
+// bit 0 = the persistent backward issues no global loads inside its item loop, bit 1 = no dQ / dK / dV stores
+#ifndef VIT_ATTN_DIAG
+#define VIT_ATTN_DIAG 0
+#endif
+// bit 2: per-wave s_memtime stamps of the forward and both backward forms (blocks < 8, 16 records of
+// 16 stamps per wave) into attn_trace, read with vit_attn_trace_read_h<HS> (tools/attn_trace.py)
+#if VIT_ATTN_DIAG & 4
+static __device__ unsigned long long attn_trace[8 * 16 * 16 * 16];
+#define ATTN_STAMP(k)                                                                                   \
+    do {                                                                                                \
+        if (blockIdx.x < 8 && it < 16 && lane == 0)                                                     \
+            attn_trace[((blockIdx.x * 16 + it) * 16 + w) * 16 + (k)] = __builtin_amdgcn_s_memtime();   \
+    } while (0)
+#else
+#define ATTN_STAMP(k) \
+    do {              \
+    } while (0)
+#endif
+
 constexpr float LOG2E = 1.4426950408889634f;
 
 template <int HS>
@@ -197,6 +217,8 @@ __global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* 
     const long long C3 = 3LL * C;
     const bf16_t* base = qkv + (long long)b * T * C3 + h * HS;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, g = lane >> 4;
+    [[maybe_unused]] int it = 15;  // ATTN_STAMP record
+    ATTN_STAMP(0);
     // Q fragments of a 16-query tile straight from HBM (rows >= T -> 0); the next tile's are
     // requested while the current one computes, the first ones before the K/V staging
     auto load_q = [&](int qt, bf16x8_t (&qf)[G::KS]) {
@@ -213,10 +235,14 @@ __global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* 
         const long long ld[2] = {C3, C3};
         load_images<HS, TP, 256, 2>(img, st, src, ld, T);
     }
+    ATTN_STAMP(1);
     __syncthreads();
+    ATTN_STAMP(2);
     const float c = LOG2E / sqrtf((float)HS);
     for (int qt = w; qt < nqt; qt += 4) {
         const int q = qt * 16 + i;
+        it = qt / 4;
+        ATTN_STAMP(0);
         bf16x8_t qf[G::KS];
 #pragma unroll
         for (int s = 0; s < G::KS; s++) qf[s] = qn[s];
@@ -229,30 +255,34 @@ __global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* 
             for (int s = 0; s < G::KS; s++) a = mfma(frag_row<HS>(Ks, G::SK, kt * 16, s, lane), qf[s], a);
             sacc[kt] = a;
         }
-        // lane (i,g) holds S^T[key = 16kt+4g+r][q]
+        ATTN_STAMP(1);
+        // lane (i,g) holds S^T[key = 16kt+4g+r][q]: the maximum of the raw scores (c > 0 commutes with
+        // it), then p = 2^(s c - max c) as one FMA (a per-key-tile branch around the padded-key mask
+        // measured slower: 107 vs 104 us, it splits the block the scheduler interleaves)
         float mx = -INFINITY;
 #pragma unroll
         for (int kt = 0; kt < NKT; kt++)
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                const int key = kt * 16 + 4 * g + r;
-                const float x = key < T ? sacc[kt][r] * c : -INFINITY;
+                const float x = kt * 16 + 4 * g + r < T ? sacc[kt][r] : -INFINITY;
                 sacc[kt][r] = x;
                 mx = fmaxf(mx, x);
             }
         mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        mx *= c;
         float l = 0.f;
 #pragma unroll
         for (int kt = 0; kt < NKT; kt++)
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                const float p = fexp2(sacc[kt][r] - mx);
+                const float p = fexp2(fmaf(sacc[kt][r], c, -mx));
                 sacc[kt][r] = p;
                 l += p;
             }
         l += __shfl_xor(l, 16, 64);
         l += __shfl_xor(l, 32, 64);
+        ATTN_STAMP(2);
         f32x4_t o[G::DT];
 #pragma unroll
         for (int dt = 0; dt < G::DT; dt++) o[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -262,6 +292,7 @@ __global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* 
 #pragma unroll
             for (int dt = 0; dt < G::DT; dt++) o[dt] = mfma(frag_tr(Vs, G::SV, 32 * ks, 16 * dt, lane), pb, o[dt]);
         }
+        ATTN_STAMP(3);
         if (q < T) {
             const float inv = 1.0f / l;
             bf16_t* dst = out + ((long long)b * T + q) * C + h * HS + 4 * g;
@@ -269,7 +300,10 @@ __global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* 
             for (int dt = 0; dt < G::DT; dt++) store4(dst + 16 * dt, o[dt], inv);
             if (g == 0) lse[(long long)bh * T + q] = mx + log2f(l);
         }
+        ATTN_STAMP(4);
     }
+    it = 15;
+    ATTN_STAMP(3);
 }
 
 // --------------------------------------------------------------------------------- backward
@@ -652,25 +686,7 @@ constexpr int ATTN_PART_ROWS = 16;   // column-sum partial rows per (b,h) a back
 #ifndef VIT_ATTN_SW_SLICE
 #define VIT_ATTN_SW_SLICE 1
 #endif
-// diagnostic builds only (tools/bench_attn.py on a -DVIT_ATTN_DIAG=n library; outputs wrong):
-// bit 0 = the persistent backward issues no global loads inside its item loop, bit 1 = no dQ / dK / dV stores
-#ifndef VIT_ATTN_DIAG
-#define VIT_ATTN_DIAG 0
-#endif
-// bit 2: per-wave s_memtime stamps of the persistent backward's slice loop (blocks < 8, the first 16
-// slices) into attn_trace (read with vit_attn_trace_read, attn_h64.hip)
-#if VIT_ATTN_DIAG & 4
-static __device__ unsigned long long attn_trace[8 * 16 * 16 * 16];
-#define ATTN_STAMP(k)                                                                                   \
-    do {                                                                                                \
-        if (blockIdx.x < 8 && it < 16 && lane == 0)                                                     \
-            attn_trace[((blockIdx.x * 16 + it) * 16 + w) * 16 + (k)] = __builtin_amdgcn_s_memtime();   \
-    } while (0)
-#else
-#define ATTN_STAMP(k) \
-    do {              \
-    } while (0)
-#endif
+
 template <int HS>
 constexpr bool sw_slice() { return HS == 64 && VIT_ATTN_SW_SLICE; }
 #ifndef VIT_ATTN_SW_DS
@@ -1030,7 +1046,7 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
     bf16_t* dq = dqkv + (long long)b * T * C3 + h * HS;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, i = lane & 15;
     const int key0 = w * 32;
-    int it = 15;  // ATTN_STAMP record: kernel-level stamps in record 15, slice sl in record sl
+    [[maybe_unused]] int it = 15;  // ATTN_STAMP record: kernel-level stamps in record 15, slice sl in record sl
     ATTN_STAMP(0);
     BwdRegs<HS> R;
     // the wave's V fragments (rows >= T -> 0), requested first so their latency hides
