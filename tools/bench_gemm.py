@@ -18,6 +18,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from vitpkg import vit  # noqa: E402
 
 
+FP8 = 108  # pseudo-variant column: the MXFP8 engine
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
@@ -31,7 +34,7 @@ def main():
                          "4 = g2 prefetch depth 3); default 0 (and 2 with --no-epi)")
     ap.add_argument("--only", default=None, help="comma-separated GEMM names")
     ap.add_argument("--fp8", action="store_true",
-                    help="also time the MXFP8 engine (variant 8) on the forward / dgrad GEMMs")
+                    help="also time the MXFP8 engine (column v108) on the forward / dgrad GEMMs")
     args = ap.parse_args()
     L = vit.lib()
     assert L.vit_init(0) == 0
@@ -77,11 +80,11 @@ def main():
     if args.only:
         keep = set(args.only.split(","))
         g = [x for x in g if x[0] in keep]
-    variants = [int(v) for v in args.variants.split(",")] + ([8] if args.fp8 else [])
+    variants = [int(v) for v in args.variants.split(",")] + ([FP8] if args.fp8 else [])
     modes = [int(x) for x in args.modes.split(",")] if args.modes else ([0, 2] if args.no_epi else [0])
 
     def run(name, M, N, K, ak, lda, bk, ldb, epi, var=2):
-        if var == 8:
+        if var == FP8:
             if epi == 2:
                 return
             aux = aux16.ptr if epi in (6, 9) else (aux32.ptr if epi == 5 else None)
@@ -103,12 +106,12 @@ def main():
         for sh in g:
             for var in variants:
                 for mode in modes:
-                    if var == 8 and sh[8] == 2:
+                    if var == FP8 and sh[8] == 2:
                         continue
-                    if var == 8:  # operands of this shape quantized (untimed)
+                    if var == FP8:  # operands of this shape quantized (untimed)
                         L.quantize_mx_bf16_ex(q_act.ptr, s_act.ptr, act.ptr, sh[1], sh[3], sh[3], sh[3])
                         L.quantize_mx_bf16_ex(q_w.ptr, s_w.ptr, wts.ptr, sh[2], sh[3], sh[3], sh[3])
-                    L.gemm_bf16_set_variant(var if var != 8 else 2)
+                    L.gemm_bf16_set_variant(var if var != FP8 else 0)
                     L.gemm_bf16_set_debug(mode)
                     for _ in range(2):
                         run(*sh, var=var)
@@ -142,7 +145,7 @@ def main():
     fl_all = sum(2.0 * x[1] * x[2] * x[3] for x in g)
     print("total per layer: " + "  ".join(
         f"v{v}/f{m} {tot[(v, m)]:.3f} ms ({fl_all / tot[(v, m)] / 1e9:.0f} TF/s)"
-        for v in variants for m in modes if v != 8))
+        for v in variants for m in modes if v != FP8))
 
 
 if __name__ == "__main__":
