@@ -512,12 +512,16 @@ __global__ __launch_bounds__(TOK * 2) void quantize_mx_cols_k(uint8_t* __restric
         }
         return;
     }
+    u32x4 vl[4];  // all four pieces requested first (clamped rows: unconditional loads)
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const int idx = i * NT + tid, row = idx >> 3, ch = idx & 7;
-        u32x4 v = u32x4{0u, 0u, 0u, 0u};
-        if (tok0 + row < R) v = *reinterpret_cast<const u32x4*>(x + (long long)(tok0 + row) * ldx + col0 + ch * 8);
-        *reinterpret_cast<u32x4*>(tile + row * 64 + ch * 8) = v;
+        vl[i] = *reinterpret_cast<const u32x4*>(x + (long long)min(tok0 + row, R - 1) * ldx + col0 + ch * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int idx = i * NT + tid, row = idx >> 3, ch = idx & 7;
+        *reinterpret_cast<u32x4*>(tile + row * 64 + ch * 8) = tok0 + row < R ? vl[i] : u32x4{0u, 0u, 0u, 0u};
     }
     __syncthreads();
     if (tb >= Kp) return;
@@ -573,11 +577,19 @@ __global__ __launch_bounds__(TOK * 2 * (COLS / 64)) void quantize_mx_rowcol_k(ui
         }
         return;
     }
+    // every row piece requested before the first is used (the clamped row keeps the load unconditional;
+    // a "zero, then load if in range" form made each iteration wait for its own load)
+    constexpr int NI = TOK * G8 / NT;
+    u32x4 wl[NI];
 #pragma unroll
-    for (int i = 0; i < TOK * G8 / NT; i++) {
+    for (int i = 0; i < NI; i++) {
+        const int idx = i * NT + tid, row = idx / G8, ch = idx % G8;
+        wl[i] = *reinterpret_cast<const u32x4*>(x + (long long)min(tok0 + row, R - 1) * ldx + col0 + ch * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < NI; i++) {
         const int idx = i * NT + tid, row = idx / G8, ch = idx % G8, tok = tok0 + row;
-        u32x4 w = u32x4{0u, 0u, 0u, 0u};
-        if (tok < R) w = *reinterpret_cast<const u32x4*>(x + (long long)tok * ldx + col0 + ch * 8);
+        const u32x4 w = tok < R ? wl[i] : u32x4{0u, 0u, 0u, 0u};
         *reinterpret_cast<u32x4*>(tile + row * COLS + ch * 8) = w;
         float v[8];
         float amax = 0.f;
