@@ -717,8 +717,9 @@ __global__ __launch_bounds__(256) void transpose_bf16_k(bf16_t* __restrict__ out
 #pragma unroll
     for (int h = 0; h < 2; h++) {  // 256 threads x 2 x 8 elements = the 64 x 64 tile
         const int r = r0 + tr, c = c0 + tc + h * 8;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (r < R && c < Cc) v = *reinterpret_cast<const uint4*>(in + mo + (long long)r * Cc + c);
+        // clamped address, zeros selected after the load (no load behind a branch)
+        const uint4 ld = *reinterpret_cast<const uint4*>(in + mo + (long long)min(r, R - 1) * Cc + min(c, Cc - 8));
+        const uint4 v = (r < R && c < Cc) ? ld : make_uint4(0, 0, 0, 0);
         const uint16_t* e = reinterpret_cast<const uint16_t*>(&v);
 #pragma unroll
         for (int j = 0; j < 8; j++) tile[tr][tc + h * 8 + j] = e[j];
