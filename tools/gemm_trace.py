@@ -68,6 +68,8 @@ def main():
     ap.add_argument("--variants", default="2,5")
     ap.add_argument("--only", default="fwd_fc,fwd_qkv,fwd_proj")
     ap.add_argument("--stagger", type=int, default=0, help="first-round stagger, 0.5 us units (g4 engines)")
+    ap.add_argument("--M", type=int, default=0, help="token rows (default 50432; 25216 = one micro-batch)")
+    ap.add_argument("--per-round", action="store_true", help="persistent engine: tile times by round")
     args = ap.parse_args()
     L = vit.lib()
     assert L.vit_init(0) == 0
@@ -86,6 +88,8 @@ def main():
     trace = vit.DeviceArray.zeros(16 * 8192, np.uint64)
     for name in args.only.split(","):
         M, N, K, epi = SHAPES[name]
+        if args.M:
+            M = args.M
         for var in [int(v) for v in args.variants.split(",")]:
             L.gemm_bf16_set_variant(var)
             L.gemm_bf16_set_debug(args.stagger * 256)
@@ -112,6 +116,23 @@ def main():
                   f"CUs {r['cus']}  wg/CU {r['wg_per_cu']:.1f}  resident {r['max_resident']}  "
                   f"epi beside other's main loop {r['epi_overlap']:.2f}  turnaround {r['turnaround_us']:.2f} us",
                   flush=True)
+            if args.per_round:  # tiles of each CU in start order: round j = the CU's j-th tile
+                t0, t1 = tr[:, 0].astype(np.int64), tr[:, 1].astype(np.int64)
+                t2 = tr[:, 4:12].astype(np.int64).max(1)
+                hw = tr[:, 3]
+                cu = (hw >> 32) * 4096 + ((hw & 0xFFFFFFFF) >> 8 & 0xFF)
+                rounds = collections.defaultdict(list)
+                by = collections.defaultdict(list)
+                for k in range(len(t0)):
+                    by[int(cu[k])].append(k)
+                for ks in by.values():
+                    for j, k in enumerate(sorted(ks, key=lambda k: t0[k])):
+                        rounds[j].append(k)
+                base = t0.min()
+                for j in sorted(rounds):
+                    ks = np.array(rounds[j])
+                    print(f"    round {j}: {len(ks):4d} tiles  start {np.mean(t0[ks] - base) * 0.01:7.1f} us  "
+                          f"main {np.mean(t1[ks] - t0[ks]) * 0.01:6.2f}  epi {np.mean(t2[ks] - t1[ks]) * 0.01:6.2f} us", flush=True)
     L.gemm_bf16_set_debug(0)
     L.gemm_bf16_set_variant(0)
 
