@@ -71,6 +71,42 @@ def _gelu_grad64(x):
     return 0.5 * (1 + th) + 0.5 * x * (1 - th * th) * s * (1 + 3 * 0.044715 * x * x)
 
 
+@pytest.mark.parametrize("M,N,K", [(16384, 8448, 64), (16424, 8452, 64), (16424, 8452, 128), (5000, 1284, 64)])
+def test_gemm_fp8_streaming_short_k_matches_one_tile(gpu, M, N, K):
+    """The persistent fp8 engine (production variant 7) against the one-tile engine (variant 2) at the
+    shortest K (one or two 64-deep steps) with more than 512 tiles (three or more tiles per workgroup)
+    and ragged M / N: K = 64 must take the one-tile engine (the streaming ring fetches two steps
+    ahead), K = 128 streams; the outputs are bit-identical either way."""
+    v = gpu
+    L = v.lib()
+    rng = np.random.default_rng(M + N + K)
+    a = rng.normal(size=(M, K)).astype(np.float32)
+    w = (rng.normal(size=(N, K)) * 0.05).astype(np.float32)
+    qa, sa, _, _ = quant_gpu(v, a, "bf16")
+    qw, sw, _, _ = quant_gpu(v, w, "f32")
+    bias = D(v, rng.normal(size=N).astype(np.float32))
+    res = D(v, rng.normal(size=(M, N)).astype(np.float32))
+    outs = {}
+    try:
+        for var in (2, 7):
+            L.gemm_bf16_set_variant(var)
+            o = []
+            for epi in (0, 3, 5, 8):
+                c = Z(v, M * N, np.float32 if epi in (0, 5) else np.uint16)
+                c2 = Z(v, M * N, np.uint16) if epi == 8 else None
+                v.call("gemm_fp8_fused", c, c2, N, res if epi == 5 else None, N if epi == 5 else 0, qa, sa, K,
+                       qw, sw, K, bias if epi != 3 else None, None, M, N, K, epi)
+                o.append(c.numpy())
+                if c2 is not None:
+                    o.append(c2.numpy())
+            outs[var] = o
+    finally:
+        L.gemm_bf16_set_variant(0)
+    for x, y in zip(outs[2], outs[7]):
+        assert np.array_equal(x, y)
+    assert np.abs(outs[7][0]).max() > 0
+
+
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 520, 128), (1576, 768, 192), (2056, 1280, 1280),
                                    (777, 3840, 320)])
 def test_gemm_fp8_epilogues(gpu, M, N, K):

@@ -2,9 +2,12 @@
 # One parameterised runner for the GPU box (replaces the per-experiment gpu_run*.sh scripts).
 #   gpurun -- bash tools/gpu_job.sh <job> [args...]
 # jobs (every GPU step has its own time limit; steps chain with &&, so the first failure ends it):
-#   tests [pytest args]   python -m pytest -m gpu (default: all GPU tests) -> gpurun_out/tests.log
-#   smoke                 __graft_entry__.smoke()                          -> gpurun_out/smoke.log
-#   bench [bench args]    python bench.py ...                              -> gpurun_out/bench.json
+#   tests [pytest args]   python -m pytest -m gpu (default: all GPU tests) -> gpurun_out/tests.<stamp>.log
+#   smoke                 __graft_entry__.smoke()                          -> gpurun_out/smoke.<stamp>.log
+#   bench [bench args]    python bench.py ...                              -> gpurun_out/bench.<stamp>.json
+# Every call writes its own timestamped log (<stamp> = UTC date-time + pid), so a run that is
+# killed leaves its log next to the retry's (gpurun_out/ is merged back, never overwritten); the
+# un-stamped names are symlinks to the newest one.
 #   attn [bench_attn args] tools/bench_attn.py                             -> stdout
 #   gemm [bench_gemm args] tools/bench_gemm.py                             -> stdout
 #   profile TAG           tools/profile.sh TAG (bench + rocprofv3 stats + PMC passes)
@@ -15,19 +18,24 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 job=${1:?job}; shift
+stamp=$(date -u +%Y%m%dT%H%M%S).$$
+keep() { ln -sfn "$(basename "$1")" "gpurun_out/$2"; }
 case "$job" in
   tests)
+    log=gpurun_out/tests.$stamp.log; keep "$log" tests.log
     timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "$@" \
-        > gpurun_out/tests.log 2>&1; rc=$?; tail -25 gpurun_out/tests.log; exit $rc ;;
+        > "$log" 2>&1; rc=$?; tail -25 "$log"; exit $rc ;;
   smoke)
-    timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tee gpurun_out/smoke.log ;;
+    log=gpurun_out/smoke.$stamp.log; keep "$log" smoke.log
+    timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tee "$log" ;;
   bench)
-    timeout -k 10 600 python3 bench.py "$@" > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?
-    cat gpurun_out/bench.json; tail -5 gpurun_out/bench.err; exit $rc ;;
+    out=gpurun_out/bench.$stamp.json; keep "$out" bench.json; keep "gpurun_out/bench.$stamp.err" bench.err
+    timeout -k 10 600 python3 bench.py "$@" > "$out" 2> "gpurun_out/bench.$stamp.err"; rc=$?
+    cat "$out"; tail -5 "gpurun_out/bench.$stamp.err"; exit $rc ;;
   attn)
-    timeout -k 10 300 python3 tools/bench_attn.py "$@" ;;
+    timeout -k 10 300 python3 tools/bench_attn.py "$@" 2>&1 | tee "gpurun_out/attn.$stamp.log" ;;
   gemm)
-    timeout -k 10 300 python3 tools/bench_gemm.py "$@" ;;
+    timeout -k 10 300 python3 tools/bench_gemm.py "$@" 2>&1 | tee "gpurun_out/gemm.$stamp.log" ;;
   profile)
     bash tools/profile.sh "$@" ;;
   ktrace)
@@ -36,6 +44,6 @@ case "$job" in
         -- python3 bench.py "$@" > "gpurun_out/$tag.json" 2> "gpurun_out/$tag.err" && echo "ktrace $tag ok" ;;
   py)
     script=${1:?script}; shift
-    timeout -k 10 600 python3 "$script" "$@" ;;
+    timeout -k 10 600 python3 "$script" "$@" 2>&1 | tee "gpurun_out/py.$(basename "$script" .py).$stamp.log" ;;
   *) echo "unknown job $job"; exit 2 ;;
 esac

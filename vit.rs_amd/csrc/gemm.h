@@ -92,8 +92,11 @@ bool gemm_bf16_supported(const GemmArgs& a);
 // engine selection for A/B measurements in one process: 1 = 128x128 everywhere, 2 = production
 // (256x256, 1 WG/CU; split-K weight gradients on 256x128, 2 WG/CU), 4 = 256x128 everywhere;
 // anything else = 2.  Debug flag 2 = skip the epilogues (main-loop-only timing).
+// 0 (or any unknown value) clears the selection: the next GEMM re-reads VIT_GEMM (default 7)
 void gemm_set_variant(int v);
 void gemm_set_debug(int flags);
+// compute units of the current device: the persistent engines' grid (one workgroup per CU)
+int gemm_cu_count();
 void gemm_set_trace(unsigned long long* trace);
 bool gemm_streaming();  // the production variant: persistent streaming engines (bf16 and fp8)
 

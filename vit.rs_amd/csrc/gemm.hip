@@ -1206,8 +1206,18 @@ static int gemm_variant() {
     }
     return g_variant;
 }
-// 0 (or any unknown value) restores the default
-void gemm_set_variant(int v) { g_variant = known_variant(v) ? v : kDefaultVariant; }
+// 0 (or any unknown value) clears the selection, so the next call re-reads VIT_GEMM (an A/B run
+// under VIT_GEMM=2 stays on variant 2 after a test fixture's reset)
+void gemm_set_variant(int v) { g_variant = known_variant(v) ? v : -1; }
+int gemm_cu_count() {
+    static int n = [] {
+        int dev = 0, cu = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
+        return cu > 0 ? cu : 256;
+    }();
+    return n;
+}
 bool gemm_streaming() { return gemm_variant() == 7; }
 void gemm_set_debug(int flags) { g_debug_flags = flags; }
 static unsigned long long* g_trace = nullptr;
@@ -1344,10 +1354,12 @@ static void launch_bf16(const GemmArgs& a, const GemmParams& p, dim3 grid, hipSt
 template <bool AK, bool BKC>
 static void launch_g2(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStream_t s) {
     if constexpr (AK && BKC) {
-        // persistent streaming engine: one workgroup per CU (at most one per tile), no split-K
-        if (gemm_variant() == 7 && grid.y == 1 && (long long)p.M * p.lda * 2 < (1LL << 31) &&
+        // persistent streaming engine: one workgroup per CU (at most one per tile), no split-K;
+        // its DMA ring runs two K-steps ahead across one tile boundary, so K >= 2 steps
+        if (gemm_variant() == 7 && grid.y == 1 && p.K >= 2 * g2::BK && (long long)p.M * p.lda * 2 < (1LL << 31) &&
             (long long)p.N * p.ldb * 2 < (1LL << 31)) {
-            const dim3 pg(grid.x < 256 ? grid.x : 256);
+            const int cus = gemm_cu_count();
+            const dim3 pg((int)grid.x < cus ? grid.x : cus);
             switch (a.epi) {
 #define VIT_CASE(E) \
     case E: g2::gemm_kernel_s<E><<<pg, g2::NT, 0, s>>>(p); return;

@@ -696,10 +696,12 @@ void gemm_fp8(const GemmArgs& a, hipStream_t s) {
     // DMA offsets; not for the aux x product epilogues (6 / 9: with both MX outputs their epilogue
     // outgrows the registers the streaming state leaves and spills; measured 8 % slower than the
     // one-tile kernel on the ViT-H/14 fcproj input gradient)
-    if (split == 1 && gemm_streaming() && b.epi != EPI_F32_ACC && !epi_aux16(b.epi) &&
+    // (its DMA ring fetches two K-steps ahead across one tile boundary: K >= 2 steps)
+    if (split == 1 && gemm_streaming() && b.epi != EPI_F32_ACC && !epi_aux16(b.epi) && a.K >= 2 * f8::KB &&
         (long long)a.M * a.lda < (1LL << 31) &&
         (long long)a.N * a.ldb < (1LL << 31)) {
-        const dim3 pg(tiles < 256 ? tiles : 256);
+        const int cus = gemm_cu_count();
+        const dim3 pg(tiles < cus ? tiles : cus);
         switch (b.epi) {
 #define VIT_CASE(E) \
     case E: f8::gemm_kernel_s<E><<<pg, f8::NT, 0, s>>>(fp); break;
