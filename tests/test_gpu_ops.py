@@ -356,11 +356,12 @@ def test_error_channel(gpu):
 
 
 # ------------------------------------------------------------------ generic bf16 GEMM engine
-@pytest.fixture(params=[2, 4, 5, 7])
+@pytest.fixture(params=[2, 4, 5, 7, 9])
 def engine(request, gpu):
     """Run a test under each production GEMM engine (2 = 256x256 one workgroup per CU, with the split-K
     weight gradients on 256x128; 4 = 256x128 two per CU everywhere; 5 = as 4 with the
-    software-pipelined main loop for K-contiguous operands), then restore the default."""
+    software-pipelined main loop for K-contiguous operands; 7 = persistent streaming 256x256, 9 = its
+    one-wave-per-SIMD 128x128-per-wave form), then restore the default."""
     gpu.lib().gemm_bf16_set_variant(request.param)
     yield request.param
     gpu.lib().gemm_bf16_set_variant(0)
@@ -396,7 +397,7 @@ def test_gemm_bf16_layouts(gpu, engine, M, N, K, ak, bk):
             assert rel_err(dbias.numpy(), ar.sum(1)) < 2e-3
 
 
-@pytest.mark.parametrize("pair", [(4, 5), (2, 7)])
+@pytest.mark.parametrize("pair", [(4, 5), (2, 7), (2, 9)])
 @pytest.mark.parametrize("M,N,K", [(6304, 3072, 768), (1576, 768, 3072), (520, 384, 256), (776, 1000, 128),
                                    (50432, 768, 768)])
 def test_gemm_bf16_pipelined_bit_identical(gpu, M, N, K, pair):
@@ -404,7 +405,8 @@ def test_gemm_bf16_pipelined_bit_identical(gpu, M, N, K, pair):
     256x128 main loop (variant 5, g4::gemm_kernel_pipe) against the 256x128 engine (4), and the
     persistent streaming 256x256 engine (7, g2::gemm_kernel_s: tiles walked per CU, the next tile's
     first K-steps fetched under the epilogue, 32-row staging) against the one-tile 256x256 engine
-    (2).  Same MFMAs in the same K order per accumulator and the same epilogue arithmetic: every
+    (2), and the one-wave-per-SIMD persistent engine (9, g5::gemm_kernel_w4: 128 x 128 per wave, one
+    barrier per 32-deep K-step) against it too.  Same MFMAs in the same K order per accumulator and the same epilogue arithmetic: every
     fused epilogue of the trainer (bf16 store, GELU pair, fp32 residual, x aux + column sums)
     bit-identical, at the trainer's K (768, 3072), its M (50 432 = 197 full 256-row tiles: several
     tiles per CU) and ragged M / N."""

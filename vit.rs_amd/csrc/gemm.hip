@@ -1196,7 +1196,7 @@ __global__ __launch_bounds__(256) void slab_reduce_k(float* __restrict__ C, long
 //   epilogues (main-loop-only timing; results are garbage).
 static int g_variant = -1;
 static int g_debug_flags = 0;
-static bool known_variant(int v) { return v == 1 || v == 2 || v == 4 || v == 5 || v == 7; }
+static bool known_variant(int v) { return v == 1 || v == 2 || v == 4 || v == 5 || v == 7 || v == 9; }
 static constexpr int kDefaultVariant = 7;
 static int gemm_variant() {
     if (g_variant < 0) {
@@ -1218,7 +1218,7 @@ int gemm_cu_count() {
     }();
     return n;
 }
-bool gemm_streaming() { return gemm_variant() == 7; }
+bool gemm_streaming() { return gemm_variant() == 7 || gemm_variant() == 9; }
 void gemm_set_debug(int flags) { g_debug_flags = flags; }
 static unsigned long long* g_trace = nullptr;
 void gemm_set_trace(unsigned long long* trace) { g_trace = trace; }
@@ -1354,6 +1354,8 @@ static void launch_bf16(const GemmArgs& a, const GemmParams& p, dim3 grid, hipSt
 template <bool AK, bool BKC>
 static void launch_g2(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStream_t s) {
     if constexpr (AK && BKC) {
+        // one-wave-per-SIMD persistent engine (gemm_w4.hip)
+        if (gemm_variant() == 9 && grid.y == 1 && gemm_bf16_w4(a, p, (int)grid.x, s)) return;
         // persistent streaming engine: one workgroup per CU (at most one per tile), no split-K;
         // its DMA ring runs two K-steps ahead across one tile boundary, so K >= 2 steps
         if (gemm_variant() == 7 && grid.y == 1 && p.K >= 2 * g2::BK && (long long)p.M * p.lda * 2 < (1LL << 31) &&
@@ -1508,7 +1510,7 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s) {
     // split-K weight gradients (M/N-contiguous operands, K = the token count) run on the 256x128
     // two-per-CU engine: 3-9 % faster than 256x256 on every ViT-B/16 wgrad shape (r02,
     // tools/bench_gemm.py), the other GEMMs are faster on 256x256
-    if ((gemm_variant() == 2 || gemm_variant() == 7) && a.epi == EPI_F32_ATOMIC && !a.a_kcontig && !a.b_kcontig &&
+    if ((gemm_variant() == 2 || gemm_variant() == 7 || gemm_variant() == 9) && a.epi == EPI_F32_ATOMIC && !a.a_kcontig && !a.b_kcontig &&
         a.K % g4::KTILE == 0 && a.M >= 256 && a.N >= 128 && a.N % 4 == 0 &&
         (a.splitk > 0 || !a.ws ||
          (size_t)choose_split_g4(cdiv(a.M, g4::BM) * cdiv(a.N, g4::BN), a.K / g4::KTILE) * a.M * a.N * sizeof(float) <=

@@ -223,7 +223,7 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, int m, int n, f32x
 // Columns n..n+7 of row m (n % 8 == 0), v = raw accumulators: one 16-B (bf16) or 2 x 16-B (fp32)
 // access per lane and operand, so a wave instruction covers whole 128-B lines.  cs accumulates
 // the column sums of the DGELU output (fused bias gradient).
-template <int EPI>
+template <int EPI, bool MX = true>
 __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, float (&v)[8],
                                           float (&cs)[8], int lane = 0, float* wb = nullptr) {
     if constexpr (epi_bias(EPI)) {
@@ -263,8 +263,10 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, flo
         *reinterpret_cast<uint4*>((bf16_t*)p.C + off) = pack8(v);
         const uint4 g8 = pack8(gv);
         if (p.C2) *reinterpret_cast<uint4*>((bf16_t*)p.C2 + off) = g8;
-        if (p.mx_q) mx_out8(p, m, n, g8.x, g8.y, g8.z, g8.w, lane);
-        if (wb) stage_back8(wb, g8.x, g8.y, g8.z, g8.w);
+        if constexpr (MX) {
+            if (p.mx_q) mx_out8(p, m, n, g8.x, g8.y, g8.z, g8.w, lane);
+            if (wb) stage_back8(wb, g8.x, g8.y, g8.z, g8.w);
+        }
     } else if constexpr (EPI == EPI_F32_RESID) {
         const float* r = (const float*)p.aux + (long long)m * p.ldaux + n;
         const float4 r0 = reinterpret_cast<const float4*>(r)[0];
@@ -279,8 +281,10 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, flo
         *reinterpret_cast<uint4*>((bf16_t*)p.C + off) = pack8(dv);
         const uint4 g8 = pack8(gv);
         if (p.C2) *reinterpret_cast<uint4*>((bf16_t*)p.C2 + off) = g8;
-        if (p.mx_q) mx_out8(p, m, n, g8.x, g8.y, g8.z, g8.w, lane);
-        if (wb) stage_back8(wb, g8.x, g8.y, g8.z, g8.w);
+        if constexpr (MX) {
+            if (p.mx_q) mx_out8(p, m, n, g8.x, g8.y, g8.z, g8.w, lane);
+            if (wb) stage_back8(wb, g8.x, g8.y, g8.z, g8.w);
+        }
     } else if constexpr (epi_aux16(EPI)) {
         const uint4 h = *reinterpret_cast<const uint4*>((const bf16_t*)p.aux + (long long)m * p.ldaux + n);
         const uint32_t hw[4] = {h.x, h.y, h.z, h.w};
@@ -299,8 +303,10 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, flo
         for (int j = 0; j < 8; j++) cs[j] += v[j];
         const uint4 d8 = pack8(v);
         if (p.C) *reinterpret_cast<uint4*>((bf16_t*)p.C + off) = d8;
-        if (p.mx_q) mx_out8(p, m, n, d8.x, d8.y, d8.z, d8.w, lane);
-        if (wb) stage_back8(wb, d8.x, d8.y, d8.z, d8.w);
+        if constexpr (MX) {
+            if (p.mx_q) mx_out8(p, m, n, d8.x, d8.y, d8.z, d8.w, lane);
+            if (wb) stage_back8(wb, d8.x, d8.y, d8.z, d8.w);
+        }
     }
 }
 
@@ -805,7 +811,7 @@ __device__ __forceinline__ void staged_epilogue_q_any(const GemmParams& p, Stage
                             *reinterpret_cast<f4*>(st + sq_off(r, cc + 4)) = f4{wb[4], wb[5], wb[6], wb[7]};
                         }
                     } else {
-                        epilogue8<EPI>(p, m, n, v, cs, lane, nullptr);
+                        epilogue8<EPI, false>(p, m, n, v, cs, lane, nullptr);
                     }
                 } else if (n + 4 <= p.N) {
                     f32x4_t t = lo;
