@@ -101,8 +101,6 @@ struct GemmParams;
 // variant 9: the one-wave-per-SIMD persistent engine (gemm_w4.hip) for K-contiguous operands without
 // split-K (K % 64 == 0, K >= 128); false = shape not taken
 bool gemm_bf16_w4(const GemmArgs& a, const GemmParams& p, int tiles, hipStream_t s);
-// variant 9 weight gradients on the same engine (M/N-contiguous operands, split-K slabs)
-bool gemm_bf16_w4_wgrad(const GemmArgs& a, hipStream_t s);
 void gemm_set_trace(unsigned long long* trace);
 bool gemm_streaming();  // the production variant: persistent streaming engines (bf16 and fp8)
 

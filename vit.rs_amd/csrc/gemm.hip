@@ -1507,7 +1507,6 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s) {
         gemm_bf16_g4(a, s);
         return;
     }
-    if (gemm_variant() == 9 && gemm_bf16_w4_wgrad(a, s)) return;
     // split-K weight gradients (M/N-contiguous operands, K = the token count) run on the 256x128
     // two-per-CU engine: 3-9 % faster than 256x256 on every ViT-B/16 wgrad shape (r02,
     // tools/bench_gemm.py), the other GEMMs are faster on 256x256

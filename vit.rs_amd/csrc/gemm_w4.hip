@@ -32,14 +32,11 @@ namespace g5 {
 constexpr int BM = 256, BN = 256, BK = 32, NT = 256;
 constexpr int IMG_BYTES = 256 * BK * 2;    // 16 KiB per operand per slot
 constexpr int SLOT_BYTES = 2 * IMG_BYTES;  // 32 KiB (A | B)
+constexpr int NS = 4;                      // ring slots
 constexpr int STG_BYTES = 8192;            // epilogue staging per wave (32 rows x 64 fp32)
-constexpr int SMEM = 5 * SLOT_BYTES;       // 160 KiB
-// Ring slots (the DMA of step kt + NS is issued in step kt, NS - 1 steps of cover).  KC (persistent,
-// items chain): 4 slots + 32 KiB of epilogue staging.  !KC (weight gradients, one item per
-// workgroup, K-steps stream from HBM): 5 slots, the epilogue staged in slot 0 once the ring drained.
-template <bool KC>
-constexpr int ring_slots() { return KC ? 4 : 5; }
-static_assert(4 * SLOT_BYTES + 4 * STG_BYTES <= SMEM && 5 * SLOT_BYTES <= 160 * 1024, "LDS");
+constexpr int SMEM = NS * SLOT_BYTES + 4 * STG_BYTES;  // 160 KiB
+constexpr int LEAD = NS;                   // the DMA of step kt + LEAD is issued in step kt
+static_assert(SMEM <= 160 * 1024, "LDS");
 
 __device__ __forceinline__ int kc_swz(int row) { return (row >> 1) & 3; }
 
@@ -50,29 +47,20 @@ __device__ __forceinline__ void wait_vm(int n) {
         case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
         case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
         case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
-        case 32: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
         default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     }
 }
 
-// M/N-contiguous image (the weight gradients' operands, as g2::stage<false>): [32 k][256 cols] of
-// 512-B rows, 16-B chunk index XOR mn_swz(k), read with ds_read_b64_tr_b16
-__device__ __forceinline__ int mn_swz(int k) { return ((k & 3) << 2) | (((k >> 3) & 1) << 1); }
-
-// KC: both operands K-contiguous (forward / input gradient); !KC: both M/N-contiguous (weight
-// gradient dW = dout^T . inp, K = the token count, split into p.kchunk ranges: one work item per
-// (tile, K-split), EPI_F32_SLAB partial planes or EPI_F32_ACC for a single split)
-template <bool KC, int EPI>
+template <int EPI>
 __global__ __launch_bounds__(NT, 1) void gemm_kernel_w4(GemmParams p) {
     __shared__ __attribute__((aligned(1024))) char smem[SMEM];
-    constexpr int NS = ring_slots<KC>(), LEAD = NS;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 1, wn = wave & 1;
     const int ntm = cdiv(p.M, BM), ntn = cdiv(p.N, BN), tiles = ntm * ntn;
-    const int nsplit = cdiv(p.K, p.kchunk), items = tiles * nsplit;
     const int nblk = gridDim.x;
-    const int my_tiles = (items - (int)blockIdx.x + nblk - 1) / nblk;
+    const int my_tiles = (tiles - (int)blockIdx.x + nblk - 1) / nblk;
+    const int nk = p.K / BK;  // host: K % 64 == 0, K >= 128 (nk even, >= LEAD)
     const char* A = (const char*)p.A;
     const char* B = (const char*)p.B;
     f32x4_t acc[8][8];
@@ -84,42 +72,28 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_w4(GemmParams p) {
     };
     zero_acc();
     if (my_tiles <= 0) return;
-    // DMA sources of a work item: piece q of this wave's share of the A / B image (1 KiB block
-    // 4 q + wave) as 32-bit byte offsets from the operand base at the item's first k (g2's swizzles):
-    // K-contiguous 16 rows x 64 B, M/N-contiguous 2 k-rows x 512 B
+    // DMA sources of a tile: piece q of this wave's share of the A / B image (1 KiB block 4 q + wave
+    // = 16 rows x 64 B), as 32-bit byte offsets from the operand base at k = 0 (g2's swizzle)
     struct TileSrc {
-        int tm0, tn0, t, split, kbeg, nk;
+        int tm0, tn0, t;
         uint32_t a[4], b[4];
     };
-    auto src_off = [&](int row0, int lim, long long ld, int q) -> uint32_t {
-        if constexpr (KC) {
-            const int row = (q * 4 + wave) * 16 + (lane >> 2);
-            const int c = (lane & 3) ^ kc_swz(row);
-            return (uint32_t)((min(row0 + row, lim - 1) * ld + c * 8) * 2);
-        } else {
-            const int k = (q * 4 + wave) * 2 + (lane >> 5);
-            const int c = (lane & 31) ^ mn_swz(k);
-            return (uint32_t)((k * ld + min(row0 + c * 8, lim - 8)) * 2);
-        }
-    };
     auto tile_src = [&](int j, TileSrc& ts) {
-        ts.t = xcd_remap(j * nblk + (int)blockIdx.x, items);
-        ts.split = ts.t / tiles;
-        const int tt = ts.t - ts.split * tiles;
-        ts.tm0 = (tt / ntn) * BM;
-        ts.tn0 = (tt % ntn) * BN;
-        ts.kbeg = ts.split * p.kchunk;
-        ts.nk = (min(p.K, ts.kbeg + p.kchunk) - ts.kbeg) / BK;  // host: every item >= LEAD steps
+        ts.t = xcd_remap(j * nblk + (int)blockIdx.x, tiles);
+        ts.tm0 = (ts.t / ntn) * BM;
+        ts.tn0 = (ts.t % ntn) * BN;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            ts.a[q] = src_off(ts.tm0, p.M, p.lda, q);
-            ts.b[q] = src_off(ts.tn0, p.N, p.ldb, q);
+            const int row = (q * 4 + wave) * 16 + (lane >> 2);
+            const int c = (lane & 3) ^ kc_swz(row);
+            ts.a[q] = (uint32_t)((min(ts.tm0 + row, p.M - 1) * p.lda + c * 8) * 2);
+            ts.b[q] = (uint32_t)((min(ts.tn0 + row, p.N - 1) * p.ldb + c * 8) * 2);
         }
     };
     TileSrc cur, nxt;
     tile_src(0, cur);
     nxt = cur;
-    if (my_tiles > 1) tile_src(1, nxt);  // (no next item: nxt = cur, see issue())
+    if (my_tiles > 1) tile_src(1, nxt);  // (no next tile: nxt = cur, see issue())
     auto glds = [&](const char* src, char* dst) {
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
@@ -132,59 +106,28 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_w4(GemmParams p) {
     // offset, so the DMA issues in the saddr form with no per-piece 64-bit VALU address chain (an
     // in-order wave would stall its MFMA stream on that chain before every piece).
     auto issue = [&](int kt2, int sl, int q) {
-        const bool c = kt2 < cur.nk;
-        const int kk = c ? cur.kbeg + kt2 * BK : nxt.kbeg + (kt2 - cur.nk) * BK;  // first k of the step
+        const bool c = kt2 < nk;
+        const int koff = __builtin_amdgcn_readfirstlane((c ? kt2 : kt2 - nk) * (BK * 2));
         char* dst = smem + sl * SLOT_BYTES;
         if (q < 4) {
-            const long long koff = KC ? (long long)kk * 2 : (long long)kk * p.lda * 2;
             const uint32_t off = c ? cur.a[q] : nxt.a[q];
             glds(A + koff + off, dst + (q * 4 + wave) * 1024);
         } else {
-            const long long koff = KC ? (long long)kk * 2 : (long long)kk * p.ldb * 2;
             const uint32_t off = c ? cur.b[q - 4] : nxt.b[q - 4];
             glds(B + koff + off, dst + IMG_BYTES + ((q - 4) * 4 + wave) * 1024);
         }
     };
-    // fragment reads.  K-contiguous: the lane's offset inside a 16-row block (rows r0 + i, 16-B chunk g
-    // of the 32-deep k-slice); r0 % 16 == 0, so the swizzle term is lane-constant.  M/N-contiguous
-    // (g2::frag<false>): two ds_read_b64_tr_b16 per fragment (k rows 8 g + q and + 4, column r0 + i),
-    // the lane's byte offset of each of the 8 A and 8 B fragments precomputed (the swizzle depends on
-    // the fragment), read as inline asm (hipcc waits vmcnt(0) in front of the builtin form while an
-    // LDS-DMA is in flight, common.h) and retired by the step's lgkmcnt(0) wait.
+    // the lane's fragment-read offset inside a 16-row block (rows r0 + i, 16-B chunk g of the
+    // 32-deep k-slice): r0 % 16 == 0, so the swizzle term is lane-constant
     const int i16 = lane & 15, g4 = lane >> 4;
     const int foff = i16 * 64 + ((g4 ^ kc_swz(i16)) << 4);
     const int arow = wm * 128, brow = wn * 128;
-    int toff[16];
-    if constexpr (!KC) {
-        const int q = i16 >> 2, pp = i16 & 3, k0 = 8 * g4 + q;
+    auto read_frags = [&](int sl, bf16x8_t (&fa)[8], bf16x8_t (&fb)[8]) {  // (tile start)
+        const char* img = smem + sl * SLOT_BYTES + foff;
 #pragma unroll
-        for (int f = 0; f < 16; f++) {
-            const int r0 = (f < 8 ? arow + f * 16 : brow + (f - 8) * 16);
-            const int ch = (r0 >> 3) + (pp >> 1);
-            toff[f] = (f < 8 ? 0 : IMG_BYTES) + k0 * 512 + ((ch ^ mn_swz(k0)) << 4) + (pp & 1) * 8;
-        }
-    }
-    auto frag = [&](const char* slot, int f) -> bf16x8_t {  // fragment f (A 0..7, B 8..15) of a slot
-        if constexpr (KC) {
-            return *reinterpret_cast<const bf16x8_t*>(slot + foff + (f < 8 ? (arow + f * 16) * 64
-                                                                           : IMG_BYTES + (brow + (f - 8) * 16) * 64));
-        } else {
-            const char* a0 = slot + toff[f];
-            const bf16x4_t lo = ds_read_tr16_asm<0>(a0);
-            const bf16x4_t hi = ds_read_tr16_asm<4 * 512>(a0);
-            return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-        }
-    };
-    auto read_frags = [&](int sl, bf16x8_t (&fa)[8], bf16x8_t (&fb)[8]) {  // (item start)
-        const char* slot = smem + sl * SLOT_BYTES;
+        for (int a = 0; a < 8; a++) fa[a] = *reinterpret_cast<const bf16x8_t*>(img + (arow + a * 16) * 64);
 #pragma unroll
-        for (int a = 0; a < 8; a++) fa[a] = frag(slot, a);
-#pragma unroll
-        for (int b = 0; b < 8; b++) fb[b] = frag(slot, 8 + b);
-        if constexpr (!KC) {  // asm reads: retired here (the compiler does not count them)
-            __builtin_amdgcn_s_waitcnt(0xC07F);
-            __builtin_amdgcn_sched_barrier(0);
-        }
+        for (int b = 0; b < 8; b++) fb[b] = *reinterpret_cast<const bf16x8_t*>(img + IMG_BYTES + (brow + b * 16) * 64);
     };
     // lgkmcnt(0) through the builtin (encoding: vmcnt / expcnt at their maxima, lgkmcnt 0), so that
     // the compiler's own wait tracking sees the fragments land here and adds no wait of its own in
@@ -208,8 +151,6 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_w4(GemmParams p) {
         if constexpr (!LAST) {
             if (j == 0 || kt >= LEAD - 1) wait_vm(8 * (LEAD - 2));
         }
-        const int nk = cur.nk;
-        (void)nk;
         bar();
 #ifndef VIT_W4_DIAG
 #define VIT_W4_DIAG 0  // diagnostic builds (timing only, wrong results): 1 no DMA in the loop, 2 no fragment reads
@@ -223,50 +164,21 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_w4(GemmParams p) {
 #ifndef VIT_W4_SCHED
 #define VIT_W4_SCHED 1
 #endif
-        const char* nslot = smem + (sl + 1 == NS ? 0 : sl + 1) * SLOT_BYTES;
+        const char* img = smem + ((sl + 1) & (NS - 1)) * SLOT_BYTES + foff;
         auto read_pair = [&](int r) {  // fragment reads 2r, 2r + 1 of the next step (A 0..7, B 0..7)
             if constexpr (!LAST && !(VIT_W4_DIAG & 2)) {
 #pragma unroll
                 for (int u = 0; u < 2; u++) {
                     const int f = 2 * r + u;
-                    if (f < 8) ga[f] = frag(nslot, f);
-                    else gb[f - 8] = frag(nslot, f);
+                    if (f < 8) ga[f] = *reinterpret_cast<const bf16x8_t*>(img + (arow + f * 16) * 64);
+                    else gb[f - 8] = *reinterpret_cast<const bf16x8_t*>(img + IMG_BYTES + (brow + (f - 8) * 16) * 64);
                 }
             }
         };
         auto dma = [&](int q) {
             if constexpr (!(VIT_W4_DIAG & 1)) issue(kt + LEAD, sl, q);
         };
-        auto mfma_row = [&](int a) {
-#pragma unroll
-            for (int b = 0; b < 8; b++)
-                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[b], fa[a], acc[a][b], 0, 0, 0);
-        };
-        if constexpr (!KC) {
-            // asm fragment reads are not classified by the scheduling groups: the source order puts
-            // each chunk's DMA piece and its four transposed reads (two fragments) in front of the
-            // chunk's 8 MFMAs; the groups spread the MFMAs, the step's scalar work and the pieces
-#pragma unroll
-            for (int r = 0; r < 8; r++) {
-                dma(r);
-                read_pair(r);
-            }
-#pragma unroll
-            for (int a = 0; a < 8; a++) mfma_row(a);
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x4, 7, 0);
-            }
-            __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
-#pragma unroll
-            for (int r = 1; r < 8; r++) {
-                __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
-                __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
-            }
-        } else if constexpr (VIT_W4_SCHED == 1) {
+        if constexpr (VIT_W4_SCHED == 1) {
             // DMA piece q, then fragment reads 2q, 2q + 1, in source order, so the compiler (which
             // keeps LDS reads and LDS-DMA writes in program order: it cannot tell slot sl from sl+1)
             // may spread both over the step: per 8 MFMAs one piece and two reads.  Every wave then
@@ -276,12 +188,22 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_w4(GemmParams p) {
                 dma(r);
                 read_pair(r);
             }
+        } else {
 #pragma unroll
-            for (int a = 0; a < 8; a++) mfma_row(a);
-            // interleave (LLVM SchedGroupMask: MFMA 0x8, VMEM_READ 0x20, DS_READ 0x100)
+            for (int r = 0; r < 8; r++) read_pair(r);
+#pragma unroll
+            for (int q = 0; q < 8; q++) dma(q);
+        }
+#pragma unroll
+        for (int a = 0; a < 8; a++)
+#pragma unroll
+            for (int b = 0; b < 8; b++)
+                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[b], fa[a], acc[a][b], 0, 0, 0);
+        // interleave (LLVM SchedGroupMask: MFMA 0x8, VMEM_READ 0x20, DS_READ 0x100)
+        if constexpr (VIT_W4_SCHED == 1) {
             // MFMAs first after the barrier, the step's scalar address work (SALU 0x4) spread over the
-            // first four gaps instead of a clump in front of the first MFMA, then one non-MFMA issue
-            // per gap: DMA, MFMA x2, read, MFMA x2, read, MFMA x2
+            // first four gaps instead of a clump in front of the first MFMA (28 SALU there measured),
+            // then one non-MFMA issue per gap: DMA, MFMA x2, read, MFMA x2, read, MFMA x2
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
@@ -304,12 +226,6 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_w4(GemmParams p) {
             }
         } else {  // the 16 reads between the first 32 MFMAs, the 8 pieces between the other 32
 #pragma unroll
-            for (int r = 0; r < 8; r++) read_pair(r);
-#pragma unroll
-            for (int q = 0; q < 8; q++) dma(q);
-#pragma unroll
-            for (int a = 0; a < 8; a++) mfma_row(a);
-#pragma unroll
             for (int r = 0; r < 8; r++) {
                 if constexpr (!LAST) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
                 __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
@@ -321,7 +237,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_w4(GemmParams p) {
             }
         }
         __builtin_amdgcn_sched_barrier(0);
-        sl = sl + 1 == NS ? 0 : sl + 1;
+        sl = (sl + 1) & (NS - 1);
     };
     using T_ = std::integral_constant<bool, true>;
     using F_ = std::integral_constant<bool, false>;
@@ -338,7 +254,6 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_w4(GemmParams p) {
         const bool more = j + 1 < my_tiles;
         if (p.trace && tid == 0) p.trace[(long long)cur.t * TRACE_WORDS] = __builtin_amdgcn_s_memrealtime();
         read_frags(sl, fa0, fb0);
-        const int nk = cur.nk;  // even, >= LEAD
         for (int kt = 0; kt < nk - 2; kt += 2) {
             step(F_{}, kt, j, fa0, fb0, fa1, fb1);
             step(F_{}, kt + 1, j, fa1, fb1, fa0, fb0);
@@ -356,7 +271,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_w4(GemmParams p) {
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         if (!skip_epilogue(p, acc)) {
-            float* st = reinterpret_cast<float*>(smem + (KC ? NS * SLOT_BYTES : 0) + wave * STG_BYTES);
+            float* st = reinterpret_cast<float*>(smem + NS * SLOT_BYTES + wave * STG_BYTES);
             const int i = lane & 15, g = lane >> 4;
             // the staging writes take the accumulators straight from their AGPRs (inline asm with an
             // "a" operand): written as C++ stores, the register allocator copied the finished
@@ -377,14 +292,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_w4(GemmParams p) {
                                          : "memory");
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 };
-                if constexpr (EPI == EPI_F32_SLAB) {  // split-K partial plane `split`: a plain fp32 store
-                    GemmParams ps = p;
-                    ps.C = (float*)p.C + (long long)cur.split * p.M * p.ldc;
-                    ps.bias = nullptr;
-                    staged_epilogue_q_any<EPI_F32_STORE, false>(ps, stage_pass, st, lane, m0, n0 + h * 64, bpre0);
-                } else {
-                    staged_epilogue_q_any<EPI, false>(p, stage_pass, st, lane, m0, n0 + h * 64, h ? bpre1 : bpre0);
-                }
+                staged_epilogue_q_any<EPI, false>(p, stage_pass, st, lane, m0, n0 + h * 64, h ? bpre1 : bpre0);
             }
         }
         if (p.trace && (tid & 63) == 0) {
@@ -408,14 +316,14 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_w4(GemmParams p) {
 // variant 9 launcher (gemm.hip launch_g2): K-contiguous A and B, no split-K, K % 64 == 0,
 // K >= 128, 32-bit DMA offsets; false = not taken (the caller falls back)
 bool gemm_bf16_w4(const GemmArgs& a, const GemmParams& p, int tiles, hipStream_t s) {
-    if (!(a.a_kcontig && a.b_kcontig) || a.K % 64 || a.K < 4 * g5::BK || p.kchunk != a.K ||
+    if (!(a.a_kcontig && a.b_kcontig) || a.K % 64 || a.K < 4 * g5::BK ||
         (long long)p.M * p.lda * 2 >= (1LL << 31) || (long long)p.N * p.ldb * 2 >= (1LL << 31))
         return false;
     const int cus = gemm_cu_count();
     const dim3 pg(tiles < cus ? tiles : cus);
     switch (a.epi) {
 #define VIT_CASE(E) \
-    case E: g5::gemm_kernel_w4<true, E><<<pg, g5::NT, 0, s>>>(p); return true;
+    case E: g5::gemm_kernel_w4<E><<<pg, g5::NT, 0, s>>>(p); return true;
         VIT_CASE(EPI_F32_STORE)
         VIT_CASE(EPI_F32_ACC)
         VIT_CASE(EPI_BF16_STORE)
@@ -427,39 +335,6 @@ bool gemm_bf16_w4(const GemmArgs& a, const GemmParams& p, int tiles, hipStream_t
 #undef VIT_CASE
         default: return false;
     }
-}
-
-// variant 9 weight gradients (gemm.hip gemm_bf16): EPI_F32_ATOMIC with M/N-contiguous A and B,
-// K split into >= 128-deep chunks (one work item per tile and split, one workgroup per CU), fp32
-// partial planes + the fixed-order slab reduce, the fused bias gradient as in the 256x128 engine.  false = shape not taken (the caller falls back).
-bool gemm_bf16_w4_wgrad(const GemmArgs& a, hipStream_t s) {
-    if (a.epi != EPI_F32_ATOMIC || a.a_kcontig || a.b_kcontig || a.K % 64 || a.M < 256 || a.N < 256 ||
-        a.M % 8 || a.N % 8)
-        return false;
-    const int tiles = cdiv(a.M, g5::BM) * cdiv(a.N, g5::BN);
-    int split = a.splitk > 0 ? a.splitk : choose_split_waves(tiles, a.K / 64);
-    const int kchunk = cdiv(cdiv(a.K, split), 64) * 64;
-    split = cdiv(a.K, kchunk);
-    // every item >= LEAD (5) steps, an even count; 32-bit lane offsets (k < 32 rows of the image + columns).  Split-K
-    // only (slab planes): the single-split in-place form (EPI_F32_ACC) spills, and a spilled or
-    // copied fragment register of the asm transposed reads would be taken before its data landed
-    if (split < 2 || kchunk < 6 * g5::BK || a.K - (split - 1) * kchunk < 6 * g5::BK) return false;
-    if (32LL * a.lda * 2 + 2LL * a.M >= (1LL << 31) || 32LL * a.ldb * 2 + 2LL * a.N >= (1LL << 31)) return false;
-    if (split > 1 && a.ws && (size_t)split * a.M * a.N * sizeof(float) > a.ws_bytes) return false;
-    GemmArgs b = a;
-    float* slab = slab_buffer(a, split);
-    if (!slab) return true;  // (error set)
-    b.epi = EPI_F32_SLAB;
-    b.C = slab;
-    b.ldc = a.N;
-    GemmParams p = make_gemm_params(b, kchunk);
-    p.tiles = tiles;
-    g5::gemm_kernel_w4<false, EPI_F32_SLAB><<<dim3(tiles * split), g5::NT, 0, s>>>(p);
-    after_launch("gemm_bf16_w4_wgrad");
-    count_hit(VIT_HIT_GEMM_256x256 + b.epi);
-    slab_reduce(a, slab, split, s);
-    if (a.dbias) colsum_bf16(a.dbias, (const bf16_t*)a.A, a.K, a.M, a.lda, s);
-    return true;
 }
 
 }  // namespace vit
