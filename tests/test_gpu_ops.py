@@ -356,12 +356,12 @@ def test_error_channel(gpu):
 
 
 # ------------------------------------------------------------------ generic bf16 GEMM engine
-@pytest.fixture(params=[2, 4, 5, 7, 9])
+@pytest.fixture(params=[2, 4, 5, 7, 9, 10])
 def engine(request, gpu):
     """Run a test under each production GEMM engine (2 = 256x256 one workgroup per CU, with the split-K
     weight gradients on 256x128; 4 = 256x128 two per CU everywhere; 5 = as 4 with the
     software-pipelined main loop for K-contiguous operands; 7 = persistent streaming 256x256, 9 = its
-    one-wave-per-SIMD 128x128-per-wave form), then restore the default."""
+    one-wave-per-SIMD 128x128-per-wave form, 10 = 7 with the split tail round), then restore the default."""
     gpu.lib().gemm_bf16_set_variant(request.param)
     yield request.param
     gpu.lib().gemm_bf16_set_variant(0)
@@ -439,6 +439,46 @@ def test_gemm_bf16_pipelined_bit_identical(gpu, M, N, K, pair):
         for x, y in zip(outs[v0][epi], outs[v1][epi]):
             assert np.array_equal(x, y), epi
     assert np.abs(outs[v1][5][0]).max() > 0
+
+
+@pytest.mark.parametrize("M,N,K", [(50432, 768, 768), (50432, 768, 3072), (25216, 768, 3072), (25216, 768, 2304),
+                                   (2056, 768, 320), (1000, 520, 128)])
+def test_gemm_bf16_tail_split(gpu, M, N, K):
+    """Variant 10: the persistent engine with the last, partly filled round's tiles split along K
+    (fp32 partial tiles + gemm_tail_fix_k) against variant 7 on the same inputs, at the trainer's
+    N = 768 shapes (591 / 297 tiles: a tail of 79 / 41 tiles on 256 CUs) and ragged ones: the bias,
+    fp32-residual and bf16-store epilogues agree to fp32 summation order (the bf16 store to one bf16
+    ulp), the full-round tiles bit for bit, and two launches are bitwise equal (fixed part order)."""
+    v = gpu
+    L = v.lib()
+    rng = np.random.default_rng(M + 5 * N + K)
+    ab = v.bf16_bits(rng.uniform(-1, 1, size=(M, K)).astype(np.float32))
+    wb = v.bf16_bits((rng.uniform(-1, 1, size=(N, K)) * 0.1).astype(np.float32))
+    A, W = D(v, ab, np.uint16), D(v, wb, np.uint16)
+    bias = D(v, rng.normal(size=N).astype(np.float32))
+    res = D(v, rng.normal(size=(M, N)).astype(np.float32))
+    outs = {}
+    try:
+        for var in (7, 10, 10):
+            L.gemm_bf16_set_variant(var)
+            o = []
+            for epi in (0, 3, 5):
+                c = Z(v, M * N, np.uint16 if epi == 3 else np.float32)
+                v.call("gemm_bf16_fused", c, None, N, res if epi == 5 else None, N, A, K, 1, W, K, 1, bias,
+                       None, M, N, K, epi)
+                o.append(c.numpy())
+            outs.setdefault(var, []).append(o)
+    finally:
+        L.gemm_bf16_set_variant(0)
+    ref, got, again = outs[7][0], outs[10][0], outs[10][1]
+    for e, (x, y, z) in enumerate(zip(ref, got, again)):
+        assert np.array_equal(y, z), e
+        if x.dtype == np.uint16:
+            xf, yf = v.bf16_to_f32(x), v.bf16_to_f32(y)
+            assert np.abs(xf - yf).max() <= 2 ** -7 * np.abs(xf).max(), e
+        else:
+            assert np.abs(x - y).max() <= 1e-5 * np.abs(x).max(), e
+    assert np.abs(ref[2]).max() > 0
 
 
 def _gelu64(x):

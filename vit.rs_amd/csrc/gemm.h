@@ -77,7 +77,11 @@ struct GemmArgs {
     // mxc_off % 64 == 0.  Bit-identical to quantize_mx_cols_bf16 of the bf16 output.  With
     // mx_q / mxc_q set, the MX-copied bf16 output (C2 of GELU / GELU_D, C of DGELU / MUL) may be
     // nullptr: not stored.
-    uint8_t* mxc_q = nullptr;
+// variant 10 (split tail of the persistent engine): fp32 partial tiles of the last round, one buffer
+    // per concurrent stream (nullptr = the thread workspace); up to 64 MiB at 256 CUs
+    float* tail_ws = nullptr;
+    size_t tail_ws_bytes = 0;
+        uint8_t* mxc_q = nullptr;
     uint8_t* mxc_s = nullptr;
     long long mxc_ld = 0;
     long long mxc_off = 0;
@@ -97,6 +101,7 @@ void gemm_set_variant(int v);
 void gemm_set_debug(int flags);
 // compute units of the current device: the persistent engines' grid (one workgroup per CU)
 int gemm_cu_count();
+int gemm_variant_selected();  // the engine variant in effect (VIT_GEMM / gemm_set_variant)
 struct GemmParams;
 // variant 9: the one-wave-per-SIMD persistent engine (gemm_w4.hip) for K-contiguous operands without
 // split-K (K % 64 == 0, K >= 128); false = shape not taken

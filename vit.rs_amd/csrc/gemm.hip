@@ -14,6 +14,7 @@
 //   bounds-checked scalar staging; the fp32 parity path.
 #include "gemm_common.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace vit {
@@ -460,7 +461,11 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel(GemmParams p) {
 // 1 (so the epilogue's own loads and stores are never waited for by a wait meant for a DMA piece,
 // except in phase 1 of the next tile's second step, when those have long completed).  Same MFMA
 // order per accumulator and the same epilogue arithmetic as gemm_kernel: bit-identical outputs.
-template <int EPI>
+// TS (variant 10): the tiles of the full rounds (p.tfull) as above, then the last round's tiles split
+// into p.tsplit K-ranges of p.kchunk (work items tfull + u * tsplit + part, part-major per tile), each
+// storing its raw fp32 accumulators as a 256x256 partial tile (tpart); gemm_tail_fix_k adds the parts
+// in order and applies the epilogue.  The tail round then keeps every CU busy instead of 1/3 of them.
+template <int EPI, bool TS = false>
 __global__ __launch_bounds__(NT, 1) void gemm_kernel_s(GemmParams p) {
     constexpr int NS = 4;  // DMA two steps ahead
     __shared__ __attribute__((aligned(1024))) char smem[NS * SLOT_BYTES];
@@ -470,8 +475,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_s(GemmParams p) {
     const int wm = wave >> 2, wn = wave & 3;
     const int ntm = cdiv(p.M, BM), ntn = cdiv(p.N, BN), tiles = ntm * ntn;
     const int nblk = gridDim.x;
-    const int my_tiles = (tiles - (int)blockIdx.x + nblk - 1) / nblk;
-    const int nk = p.K / BK;
+    const int items = TS ? p.tfull + (tiles - p.tfull) * p.tsplit : tiles;
+    const int my_tiles = (items - (int)blockIdx.x + nblk - 1) / nblk;
+    const int nk_all = p.K / BK;
     const char* A = (const char*)p.A;
     const char* B = (const char*)p.B;
     f32x4_t acc[8][4];
@@ -487,11 +493,23 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_s(GemmParams p) {
     // the lane's DMA source of piece j of the A / B image of a tile, as a 32-bit byte offset from
     // the operand base at k = 0 (K-contiguous image: as stage<true>; host: M*lda, N*ldb < 2^31)
     struct TileSrc {
-        int tm0, tn0, t;
+        int tm0, tn0, t, kbeg, nk, part;  // part: index of the partial tile (TS tail items), else -1
         uint32_t a[2], b[2];
     };
     auto tile_src = [&](int j, TileSrc& ts) {
-        ts.t = xcd_remap(j * nblk + (int)blockIdx.x, tiles);
+        const int it = j * nblk + (int)blockIdx.x;
+        ts.kbeg = 0;
+        ts.nk = nk_all;
+        ts.part = -1;
+        if (!TS || it < p.tfull) {
+            ts.t = xcd_remap(it, TS ? p.tfull : tiles);
+        } else {
+            const int v = it - p.tfull, u = v / p.tsplit;
+            ts.t = p.tfull + u;
+            ts.part = v;
+            ts.kbeg = (v - u * p.tsplit) * p.kchunk;
+            ts.nk = (min(p.K, ts.kbeg + p.kchunk) - ts.kbeg) / BK;  // host: >= 2 steps
+        }
         ts.tm0 = (ts.t / ntn) * BM;
         ts.tn0 = (ts.t % ntn) * BN;
 #pragma unroll
@@ -513,17 +531,19 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_s(GemmParams p) {
     // A / B pieces of step kt2 of the current tile (kt2 >= nk: step kt2 - nk of the next one, if
     // this workgroup has one) into slot sl
     auto issue_a = [&](int kt2, int sl, bool more) {
+        const int nk = cur.nk;
         if (kt2 >= nk && !more) return;
         const bool c = kt2 < nk;
-        const char* base = A + (long long)(c ? kt2 : kt2 - nk) * (BK * 2);
+        const char* base = A + (long long)(c ? cur.kbeg / BK + kt2 : nxt.kbeg / BK + kt2 - nk) * (BK * 2);
         char* dst = smem + sl * SLOT_BYTES;
 #pragma unroll
         for (int q = 0; q < 2; q++) glds(base + (c ? cur.a[q] : nxt.a[q]), dst + (q * 8 + wave) * 1024);
     };
     auto issue_b = [&](int kt2, int sl, bool more) {
+        const int nk = cur.nk;
         if (kt2 >= nk && !more) return;
         const bool c = kt2 < nk;
-        const char* base = B + (long long)(c ? kt2 : kt2 - nk) * (BK * 2);
+        const char* base = B + (long long)(c ? cur.kbeg / BK + kt2 : nxt.kbeg / BK + kt2 - nk) * (BK * 2);
         char* dst = smem + sl * SLOT_BYTES + IMG_BYTES;
 #pragma unroll
         for (int q = 0; q < 2; q++) glds(base + (c ? cur.b[q] : nxt.b[q]), dst + (q * 8 + wave) * 1024);
@@ -558,6 +578,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_s(GemmParams p) {
     bf16x8_t fb[4], alo[4], ahi[4];
     for (int j = 0; j < my_tiles; j++) {
         const bool more = j + 1 < my_tiles;
+        const int nk = cur.nk;
         if (p.trace && tid == 0) p.trace[(long long)cur.t * TRACE_WORDS] = __builtin_amdgcn_s_memrealtime();
         bar();
         if (lagging) {
@@ -604,8 +625,19 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_s(GemmParams p) {
         if (!skip_epilogue(p, acc)) {
             // this tile's last two steps were in slots sl - 1, sl - 2 (mod 4)
             char* stg = smem + ((wave < 4 ? sl + 2 : sl + 3) & 3) * SLOT_BYTES + (wave & 3) * 8192;
-            staged_epilogue_q<EPI>(p, acc, reinterpret_cast<float*>(stg), lane, cur.tm0 + wm * 128,
-                                   cur.tn0 + wn * 64, bpre);
+            if (TS && cur.part >= 0) {
+                // raw accumulators into the partial tile in accumulator order (a wave's 32 x 16-B
+                // stores cover whole 1 KiB blocks; no staging, no epilogue registers):
+                // float4 (wave, a, b, lane) at ((wave * 32 + a * 4 + b) * 64 + lane) * 4
+                float* dst = p.tpart + (long long)cur.part * (BM * BN) + wave * 32 * 256 + lane * 4;
+#pragma unroll
+                for (int a = 0; a < 8; a++)
+#pragma unroll
+                    for (int b = 0; b < 4; b++) *reinterpret_cast<f32x4_t*>(dst + (a * 4 + b) * 256) = acc[a][b];
+            } else {
+                staged_epilogue_q<EPI>(p, acc, reinterpret_cast<float*>(stg), lane, cur.tm0 + wm * 128,
+                                       cur.tn0 + wn * 64, bpre);
+            }
         }
         if (p.trace && (tid & 63) == 0) {
             const long long rec = (long long)cur.t * TRACE_WORDS;
@@ -621,6 +653,41 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_s(GemmParams p) {
         // recomputed rather than carried: nothing of the next tiles' sources stays live through the epilogue
         if (more) tile_src(j + 1, cur);
         if (j + 2 < my_tiles) tile_src(j + 2, nxt);
+    }
+}
+
+// finish of the split tail (variant 10): tile tfull + u = the sum of its tsplit partial tiles in
+// part order, then the GEMM's epilogue (bias, fp32 residual or bf16 store) as epilogue8 applies it.
+// Block (u, rc): rows 32 rc .. 32 rc + 31 of the tile, thread = (row, 8-column group).
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_tail_fix_k(GemmParams p) {
+    const int ntn = cdiv(p.N, BN), u = blockIdx.x, t = p.tfull + u;
+    const int tm0 = (t / ntn) * BM, tn0 = (t % ntn) * BN;
+    const int cg = threadIdx.x & 31, r0 = blockIdx.y * 32 + (threadIdx.x >> 5);
+    float cs[8];
+#pragma unroll
+    for (int it = 0; it < 4; it++) {
+        const int r = r0 + it * 8;
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        // (r, 8 cg ..) in the accumulator order of gemm_kernel_s: wave (r / 128) * 4 + c / 64, tile
+        // a = (r % 128) / 16, b = (c % 64) / 16, lane 16 g + r % 16 with g = (c % 16) / 4
+        const int c = cg * 8, wv = (r >> 7) * 4 + (c >> 6), a = (r & 127) >> 4, b = (c & 63) >> 4;
+        const int g = (c & 15) >> 2, i = r & 15;
+        const long long o0 = ((long long)(wv * 32 + a * 4 + b) * 64 + g * 16 + i) * 4, o1 = o0 + 16 * 4;
+        for (int part = 0; part < p.tsplit; part++) {
+            const float* q = p.tpart + ((long long)u * p.tsplit + part) * (BM * BN);
+            const float4 x0 = *reinterpret_cast<const float4*>(q + o0), x1 = *reinterpret_cast<const float4*>(q + o1);
+            v[0] += x0.x; v[1] += x0.y; v[2] += x0.z; v[3] += x0.w;
+            v[4] += x1.x; v[5] += x1.y; v[6] += x1.z; v[7] += x1.w;
+        }
+        const int m = tm0 + r, n = tn0 + cg * 8;
+        if (m >= p.M) continue;
+        if (n + 8 <= p.N) {
+            epilogue8<EPI, false>(p, m, n, v, cs);
+        } else if (n + 4 <= p.N) {
+            f32x4_t w = {v[0], v[1], v[2], v[3]};
+            epilogue<EPI>(p, m, n, w);
+        }
     }
 }
 
@@ -1196,7 +1263,7 @@ __global__ __launch_bounds__(256) void slab_reduce_k(float* __restrict__ C, long
 //   epilogues (main-loop-only timing; results are garbage).
 static int g_variant = -1;
 static int g_debug_flags = 0;
-static bool known_variant(int v) { return v == 1 || v == 2 || v == 4 || v == 5 || v == 7 || v == 9; }
+static bool known_variant(int v) { return v == 1 || v == 2 || v == 4 || v == 5 || v == 7 || v == 9 || v == 10; }
 static constexpr int kDefaultVariant = 7;
 static int gemm_variant() {
     if (g_variant < 0) {
@@ -1218,7 +1285,8 @@ int gemm_cu_count() {
     }();
     return n;
 }
-bool gemm_streaming() { return gemm_variant() == 7 || gemm_variant() == 9; }
+int gemm_variant_selected() { return gemm_variant(); }
+bool gemm_streaming() { return gemm_variant() == 7 || gemm_variant() == 9 || gemm_variant() == 10; }
 void gemm_set_debug(int flags) { g_debug_flags = flags; }
 static unsigned long long* g_trace = nullptr;
 void gemm_set_trace(unsigned long long* trace) { g_trace = trace; }
@@ -1240,6 +1308,9 @@ GemmParams make_gemm_params(const GemmArgs& a, int kchunk) {
     p.mxc_off = (int)a.mxc_off;
     p.mxc_rg = (int)(mx_rows_padded(a.N) / 32);
     p.tiles = 1;
+    p.tsplit = 0;
+    p.tfull = 0;
+    p.tpart = nullptr;
     return p;
 }
 
@@ -1356,9 +1427,46 @@ static void launch_g2(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStre
     if constexpr (AK && BKC) {
         // one-wave-per-SIMD persistent engine (gemm_w4.hip)
         if (gemm_variant() == 9 && grid.y == 1 && gemm_bf16_w4(a, p, (int)grid.x, s)) return;
+        // persistent streaming engine with a split tail (variant 10): when the last round fills at
+        // most half the CUs, its tiles run as K-ranges on all of them (bias / residual / bf16 store
+        // epilogues; fp32 partial tiles in a.tail_ws or the thread workspace + gemm_tail_fix_k)
+        if (gemm_variant() == 10 && grid.y == 1 && p.K >= 2 * g2::BK && p.kchunk == p.K &&
+            (a.epi == EPI_F32_STORE || a.epi == EPI_BF16_STORE || a.epi == EPI_F32_RESID) &&
+            (long long)p.M * p.lda * 2 < (1LL << 31) && (long long)p.N * p.ldb * 2 < (1LL << 31)) {
+            const int cus = gemm_cu_count(), tiles = (int)grid.x;
+            const int nblk = tiles < cus ? tiles : cus, full = tiles / nblk * nblk, tail = tiles - full;
+            const int nk = p.K / g2::BK;
+            int split = tail > 0 && full > 0 ? std::min(nblk / tail, nk / 2) : 1;
+            if (split >= 2) {
+                const int kchunk = cdiv(cdiv(p.K, split), 2 * g2::BK) * (2 * g2::BK);  // even step count
+                split = cdiv(p.K, kchunk);
+                const size_t need = (size_t)tail * split * g2::BM * g2::BN * sizeof(float);
+                float* part = a.tail_ws ? (a.tail_ws_bytes >= need ? a.tail_ws : nullptr) : (float*)workspace(need);
+                if (split >= 2 && part) {
+                    GemmParams q = p;
+                    q.tsplit = split;
+                    q.tfull = full;
+                    q.kchunk = kchunk;
+                    q.tpart = part;
+                    switch (a.epi) {
+#define VIT_CASE(E)                                                                   \
+    case E:                                                                           \
+        g2::gemm_kernel_s<E, true><<<nblk, g2::NT, 0, s>>>(q);                         \
+        g2::gemm_tail_fix_k<E><<<dim3(tail, g2::BM / 32), 256, 0, s>>>(q);            \
+        return;
+                        VIT_CASE(EPI_F32_STORE)
+                        VIT_CASE(EPI_BF16_STORE)
+                        VIT_CASE(EPI_F32_RESID)
+#undef VIT_CASE
+                        default: break;
+                    }
+                }
+            }
+        }
         // persistent streaming engine: one workgroup per CU (at most one per tile), no split-K;
         // its DMA ring runs two K-steps ahead across one tile boundary, so K >= 2 steps
-        if (gemm_variant() == 7 && grid.y == 1 && p.K >= 2 * g2::BK && (long long)p.M * p.lda * 2 < (1LL << 31) &&
+        if ((gemm_variant() == 7 || gemm_variant() == 10) && grid.y == 1 && p.K >= 2 * g2::BK &&
+            (long long)p.M * p.lda * 2 < (1LL << 31) &&
             (long long)p.N * p.ldb * 2 < (1LL << 31)) {
             const int cus = gemm_cu_count();
             const dim3 pg((int)grid.x < cus ? grid.x : cus);
@@ -1510,7 +1618,7 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s) {
     // split-K weight gradients (M/N-contiguous operands, K = the token count) run on the 256x128
     // two-per-CU engine: 3-9 % faster than 256x256 on every ViT-B/16 wgrad shape (r02,
     // tools/bench_gemm.py), the other GEMMs are faster on 256x256
-    if ((gemm_variant() == 2 || gemm_variant() == 7 || gemm_variant() == 9) && a.epi == EPI_F32_ATOMIC && !a.a_kcontig && !a.b_kcontig &&
+    if ((gemm_variant() == 2 || gemm_variant() == 7 || gemm_variant() == 9 || gemm_variant() == 10) && a.epi == EPI_F32_ATOMIC && !a.a_kcontig && !a.b_kcontig &&
         a.K % g4::KTILE == 0 && a.M >= 256 && a.N >= 128 && a.N % 4 == 0 &&
         (a.splitk > 0 || !a.ws ||
          (size_t)choose_split_g4(cdiv(a.M, g4::BM) * cdiv(a.N, g4::BN), a.K / g4::KTILE) * a.M * a.N * sizeof(float) <=

@@ -28,6 +28,11 @@ struct GemmParams {
     uint8_t* mxc_s;
     long long mxc_ld;
     int mxc_off, mxc_rg;
+    // persistent engine with a split tail (variant 10): the last, partly filled round's tiles run as
+    // tsplit K-ranges of kchunk each into fp32 partial tiles tpart[tile][part][256][256]; tfull = the
+    // tiles of the full rounds (gemm_tail_fix_k finishes the tail tiles)
+    int tsplit, tfull;
+    float* tpart;
 };
 
 // E8M0 scale byte of an MX block: X + 127 with X = ceil(log2(amax / 448)) (no element overflows

@@ -256,6 +256,10 @@ struct Trainer {
     float* params = nullptr;
     float* grads = nullptr;
     float* gemm_ws = nullptr;     // split-K slabs of the wgrad GEMMs (stream-ordered on s)
+    // GEMM variant 10 (split tail round): fp32 partial tiles, one buffer per concurrent stream
+    // (ms[0..MAXMB-1], s2): 256 x 256 KiB at most per GEMM (gemm.hip launch_g2)
+    float* tail_buf[MAXMB + 1]{};
+    size_t tail_bytes = 0;
     float* attn_part = nullptr;   // per-(b,h) qkv-bias partial sums of the attention backward
     size_t gemm_ws_bytes = 0;
     bf16_t* pbf = nullptr;
@@ -496,8 +500,19 @@ struct Trainer {
         ev_used = 0;
     }
 
+    // the stream's own partial-tile buffer for GEMM variant 10 (never the shared thread workspace:
+    // the micro-batch streams run GEMMs concurrently)
+    void set_tail(GemmArgs& a, hipStream_t st) {
+        if (a.tail_ws || !tail_bytes) return;
+        int k = MAXMB;  // s2
+        for (int i = 0; i < MAXMB; i++)
+            if (st == ms[i]) k = i;
+        a.tail_ws = tail_buf[k];
+        a.tail_ws_bytes = tail_bytes;
+    }
     void gemm(int cls, GemmArgs a, bool bf, hipStream_t st = nullptr) {
         if (!st) st = s;
+        if (bf) set_tail(a, st);
         tbeg(cls, 2.0 * a.M * (double)a.N * a.K, st);
         if (bf) gemm_bf16(a, st); else gemm_f32(a, st);
         tend();
@@ -595,6 +610,10 @@ struct Trainer {
         if (!lowp()) {  // the fp32 engine's split-K slabs (<= ~16 MB: splits x tiles <= 1024 tiles of 64 x 64)
             gemm_ws_bytes = (size_t)32 << 20;
             gemm_ws = alloc<float>((long long)(gemm_ws_bytes / sizeof(float)));
+        }
+        if (lowp() && gemm_variant_selected() == 10) {  // (A/B runs only: VIT_GEMM=10 at build time)
+            tail_bytes = (size_t)gemm_cu_count() * 256 * 256 * sizeof(float);
+            for (int k = 0; k <= MAXMB; k++) tail_buf[k] = alloc<float>((long long)(tail_bytes / sizeof(float)));
         }
         if (lowp()) {
             if (!(attn_fused_supported(T, C, NH) || attn_generic_supported(T, C, NH)) || C % 8) {
@@ -952,11 +971,13 @@ struct Trainer {
                 im2col_pad_bf16(patches_bf + img0 * NP * KPP, pixels + img0 * 3 * cfg.img * cfg.img, Bm, cfg.img,
                                 cfg.patch, KPP, st);
                 a.A = patches_bf + img0 * NP * KPP; a.lda = KPP; a.B = wpatch_pad; a.ldb = KPP; a.K = KPP;
+                set_tail(a, st);
                 gemm_bf16(a, st);
             } else {
                 im2col_bf16(patches_bf + img0 * NP * KP, pixels + img0 * 3 * cfg.img * cfg.img, Bm, cfg.img,
                             cfg.patch, st);
                 a.A = patches_bf + img0 * NP * KP; a.lda = KP; a.B = W(P_PATCH_W); a.ldb = KP;
+                set_tail(a, st);
                 gemm_bf16(a, st);
             }
             patch_assemble(encoded + img0 * T * C, emb_tmp + img0 * NP * C, P(P_CLS), P(P_WPE), Bm, NP, C, st);
