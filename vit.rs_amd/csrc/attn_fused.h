@@ -739,6 +739,9 @@ struct BwdRegs {  // per-wave state of the one-pass backward: the wave owns KK 1
 // MASK: for operands whose rows past T are copies of row T-1 (not zero), the probabilities
 // of padded queries (q >= T) and keys (key >= T) are masked to 0 (nq / nk: valid queries / keys
 // counted from the slice's and the wave's first one)
+#ifndef VIT_ATTN_AHOIST
+#define VIT_ATTN_AHOIST 0  // phase A: all reads / score MFMAs first, 1-3: transposed reads all / half / none hoisted (0: per 16-query half; 1-3 spill at ViT-B/16)
+#endif
 template <int HS, int KK = 2, bool MASK = false>
 __device__ __forceinline__ void bwd_slice_a(BwdRegs<HS, KK>& R, const bf16_t* Qc, const bf16_t* Dc, const float* lq_s,
                                             const float* dl_s, bf16_t* dSk, float c, int lane, int nq = 0,
@@ -748,6 +751,88 @@ __device__ __forceinline__ void bwd_slice_a(BwdRegs<HS, KK>& R, const bf16_t* Qc
     constexpr bool SW = sw_slice<HS>(), SWD = sw_ds<HS>();  // swizzled slice / dS^T images (sl_off / ds_off)
     const int i = lane & 15, g = lane >> 4;
     f32x4_t P[KK][2], dS[KK][2];  // [kk][u]: lane (i,g) -> [q = 16u+4g+r][key = 16kk+i]
+    bf16x8_t pb[KK], db[KK];
+    auto tr_frags = [&](int dt, bf16x8_t& td, bf16x8_t& tq) {
+        if constexpr (SW) {
+            td = frag_tr_sw(reinterpret_cast<const char*>(Dc), 0, 16 * dt, lane);
+            tq = frag_tr_sw(reinterpret_cast<const char*>(Qc), 0, 16 * dt, lane);
+        } else {
+            td = frag_tr(Dc, SK, 0, 16 * dt, lane);
+            tq = frag_tr(Qc, SK, 0, 16 * dt, lane);
+        }
+    };
+#if VIT_ATTN_AHOIST
+    // Every LDS read first (both 16-query halves' row fragments, lse / delta), then all 16 score
+    // MFMAs, then the transposed fragments of the dV / dK products, requested before the
+    // exponentials so they land under them.  Same products and sums in the same order as the
+    // per-half form below (bit-identical); it waited on each half's reads and on the transposed
+    // reads right in front of the MFMAs that consume them.
+    bf16x8_t qr[2][KS], dr[2][KS];
+    float lq[2][4], dq[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+#pragma unroll
+        for (int s = 0; s < KS; s++) {
+            if constexpr (SW) {
+                qr[u][s] = frag_row_sw(reinterpret_cast<const char*>(Qc), 16 * u, s, lane);
+                dr[u][s] = frag_row_sw(reinterpret_cast<const char*>(Dc), 16 * u, s, lane);
+            } else {
+                qr[u][s] = frag_row<HS>(Qc, SK, 16 * u, s, lane);
+                dr[u][s] = frag_row<HS>(Dc, SK, 16 * u, s, lane);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            lq[u][r] = lq_s[16 * u + 4 * g + r];
+            dq[u][r] = dl_s[16 * u + 4 * g + r];
+        }
+    }
+    f32x4_t sa[KK][2], pa[KK][2];
+#pragma unroll
+    for (int u = 0; u < 2; u++)
+#pragma unroll
+        for (int kk = 0; kk < KK; kk++) {
+            f32x4_t s_ = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < KS; s++) {
+                s_ = mfma(qr[u][s], R.kf[kk][s], s_);
+                dp = mfma(dr[u][s], R.vf[kk][s], dp);
+            }
+            sa[kk][u] = s_;
+            pa[kk][u] = dp;
+        }
+    // VIT_ATTN_AHOIST 1: all DT transposed pairs before the exponentials; 2: the first TRH of them
+    constexpr int TRH = VIT_ATTN_AHOIST == 1 ? DT : VIT_ATTN_AHOIST == 2 ? (DT + 1) / 2 : 0;
+    bf16x8_t td[DT], tq[DT];
+#pragma unroll
+    for (int dt = 0; dt < TRH; dt++) tr_frags(dt, td[dt], tq[dt]);
+#pragma unroll
+    for (int u = 0; u < 2; u++)
+#pragma unroll
+        for (int kk = 0; kk < KK; kk++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                float pv = fexp2(sa[kk][u][r] * c - lq[u][r]);
+                if constexpr (MASK) pv = (16 * u + 4 * g + r < nq && 16 * kk + i < nk) ? pv : 0.f;
+                P[kk][u][r] = pv;
+                dS[kk][u][r] = pv * (pa[kk][u][r] - dq[u][r]);
+                R.sds[kk] += dS[kk][u][r];
+            }
+#pragma unroll
+    for (int kk = 0; kk < KK; kk++) {
+        pb[kk] = pack_acc(P[kk][0], P[kk][1]);
+        db[kk] = pack_acc(dS[kk][0], dS[kk][1]);
+    }
+#pragma unroll
+    for (int dt = TRH; dt < DT; dt++) tr_frags(dt, td[dt], tq[dt]);
+#pragma unroll
+    for (int dt = 0; dt < DT; dt++)
+#pragma unroll
+        for (int kk = 0; kk < KK; kk++) {
+            R.dv[kk][dt] = mfma(td[dt], pb[kk], R.dv[kk][dt]);
+            R.dk[kk][dt] = mfma(tq[dt], db[kk], R.dk[kk][dt]);
+        }
+#else
 #pragma unroll
     for (int u = 0; u < 2; u++) {
         bf16x8_t qr[KS], dr[KS];
@@ -785,7 +870,6 @@ __device__ __forceinline__ void bwd_slice_a(BwdRegs<HS, KK>& R, const bf16_t* Qc
             }
         }
     }
-    bf16x8_t pb[KK], db[KK];
 #pragma unroll
     for (int kk = 0; kk < KK; kk++) {
         pb[kk] = pack_acc(P[kk][0], P[kk][1]);
@@ -794,19 +878,14 @@ __device__ __forceinline__ void bwd_slice_a(BwdRegs<HS, KK>& R, const bf16_t* Qc
 #pragma unroll
     for (int dt = 0; dt < DT; dt++) {
         bf16x8_t td, tq;
-        if constexpr (SW) {
-            td = frag_tr_sw(reinterpret_cast<const char*>(Dc), 0, 16 * dt, lane);
-            tq = frag_tr_sw(reinterpret_cast<const char*>(Qc), 0, 16 * dt, lane);
-        } else {
-            td = frag_tr(Dc, SK, 0, 16 * dt, lane);
-            tq = frag_tr(Qc, SK, 0, 16 * dt, lane);
-        }
+        tr_frags(dt, td, tq);
 #pragma unroll
         for (int kk = 0; kk < KK; kk++) {
             R.dv[kk][dt] = mfma(td, pb[kk], R.dv[kk][dt]);
             R.dk[kk][dt] = mfma(tq, db[kk], R.dk[kk][dt]);
         }
     }
+#endif
     // dS^T -> LDS [key][query] (bf16, the MFMA operand's values): 4 consecutive queries per lane
     // and tile.  Without MASK, padded keys carry P != 0 (their K, V rows are zero): their dS is
     // finite and multiplies the zero K rows in dQ.  dSk = the wave's first key row.
@@ -827,6 +906,9 @@ __device__ __forceinline__ void bwd_slice_a(BwdRegs<HS, KK>& R, const bf16_t* Qc
 // xk_ds / xk_k (XK): dS[q][T-1] per query of the slice and K[T-1] (fp32) of a key the kernel does not
 // own on the MFMA path (the XK side path): its rank-1 term dS[q][T-1] K[T-1] joins the dQ
 // accumulators before the store
+#ifndef VIT_ATTN_BLA
+#define VIT_ATTN_BLA 2  // phase B operand lookahead (blocks); 0: reads in front of each MFMA
+#endif
 template <int HS, int NSL, int NW, bool XK = false>
 __device__ __forceinline__ void bwd_slice_b(const bf16_t* Ks, const bf16_t* dSs, bf16_t* dq, long long C3, int q0,
                                             int T, float scale, int w, int lane, const float* xk_ds = nullptr,
@@ -840,15 +922,39 @@ __device__ __forceinline__ void bwd_slice_b(const bf16_t* Ks, const bf16_t* dSs,
         const int dt = jj >> 1, u = jj & 1;
         // two accumulation chains (even / odd key blocks) halve the dependent-MFMA latency
         f32x4_t acc = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+        auto fa = [&](int ks) { return frag_tr(Ks, SV, 32 * ks, 16 * dt, lane); };
+        auto fb = [&](int ks) {
+            if constexpr (SW) return frag_tr_ds(reinterpret_cast<const char*>(dSs), 32 * ks, 16 * u, lane);
+            else return frag_tr(dSs, BWD_SDS, 32 * ks, 16 * u, lane);
+        };
+#if VIT_ATTN_BLA
+        // operands of block ks + BLA requested before block ks's MFMA (the unpipelined form waited for
+        // each block's four reads right in front of its MFMA: an LDS round trip per MFMA)
+        constexpr int LA = VIT_ATTN_BLA < NSL ? VIT_ATTN_BLA : NSL;
+        bf16x8_t ra[LA], rb[LA];
+#pragma unroll
+        for (int k = 0; k < LA; k++) {
+            ra[k] = fa(k);
+            rb[k] = fb(k);
+        }
 #pragma unroll
         for (int ks = 0; ks < NSL; ks++) {
-            const bf16x8_t a = frag_tr(Ks, SV, 32 * ks, 16 * dt, lane);
-            bf16x8_t b;
-            if constexpr (SW) b = frag_tr_ds(reinterpret_cast<const char*>(dSs), 32 * ks, 16 * u, lane);
-            else b = frag_tr(dSs, BWD_SDS, 32 * ks, 16 * u, lane);
+            const bf16x8_t a = ra[ks % LA], b = rb[ks % LA];
+            if (ks + LA < NSL) {
+                ra[ks % LA] = fa(ks + LA);
+                rb[ks % LA] = fb(ks + LA);
+            }
             if (ks & 1) acc1 = mfma(a, b, acc1);
             else acc = mfma(a, b, acc);
         }
+#else
+#pragma unroll
+        for (int ks = 0; ks < NSL; ks++) {
+            const bf16x8_t a = fa(ks), b = fb(ks);
+            if (ks & 1) acc1 = mfma(a, b, acc1);
+            else acc = mfma(a, b, acc);
+        }
+#endif
         acc += acc1;
         // lane (i,g): d = 16dt + 4g + r, q = q0 + 16u + i (padded queries: dS = 0)
         const int q = q0 + 16 * u + i;
