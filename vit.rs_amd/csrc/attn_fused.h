@@ -70,6 +70,34 @@ __device__ __forceinline__ bf16x8_t frag_row(const bf16_t* img, int stride, int 
     if (!(Geo<HS>::HALF && s == Geo<HS>::KS - 1)) hi = *reinterpret_cast<const bf16x4_t*>(p + 16);
     return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
+// The same fragments as two ds_read_b64 each.  hipcc merges the four 8-byte reads of a row block
+// (k offsets 0, 16, 32, 48 of the HS = 64 row) into two ds_read2_b64: 8 LDS cycles each with 32-bank
+// groups of 16 lanes, where rows i and i + 8 of the HS + 8 stride collide (16 cycles) — against 2
+// cycles for a ds_read_b64 (64 banks, conflict-free at that stride: MI355X_MICROARCH.md §LDS).
+// `RowBases` holds one address per (k-step, half) with the offsets hidden from the compiler, so
+// no two reads share a base and a constant offset.
+template <int HS>
+struct RowBases {
+    static constexpr int N = 2 * Geo<HS>::KS;
+    const char* b[N];
+    __device__ __forceinline__ RowBases(const bf16_t* img, int stride, int lane) {
+        const int i = lane & 15, g = lane >> 4;
+        const char* p = reinterpret_cast<const char*>(img + i * stride + 4 * g);
+#pragma unroll
+        for (int k = 0; k < N; k++) {
+            int off = 32 * k;  // k = 2 s + half
+            if (k > 0) asm volatile("" : "+v"(off));
+            b[k] = p + off;
+        }
+    }
+    // rows r0 + i, k-step s
+    __device__ __forceinline__ bf16x8_t frag(int r0, int stride, int s) const {
+        const bf16x4_t lo = *reinterpret_cast<const bf16x4_t*>(b[2 * s] + r0 * stride * 2);
+        bf16x4_t hi = {};
+        if (!(Geo<HS>::HALF && s == Geo<HS>::KS - 1)) hi = *reinterpret_cast<const bf16x4_t*>(b[2 * s + 1] + r0 * stride * 2);
+        return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+};
 // the same fragment straight from a [T][ld] global operand (rows >= T -> 0)
 template <int HS>
 __device__ __forceinline__ bf16x8_t frag_glb(const bf16_t* base, long long ld, int row, int T, int s, int lane) {
@@ -239,6 +267,10 @@ __global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* 
     __syncthreads();
     ATTN_STAMP(2);
     const float c = LOG2E / sqrtf((float)HS);
+#ifndef VIT_ATTN_FWD_SPLIT
+#define VIT_ATTN_FWD_SPLIT 1  // K row fragments as separate ds_read_b64 (RowBases); 0: hipcc merges them into ds_read2_b64
+#endif
+    const RowBases<HS> kb(Ks, G::SK, lane);
     for (int qt = w; qt < nqt; qt += 4) {
         const int q = qt * 16 + i;
         it = qt / 4;
@@ -252,7 +284,10 @@ __global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* 
         for (int kt = 0; kt < NKT; kt++) {
             f32x4_t a = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int s = 0; s < G::KS; s++) a = mfma(frag_row<HS>(Ks, G::SK, kt * 16, s, lane), qf[s], a);
+            for (int s = 0; s < G::KS; s++) {
+                if constexpr (VIT_ATTN_FWD_SPLIT) a = mfma(kb.frag(kt * 16, G::SK, s), qf[s], a);
+                else a = mfma(frag_row<HS>(Ks, G::SK, kt * 16, s, lane), qf[s], a);
+            }
             sacc[kt] = a;
         }
         ATTN_STAMP(1);
