@@ -1219,6 +1219,25 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
         }
     };
     fetch_slice(0);
+    // lse and delta = rowsum(dO * O) for every query (padded queries: lse = +inf -> P = 0).  With one
+    // query per thread their rows are requested here, before the K image's, so the prologue is one
+    // memory round trip, not two (rows past T are clamped to row T-1 and their results dropped: no
+    // branch around the loads)
+#ifndef VIT_ATTN_BWD1_EARLY
+#define VIT_ATTN_BWD1_EARLY 1
+#endif
+    constexpr bool EARLY = VIT_ATTN_BWD1_EARLY && TPQ <= NT;
+    uint4 ov[EARLY ? CH : 1], dv[EARLY ? CH : 1];
+    float ls_e = INFINITY;
+    if constexpr (EARLY) {
+        const int t = min(tid, T - 1);
+#pragma unroll
+        for (int cc = 0; cc < CH; cc++) {
+            ov[cc] = *reinterpret_cast<const uint4*>(obase + (long long)t * C + cc * 8);
+            dv[cc] = *reinterpret_cast<const uint4*>(dbase + (long long)t * C + cc * 8);
+        }
+        ls_e = lse[(long long)bh * T + t];
+    }
     {
         bf16_t* const img[1] = {Ks};
         const int st[1] = {SV};
@@ -1227,18 +1246,27 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
         load_images<HS, TP, NT, 1>(img, st, src, ld, T);
     }
     put_slice(0);
-    // lse and delta = rowsum(dO * O) for every query (padded queries: lse = +inf -> P = 0)
-    for (int t = tid; t < TPQ; t += NT) {
-        float dl = 0.f, ls = INFINITY;
-        if (t < T) {
-            ls = lse[(long long)bh * T + t];
+    if constexpr (EARLY) {
+        if (tid < TPQ) {
+            float dl = 0.f;
 #pragma unroll
-            for (int cc = 0; cc < CH; cc++)
-                dl += dot8_bf16(*reinterpret_cast<const uint4*>(obase + (long long)t * C + cc * 8),
-                                *reinterpret_cast<const uint4*>(dbase + (long long)t * C + cc * 8));
+            for (int cc = 0; cc < CH; cc++) dl += dot8_bf16(ov[cc], dv[cc]);
+            lse_s[tid] = tid < T ? ls_e : INFINITY;
+            del_s[tid] = tid < T ? dl : 0.f;
         }
-        lse_s[t] = ls;
-        del_s[t] = dl;
+    } else {
+        for (int t = tid; t < TPQ; t += NT) {
+            float dl = 0.f, ls = INFINITY;
+            if (t < T) {
+                ls = lse[(long long)bh * T + t];
+#pragma unroll
+                for (int cc = 0; cc < CH; cc++)
+                    dl += dot8_bf16(*reinterpret_cast<const uint4*>(obase + (long long)t * C + cc * 8),
+                                    *reinterpret_cast<const uint4*>(dbase + (long long)t * C + cc * 8));
+            }
+            lse_s[t] = ls;
+            del_s[t] = dl;
+        }
     }
     if constexpr (XK) {
         for (int d = tid; d < HS; d += NT) {
