@@ -70,6 +70,8 @@ def main():
     ap.add_argument("--stagger", type=int, default=0, help="first-round stagger, 0.5 us units (g4 engines)")
     ap.add_argument("--M", type=int, default=0, help="token rows (default 50432; 25216 = one micro-batch)")
     ap.add_argument("--per-round", action="store_true", help="persistent engine: tile times by round")
+    ap.add_argument("--debug", default="0", help="comma-separated extra gemm_bf16_set_debug flags to compare "
+                    "(16: the persistent engine drains its stores after each epilogue)")
     args = ap.parse_args()
     L = vit.lib()
     assert L.vit_init(0) == 0
@@ -90,9 +92,9 @@ def main():
         M, N, K, epi = SHAPES[name]
         if args.M:
             M = args.M
-        for var in [int(v) for v in args.variants.split(",")]:
+        for var, dbg in [(int(v), int(d)) for v in args.variants.split(",") for d in args.debug.split(",")]:
             L.gemm_bf16_set_variant(var)
-            L.gemm_bf16_set_debug(args.stagger * 256)
+            L.gemm_bf16_set_debug(args.stagger * 256 + dbg)
 
             def run():
                 aux = aux16.ptr if epi in (6, 9) else (aux32.ptr if epi == 5 else None)
@@ -111,7 +113,7 @@ def main():
             nwg = -(-M // bm) * -(-N // bn)
             tr = trace.numpy().reshape(-1, 16)[:nwg]
             r = analyse(tr, 8 if var in (2, 7) else 4)
-            print(f"{name:13s} v{var} span {r['span_us']:7.1f} us  prologue {r['prologue_us']:5.2f}  main {r['main_us']:6.2f}  "
+            print(f"{name:13s} v{var} d{dbg} span {r['span_us']:7.1f} us  prologue {r['prologue_us']:5.2f}  main {r['main_us']:6.2f}  "
                   f"epi(last wave) {r['epi_us']:6.2f}  wave-end skew {r['wave_skew_us']:5.2f}  "
                   f"CUs {r['cus']}  wg/CU {r['wg_per_cu']:.1f}  resident {r['max_resident']}  "
                   f"epi beside other's main loop {r['epi_overlap']:.2f}  turnaround {r['turnaround_us']:.2f} us",

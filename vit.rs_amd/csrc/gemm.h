@@ -77,14 +77,14 @@ struct GemmArgs {
     // mxc_off % 64 == 0.  Bit-identical to quantize_mx_cols_bf16 of the bf16 output.  With
     // mx_q / mxc_q set, the MX-copied bf16 output (C2 of GELU / GELU_D, C of DGELU / MUL) may be
     // nullptr: not stored.
-// variant 10 (split tail of the persistent engine): fp32 partial tiles of the last round, one buffer
-    // per concurrent stream (nullptr = the thread workspace); up to 64 MiB at 256 CUs
-    float* tail_ws = nullptr;
-    size_t tail_ws_bytes = 0;
-        uint8_t* mxc_q = nullptr;
+    uint8_t* mxc_q = nullptr;
     uint8_t* mxc_s = nullptr;
     long long mxc_ld = 0;
     long long mxc_off = 0;
+    // variant 10 (split tail of the persistent engine): fp32 partial tiles of the last round, one buffer
+    // per concurrent stream (nullptr = the thread workspace); up to 64 MiB at 256 CUs
+    float* tail_ws = nullptr;
+    size_t tail_ws_bytes = 0;
 };
 
 // fp32 operands, exact-fp32 MFMA (v_mfma_f32_16x16x4_f32); any shape/stride. Parity path.

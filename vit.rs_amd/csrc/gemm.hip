@@ -649,6 +649,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_s(GemmParams p) {
                                    __builtin_amdgcn_s_getreg((31 << 11) | 4);
             }
         }
+        if (p.dbg & 16) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // diagnostic: store drain
         zero_acc();
         // recomputed rather than carried: nothing of the next tiles' sources stays live through the epilogue
         if (more) tile_src(j + 1, cur);
@@ -1297,6 +1298,7 @@ GemmParams make_gemm_params(const GemmArgs& a, int kchunk) {
     p.lda = a.lda; p.ldb = a.ldb; p.ldc = a.ldc; p.ldaux = a.ldaux;
     p.M = a.M; p.N = a.N; p.K = a.K; p.kchunk = kchunk;
     p.no_epi = (g_debug_flags & 2) ? 1 : 0;
+    p.dbg = g_debug_flags & 0xF0;
     p.stagger = (g_debug_flags >> 8) * 50;  // debug: 0.5 us units
     p.trace = g_trace;
     p.mx_q = a.mx_q;

@@ -18,6 +18,8 @@ struct GemmParams {
     int M, N, K;
     int kchunk;  // K range per split (multiple of the K tile)
     int no_epi;  // diagnostic (gemm_bf16_set_debug): skip the epilogue, keep the accumulators live
+    int dbg;     // diagnostic flags (gemm_bf16_set_debug & 0xF0): 16 = persistent engine drains its
+                 // epilogue stores (vmcnt(0)) before the next tile's main loop
     int stagger;  // two-per-CU engines: first-round delay (100 MHz ticks) of the CU's second workgroup
     unsigned long long* trace;  // diagnostic: [workgroup][4] start, main-loop end, end, hw id
     int tiles;   // output tiles of the launch (the grid is tiles x K-splits)
