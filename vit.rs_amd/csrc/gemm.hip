@@ -510,8 +510,16 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_s(GemmParams p) {
             ts.kbeg = (v - u * p.tsplit) * p.kchunk;
             ts.nk = (min(p.K, ts.kbeg + p.kchunk) - ts.kbeg) / BK;  // host: >= 2 steps
         }
-        ts.tm0 = (ts.t / ntn) * BM;
-        ts.tn0 = (ts.t % ntn) * BN;
+        if (!TS && p.gm > 0) {  // (the split-tail variant keeps the row-major order its fix-up assumes)
+            // groups of gm row panels walked column by column: the tiles an XCD runs at once share
+            // gm A panels and 32 / gm B panels instead of ~3 A panels and every B panel
+            const int per = p.gm * ntn, g = ts.t / per, r = ts.t - g * per, rows = min(p.gm, ntm - g * p.gm);
+            ts.tm0 = (g * p.gm + r % rows) * BM;
+            ts.tn0 = (r / rows) * BN;
+        } else {
+            ts.tm0 = (ts.t / ntn) * BM;
+            ts.tn0 = (ts.t % ntn) * BN;
+        }
 #pragma unroll
         for (int q = 0; q < 2; q++) {
             const int row = (q * 8 + wave) * 16 + (lane >> 2);
@@ -1299,6 +1307,15 @@ GemmParams make_gemm_params(const GemmArgs& a, int kchunk) {
     p.M = a.M; p.N = a.N; p.K = a.K; p.kchunk = kchunk;
     p.no_epi = (g_debug_flags & 2) ? 1 : 0;
     p.dbg = g_debug_flags & 0xF0;
+    // persistent-engine tile order (bench_gemm, ViT-B/16 shapes, GM 0 / 4 / 8 / 16): groups of 8 row
+    // panels help where the A panels are small (K <= 768: qkv fwd 188 -> 179 us, proj fwd 137 -> 133)
+    // and hurt where they are large (K = 3072: fcproj fwd 289 -> 302, fc dgrad 235 -> 247: each A panel
+    // is then re-read once per column group); VIT_GEMM_GM overrides
+    static const int gm_env = [] {
+        const char* e = getenv("VIT_GEMM_GM");
+        return e && *e ? atoi(e) : -1;
+    }();
+    p.gm = gm_env >= 0 ? gm_env : (a.K <= 768 ? 8 : 0);
     p.stagger = (g_debug_flags >> 8) * 50;  // debug: 0.5 us units
     p.trace = g_trace;
     p.mx_q = a.mx_q;

@@ -23,6 +23,8 @@ struct GemmParams {
     int stagger;  // two-per-CU engines: first-round delay (100 MHz ticks) of the CU's second workgroup
     unsigned long long* trace;  // diagnostic: [workgroup][4] start, main-loop end, end, hw id
     int tiles;   // output tiles of the launch (the grid is tiles x K-splits)
+    int gm;      // persistent engine tile order: groups of gm row panels, column-major inside a group
+                 // (0: row-major; VIT_GEMM_GM)
     uint8_t* mx_q;  // fused MX output (GemmArgs::mx_q / mx_s); mx_rg = padded rows / 32
     uint8_t* mx_s;
     int mx_rg;
