@@ -397,6 +397,39 @@ def test_gemm_bf16_layouts(gpu, engine, M, N, K, ak, bk):
             assert rel_err(dbias.numpy(), ar.sum(1)) < 2e-3
 
 
+@pytest.mark.parametrize("gm", [0, 1, 3, 8, 14])
+@pytest.mark.parametrize("M,N,K", [(6304, 3072, 768), (1576, 768, 3072), (776, 1000, 128)])
+def test_gemm_bf16_tile_order_bit_identical(gpu, M, N, K, gm):
+    """The persistent engine's tile order (row-major, or groups of gm row panels walked column by
+    column, partial last group included) only moves tiles between CUs and rounds: every output is
+    bit-identical to the one-tile engine (variant 2)."""
+    v = gpu
+    L = v.lib()
+    rng = np.random.default_rng(M + 5 * N + K + gm)
+    ab = v.bf16_bits(rng.uniform(-1, 1, size=(M, K)).astype(np.float32))
+    wb = v.bf16_bits((rng.uniform(-1, 1, size=(N, K)) * 0.1).astype(np.float32))
+    A, W = D(v, ab, np.uint16), D(v, wb, np.uint16)
+    bias = D(v, rng.normal(size=N).astype(np.float32))
+    res = D(v, rng.normal(size=(M, N)).astype(np.float32))
+    outs = {}
+    try:
+        for var, flags in ((2, 0), (7, (gm + 1) << 16)):
+            L.gemm_bf16_set_variant(var)
+            L.gemm_bf16_set_debug(flags)
+            o = []
+            for epi in (3, 5):
+                c = Z(v, M * N, np.float32 if epi == 5 else np.uint16)
+                v.call("gemm_bf16_fused", c, None, N, res if epi == 5 else None, N, A, K, 1, W, K, 1, bias,
+                       None, M, N, K, epi)
+                o.append(c.numpy())
+            outs[var] = o
+    finally:
+        L.gemm_bf16_set_debug(0)
+        L.gemm_bf16_set_variant(0)
+    for x, y in zip(outs[2], outs[7]):
+        assert np.array_equal(x, y)
+
+
 @pytest.mark.parametrize("pair", [(4, 5), (2, 7), (2, 9)])
 @pytest.mark.parametrize("M,N,K", [(6304, 3072, 768), (1576, 768, 3072), (520, 384, 256), (776, 1000, 128),
                                    (50432, 768, 768)])

@@ -1315,8 +1315,9 @@ GemmParams make_gemm_params(const GemmArgs& a, int kchunk) {
         const char* e = getenv("VIT_GEMM_GM");
         return e && *e ? atoi(e) : -1;
     }();
-    p.gm = gm_env >= 0 ? gm_env : (a.K <= 768 ? 8 : 0);
-    p.stagger = (g_debug_flags >> 8) * 50;  // debug: 0.5 us units
+    const int gm_dbg = (g_debug_flags >> 16) & 0xF;  // diagnostic: (gm + 1) << 16 forces gm (tests)
+    p.gm = gm_dbg ? gm_dbg - 1 : gm_env >= 0 ? gm_env : (a.K <= 768 ? 8 : 0);
+    p.stagger = ((g_debug_flags >> 8) & 0xFF) * 50;  // debug: 0.5 us units
     p.trace = g_trace;
     p.mx_q = a.mx_q;
     p.mx_s = a.mx_s;
