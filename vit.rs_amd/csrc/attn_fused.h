@@ -1281,6 +1281,7 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
 #pragma unroll
         for (int s = 0; s < KS; s++) R.kf[kk][s] = frag_row<HS>(Ks, SV, key0 + 16 * kk, s, lane);
     float xacc = 0.f, xsds = 0.f;  // XK: this thread's dK / dV element of key T-1; sum of its dS
+    [[maybe_unused]] const int xo = tid - (NT - 2 * HS);  // XK: that element's index (>= 0: the last 2 HS threads)
     // XK: the 8 dims 8p .. 8p+7 (p = tid & 15 < HS / 8) of key T-1's K and V rows, in registers for
     // the item: each query's s = q . k and dP = do . v is 16 lanes x one 16-B slice read
     float xkr[8], xvr[8];
@@ -1331,10 +1332,12 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
         __syncthreads();
         ATTN_STAMP(2);
         if constexpr (XK) {
-            if (tid < 2 * HS) {
-                const bf16_t* img = (tid < HS ? Qs : Ds) + cur * 32 * SK;
-                const float* wv = tid < HS ? xds_s : xp_s;
-                const int d = tid < HS ? tid : tid - HS;
+            // the last 2 HS threads (waves 5-7 at 8 waves): waves 0-4 carry put_slice's pieces and
+            // waves 0-1 phase B's two extra dQ tiles, so these run beside them instead of after them
+            if (xo >= 0) {
+                const bf16_t* img = (xo < HS ? Qs : Ds) + cur * 32 * SK;
+                const float* wv = xo < HS ? xds_s : xp_s;
+                const int d = xo < HS ? xo : xo - HS;
 #pragma unroll 8
                 for (int j = 0; j < 32; j++) {
                     xacc += wv[j] * slice_at<HS>(img, j, d);
@@ -1357,8 +1360,8 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
                      dsum ? dsum + ((long long)(b * NWR + w) * NH + h) * 3 * HS : nullptr, lane, it);
     ATTN_STAMP(7);
     if constexpr (XK) {  // key T-1's dK, dV and its column-sum row (index NW of the item)
-        if (tid < 2 * HS) {
-            const int o = tid, d = o < HS ? o : o - HS;
+        if (xo >= 0) {
+            const int o = xo, d = o < HS ? o : o - HS;
             const float v = o < HS ? xacc * scale : xacc;
             dq[(long long)(T - 1) * C3 + (o < HS ? C : 2 * C) + d] = f2bf(v);
             if (dsum) {
