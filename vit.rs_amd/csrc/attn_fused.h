@@ -1431,6 +1431,13 @@ __global__ __launch_bounds__(NKT / KK * 64, 1) void attn_bwdp_k(bf16_t* __restri
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int key0 = w * 16 * KK;
+    // the waves that own a slice piece (PER = 1: the first 32 CH / 64); the others would fetch and
+    // store duplicates (VIT_ATTN_SLICE_ALL=1: every wave does, the pre-r05 form)
+#ifndef VIT_ATTN_SLICE_ALL
+#define VIT_ATTN_SLICE_ALL 0
+#endif
+    constexpr bool SPLIT_SLICE = !VIT_ATTN_SLICE_ALL && Bwdp<HS, NKT, KK>::PER == 1 && (32 * G::CH) % 64 == 0;
+    const bool slice_wave = !SPLIT_SLICE || w < 32 * G::CH / 64;
     const float scale = 1.0f / sqrtf((float)HS);
     const float c = LOG2E * scale;
     auto qkv_of = [&](int bh) { return qkv + (long long)(bh / NH) * T * C3 + (bh % NH) * HS; };
@@ -1544,8 +1551,10 @@ __global__ __launch_bounds__(NKT / KK * 64, 1) void attn_bwdp_k(bf16_t* __restri
             // reads again, so the compiler sees every prefetch register consumed on every path and
             // does not drain vmcnt before re-using them)
             if constexpr (!(VIT_ATTN_DIAG & 1)) {
-                if (sl + 1 < NSL) fetch_slice(s_cur, q0 + 32);
-                else fetch_slice(s_nxt, 0);
+                if (slice_wave) {
+                    if (sl + 1 < NSL) fetch_slice(s_cur, q0 + 32);
+                    else fetch_slice(s_nxt, 0);
+                }
                 fetch_side(s_nxt, sl);
                 // unconditional load (past T: 0); padded keys get +inf when it is put
                 if (sl == 0) lse_n = buf_ldf(s_nxt.l, 4 * tid);
@@ -1561,7 +1570,7 @@ __global__ __launch_bounds__(NKT / KK * 64, 1) void attn_bwdp_k(bf16_t* __restri
                     bwd_slice_b<HS, NSL, NW>(Kimg + kb * TP * SV, dSs + ((sl - 1) & 1) * TP * Z::SDS, dq, C3,
                                              q0 - 32, T, scale, w, lane);
                 ATTN_STAMP(2);
-                put_slice(cur ^ 1);
+                if (slice_wave) put_slice(cur ^ 1);
                 if (sl == 0 && tid < TP) lse_s[((n + 1) & 1) * TP + tid] = tid < T ? lse_n : INFINITY;
                 ATTN_STAMP(3);
                 __syncthreads();
