@@ -1197,6 +1197,25 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
         for (int s = 0; s < KS; s++) R.vf[kk][s] = frag_glb<HS>(base + 2 * C, C3, key0 + 16 * kk + i, T, s, lane);
     // one slice (32 rows) of Q and dO: PER 16-B pieces per thread and operand
     uint4 pq[PER], pd[PER];
+#ifndef VIT_ATTN_BWD1_BUF
+#define VIT_ATTN_BWD1_BUF 1
+#endif
+#if VIT_ATTN_BWD1_BUF
+    // buffer loads (rows >= T read 0, no "zero, then load if in range" merge), lanes past the last
+    // piece repeating one (put_slice skips them), and only the waves that own a piece
+    const auto rq_s = buf_rsrc(base, (uint32_t)(T * C3 * 2)), rd_s = buf_rsrc(dbase, (uint32_t)(T * C * 2));
+    const bool slice_wave = __builtin_amdgcn_readfirstlane(w) * 64 < 32 * CH;  // a piece in the wave's first lane
+    auto fetch_slice = [&](int q0) {
+        if (!slice_wave) return;
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            const int idx = (j * NT + tid) % (32 * CH), t = idx / CH, c = idx - t * CH;
+            const uint32_t r = (uint32_t)(q0 + t);
+            pq[j] = buf_ld16(rq_s, r * (uint32_t)(C3 * 2) + 16 * c);
+            pd[j] = buf_ld16(rd_s, r * (uint32_t)(C * 2) + 16 * c);
+        }
+    };
+#else
     auto fetch_slice = [&](int q0) {
 #pragma unroll
         for (int j = 0; j < PER; j++) {
@@ -1208,6 +1227,7 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
             }
         }
     };
+#endif
     auto put_slice = [&](int buf) {
 #pragma unroll
         for (int j = 0; j < PER; j++) {
