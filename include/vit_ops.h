@@ -233,7 +233,8 @@ void gemm_fp8_fused_mxc(void* C, void* C2, long long ldc, const void* aux, long 
  * workgroup with the split-K weight gradients on 256x128, 4 = 256x128 two per CU everywhere,
  * 5 = 4 with a software-pipelined main loop, 7 = production: 2 with the persistent streaming
  * 256x256 engine for the K-contiguous GEMMs) and diagnostics (flag 2: skip epilogues, main-loop
- * timing only; flag 16: the persistent engine drains its stores after each epilogue; (flags >> 8) &
+ * timing only; flag 16: the persistent engine drains its stores after each epilogue; flag 32: every
+ * output row stored onto row 0 (timing only, wrong outputs: no HBM write traffic); (flags >> 8) &
  * 0xFF: first-round stagger in 0.5 us units; (flags >> 16) & 0xF = g + 1: persistent-engine tile
  * groups of g row panels, 0 = column-major ... default 8 for K <= 768, else row-major) */
 void gemm_bf16_set_variant(int variant);

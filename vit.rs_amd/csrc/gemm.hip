@@ -625,8 +625,14 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_s(GemmParams p) {
         float bpre[8];
         staged_bias_prefetch<EPI>(p, lane, cur.tn0 + wn * 64, bpre);
         // the next tile's steps 0 and 1 (and the bias) landed; every wave's reads of this tile's
-        // last two slots done before they become staging space
+        // last two slots done before they become staging space.  Through the builtin, not asm: hipcc
+        // then knows no LDS-DMA is pending after the epilogue and does not put a vmcnt(0) in front
+        // of the next tile's first fragment reads (it did: a wait for all of this epilogue's stores)
+#if VIT_G2_EPI_WAIT_ASM
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#else
+        __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) expcnt(7) lgkmcnt(0), visible to the compiler (below)
+#endif
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
@@ -1304,6 +1310,7 @@ GemmParams make_gemm_params(const GemmArgs& a, int kchunk) {
     GemmParams p;
     p.A = a.A; p.B = a.B; p.C = a.C; p.C2 = a.C2; p.aux = a.aux; p.bias = a.bias; p.dbias = a.dbias; p.colsum_out = nullptr;
     p.lda = a.lda; p.ldb = a.ldb; p.ldc = a.ldc; p.ldaux = a.ldaux;
+    if (g_debug_flags & 32) p.ldc = 0;  // diagnostic (timing only, wrong outputs): every row stores onto row 0
     p.M = a.M; p.N = a.N; p.K = a.K; p.kchunk = kchunk;
     p.no_epi = (g_debug_flags & 2) ? 1 : 0;
     p.dbg = g_debug_flags & 0xF0;
