@@ -403,7 +403,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_s(F8Params fp) {
         if (!lagging) bar();  // balance the stagger barrier
         float bpre[8];
         staged_bias_prefetch<EPI>(p, lane, cur.tn0 + wn * 64, bpre);
+        // through the builtin so hipcc knows no LDS-DMA is pending afterwards (as g2::gemm_kernel_s)
+#if VIT_F8_EPI_WAIT_ASM
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#else
+        __builtin_amdgcn_s_waitcnt(0x0070);
+#endif
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
