@@ -195,6 +195,17 @@ __device__ __forceinline__ uint4 buf_ld16(__amdgpu_buffer_rsrc_t r, uint32_t off
 __device__ __forceinline__ float buf_ldf(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
 }
+typedef uint32_t v2u32_t __attribute__((ext_vector_type(2)));
+// the fragment of frag_glb from a buffer resource over the [T][ld] operand (rows >= T read 0)
+template <int HS>
+__device__ __forceinline__ bf16x8_t frag_buf(__amdgpu_buffer_rsrc_t r, uint32_t ld_bytes, int row, int s, int lane) {
+    const uint32_t off = (uint32_t)row * ld_bytes + 2u * (32 * s + 4 * (lane >> 4));
+    const bf16x4_t lo = __builtin_bit_cast(bf16x4_t, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+    bf16x4_t hi = {};
+    if (!(Geo<HS>::HALF && s == Geo<HS>::KS - 1))
+        hi = __builtin_bit_cast(bf16x4_t, __builtin_amdgcn_raw_buffer_load_b64(r, off + 32, 0, 0));
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
 
 // Swizzled LDS images of the one-pass backward at head size 64 (rows of 128 B), conflict-free for
 // every access (tools/lds_banks.py model, MI355X_MICROARCH.md §LDS):
@@ -232,7 +243,9 @@ constexpr int fwd_lds_bytes() { return NKT * 16 * (Geo<HS>::SK + Geo<HS>::SV) * 
 template <int HS, int NKT>
 constexpr int fwd_occ() { return fwd_lds_bytes<HS, NKT>() <= 80 * 1024 ? 2 : 1; }
 
-template <int HS, int NKT>
+// NS: key tiles that hold a key (< T) -- the score MFMAs, the mask and the exponentials skip the
+// all-padding tiles (NKT - NS of them, at most one: TP rounds T up to 32); P.V still runs NKT/2 pairs
+template <int HS, int NKT, int NS = NKT>
 __global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* __restrict__ out,
                                                                         float* __restrict__ lse,
                                                                         const bf16_t* __restrict__ qkv,
@@ -249,9 +262,21 @@ __global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* 
     ATTN_STAMP(0);
     // Q fragments of a 16-query tile straight from HBM (rows >= T -> 0); the next tile's are
     // requested while the current one computes, the first ones before the K/V staging
+#ifndef VIT_ATTN_FWD_BUF
+#define VIT_ATTN_FWD_BUF 1  // Q loads and output / lse stores as buffer operations (no branches in the loop)
+#endif
+    // Branch-free Q loads and output stores (buffer operations: rows >= T read 0 / are dropped) let
+    // hipcc count the loop's vmcnt: the next tile's Q loads are waited for, the previous tile's
+    // stores stay in flight (with the "if (q < T)" stores and "row < T" loads it waited vmcnt(0))
+    [[maybe_unused]] const auto rq = buf_rsrc(base, (uint32_t)(T * C3 * 2));
+    [[maybe_unused]] const auto ro = buf_rsrc(out + (long long)b * T * C + h * HS, (uint32_t)(T * C * 2));
+    [[maybe_unused]] const auto rl = buf_rsrc(lse + (long long)bh * T, (uint32_t)(T * 4));
     auto load_q = [&](int qt, bf16x8_t (&qf)[G::KS]) {
 #pragma unroll
-        for (int s = 0; s < G::KS; s++) qf[s] = frag_glb<HS>(base, C3, qt * 16 + i, T, s, lane);
+        for (int s = 0; s < G::KS; s++) {
+            if constexpr (VIT_ATTN_FWD_BUF) qf[s] = frag_buf<HS>(rq, (uint32_t)(C3 * 2), qt * 16 + i, s, lane);
+            else qf[s] = frag_glb<HS>(base, C3, qt * 16 + i, T, s, lane);
+        }
     };
     const int nqt = (T + 15) / 16;
     bf16x8_t qn[G::KS];
@@ -281,7 +306,9 @@ __global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* 
         if (qt + 4 < nqt) load_q(qt + 4, qn);
         f32x4_t sacc[NKT];
 #pragma unroll
-        for (int kt = 0; kt < NKT; kt++) {
+        for (int kt = NS; kt < NKT; kt++) sacc[kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kt = 0; kt < NS; kt++) {
             f32x4_t a = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int s = 0; s < G::KS; s++) {
@@ -296,10 +323,11 @@ __global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* 
         // measured slower: 107 vs 104 us, it splits the block the scheduler interleaves)
         float mx = -INFINITY;
 #pragma unroll
-        for (int kt = 0; kt < NKT; kt++)
+        for (int kt = 0; kt < NS; kt++)
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                const float x = kt * 16 + 4 * g + r < T ? sacc[kt][r] : -INFINITY;
+                // only the last score tile can hold padded keys (NKT = 2 ceil(T/32), launch_fwd)
+                const float x = kt < NS - 1 || kt * 16 + 4 * g + r < T ? sacc[kt][r] : -INFINITY;
                 sacc[kt][r] = x;
                 mx = fmaxf(mx, x);
             }
@@ -308,7 +336,7 @@ __global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* 
         mx *= c;
         float l = 0.f;
 #pragma unroll
-        for (int kt = 0; kt < NKT; kt++)
+        for (int kt = 0; kt < NS; kt++)
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 const float p = fexp2(fmaf(sacc[kt][r], c, -mx));
@@ -328,7 +356,19 @@ __global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* 
             for (int dt = 0; dt < G::DT; dt++) o[dt] = mfma(frag_tr(Vs, G::SV, 32 * ks, 16 * dt, lane), pb, o[dt]);
         }
         ATTN_STAMP(3);
-        if (q < T) {
+        if constexpr (VIT_ATTN_FWD_BUF) {
+            // every lane stores: rows q >= T fall past the resources' ends; the four lanes of a query
+            // write the same lse value
+            const float inv = 1.0f / l;
+            const uint32_t off = (uint32_t)q * (uint32_t)(C * 2) + 8u * g;
+#pragma unroll
+            for (int dt = 0; dt < G::DT; dt++) {
+                const uint2 v = make_uint2(pack_bf16x2(o[dt][0] * inv, o[dt][1] * inv),
+                                           pack_bf16x2(o[dt][2] * inv, o[dt][3] * inv));
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, v), ro, off + 32u * dt, 0, 0);
+            }
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, mx + log2f(l)), rl, 4u * q, 0, 0);
+        } else if (q < T) {
             const float inv = 1.0f / l;
             bf16_t* dst = out + ((long long)b * T + q) * C + h * HS + 4 * g;
 #pragma unroll
@@ -1641,9 +1681,17 @@ constexpr int max_tp() {
 
 // launchers over the key-tile count (NKT = 2, 4, ..., 2*max_tp/32)
 template <int HS, int NKT>
-void launch_fwd(bf16_t* out, float* lse, const bf16_t* qkv, int B, int T, int C, int NH, hipStream_t s) {
-    attn_fwd_k<HS, NKT><<<B * NH, 256, 0, s>>>(out, lse, qkv, T, C, NH);
+bool launch_fwd(bf16_t* out, float* lse, const bf16_t* qkv, int B, int T, int C, int NH, hipStream_t s) {
+    if (T > NKT * 16 || T <= (NKT - 2) * 16) return false;  // the kernel masks keys in its last score tile only
+#ifndef VIT_ATTN_FWD_TRIM
+#define VIT_ATTN_FWD_TRIM 1
+#endif
+    if (VIT_ATTN_FWD_TRIM && (NKT - 1) * 16 >= T)
+        attn_fwd_k<HS, NKT, NKT - 1><<<B * NH, 256, 0, s>>>(out, lse, qkv, T, C, NH);
+    else
+        attn_fwd_k<HS, NKT><<<B * NH, 256, 0, s>>>(out, lse, qkv, T, C, NH);
     count_hit(VIT_HIT_ATTN_FWD_MFMA);
+    return true;
 }
 int attn_bwd_variant();  // attention.hip: VIT_ATTN_BWD = pair | one | (default) persistent (A/B)
 int attn_cu_count();     // attention.hip: compute units of the current device
@@ -1699,7 +1747,7 @@ bool dispatch_fwd(int nkt, bf16_t* out, float* lse, const bf16_t* qkv, int B, in
     if constexpr (NKT * 16 > max_tp<HS>()) {
         return false;
     } else {
-        if (nkt == NKT) { launch_fwd<HS, NKT>(out, lse, qkv, B, T, C, NH, s); return true; }
+        if (nkt == NKT) return launch_fwd<HS, NKT>(out, lse, qkv, B, T, C, NH, s);
         return dispatch_fwd<HS, NKT + 2>(nkt, out, lse, qkv, B, T, C, NH, s);
     }
 }
