@@ -243,6 +243,9 @@ constexpr int fwd_lds_bytes() { return NKT * 16 * (Geo<HS>::SK + Geo<HS>::SV) * 
 template <int HS, int NKT>
 constexpr int fwd_occ() { return fwd_lds_bytes<HS, NKT>() <= 80 * 1024 ? 2 : 1; }
 
+#ifndef VIT_ATTN_FWD_BUF
+#define VIT_ATTN_FWD_BUF 1  // K / V staging, Q loads and output / lse stores as buffer operations (no branches in the loop)
+#endif
 // NS: key tiles that hold a key (< T) -- the score MFMAs, the mask and the exponentials skip the
 // all-padding tiles (NKT - NS of them, at most one: TP rounds T up to 32); P.V still runs NKT/2 pairs
 template <int HS, int NKT, int NS = NKT>
@@ -262,9 +265,6 @@ __global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* 
     ATTN_STAMP(0);
     // Q fragments of a 16-query tile straight from HBM (rows >= T -> 0); the next tile's are
     // requested while the current one computes, the first ones before the K/V staging
-#ifndef VIT_ATTN_FWD_BUF
-#define VIT_ATTN_FWD_BUF 1  // Q loads and output / lse stores as buffer operations (no branches in the loop)
-#endif
     // Branch-free Q loads and output stores (buffer operations: rows >= T read 0 / are dropped) let
     // hipcc count the loop's vmcnt: the next tile's Q loads are waited for, the previous tile's
     // stores stay in flight (with the "if (q < T)" stores and "row < T" loads it waited vmcnt(0))
@@ -281,7 +281,28 @@ __global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* 
     const int nqt = (T + 15) / 16;
     bf16x8_t qn[G::KS];
     load_q(w, qn);
-    {
+    if constexpr (VIT_ATTN_FWD_BUF) {
+        // K | V rows through one resource from K's first column (every byte of rows >= T is past its
+        // end, so those rows read 0 without a branch); all loads before the first LDS store
+        const auto rkv = buf_rsrc(base + C, (uint32_t)(T * C3 * 2 - 2 * C));
+        constexpr int CH = G::CH, PER = (TP * CH + 255) / 256;
+        uint4 v[2][PER];
+#pragma unroll
+        for (int o = 0; o < 2; o++)
+#pragma unroll
+            for (int j = 0; j < PER; j++) {
+                const int idx = j * 256 + (int)threadIdx.x, t = idx / CH, cc = idx - t * CH;
+                v[o][j] = buf_ld16(rkv, (uint32_t)t * (uint32_t)(C3 * 2) + (uint32_t)(o * C * 2) + 16 * cc);
+            }
+#pragma unroll
+        for (int o = 0; o < 2; o++)
+#pragma unroll
+            for (int j = 0; j < PER; j++) {
+                const int idx = j * 256 + (int)threadIdx.x, t = idx / CH, cc = idx - t * CH;
+                if ((TP * CH) % 256 == 0 || idx < TP * CH)
+                    *reinterpret_cast<uint4*>((o ? Vs + t * G::SV : Ks + t * G::SK) + cc * 8) = v[o][j];
+            }
+    } else {
         bf16_t* const img[2] = {Ks, Vs};
         const int st[2] = {G::SK, G::SV};
         const bf16_t* const src[2] = {base + C, base + 2 * C};
