@@ -356,14 +356,35 @@ __global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* 
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
         mx *= c;
         float l = 0.f;
+#ifndef VIT_ATTN_FWD_PK
+#define VIT_ATTN_FWD_PK 1  // exponent arguments and the row sum as packed fp32 (v_pk_fma_f32 / v_pk_add_f32)
+#endif
+        if constexpr (VIT_ATTN_FWD_PK) {
+            typedef float f32x2_t __attribute__((ext_vector_type(2)));
+            f32x2_t l2 = {0.f, 0.f};
+            const f32x2_t c2 = {c, c}, m2 = {-mx, -mx};
 #pragma unroll
-        for (int kt = 0; kt < NS; kt++)
+            for (int kt = 0; kt < NS; kt++)
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const float p = fexp2(fmaf(sacc[kt][r], c, -mx));
-                sacc[kt][r] = p;
-                l += p;
-            }
+                for (int r = 0; r < 4; r += 2) {
+                    const f32x2_t x = {sacc[kt][r], sacc[kt][r + 1]};
+                    const f32x2_t y = __builtin_elementwise_fma(x, c2, m2);
+                    const f32x2_t p = {fexp2(y.x), fexp2(y.y)};
+                    sacc[kt][r] = p.x;
+                    sacc[kt][r + 1] = p.y;
+                    l2 += p;
+                }
+            l = l2.x + l2.y;
+        } else {
+#pragma unroll
+            for (int kt = 0; kt < NS; kt++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const float p = fexp2(fmaf(sacc[kt][r], c, -mx));
+                    sacc[kt][r] = p;
+                    l += p;
+                }
+        }
         l += __shfl_xor(l, 16, 64);
         l += __shfl_xor(l, 32, 64);
         ATTN_STAMP(2);
