@@ -347,8 +347,8 @@ __global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* 
         for (int kt = 0; kt < NS; kt++)
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                // only the last score tile can hold padded keys (NKT = 2 ceil(T/32), launch_fwd)
-                const float x = kt < NS - 1 || kt * 16 + 4 * g + r < T ? sacc[kt][r] : -INFINITY;
+                // padded keys lie in the last score tile (trimmed launch) or the last two (NKT = 2 ceil(T/32))
+                const float x = kt < (NS < NKT ? NS - 1 : NKT - 2) || kt * 16 + 4 * g + r < T ? sacc[kt][r] : -INFINITY;
                 sacc[kt][r] = x;
                 mx = fmaxf(mx, x);
             }
@@ -400,8 +400,9 @@ __global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* 
         ATTN_STAMP(3);
         if constexpr (VIT_ATTN_FWD_BUF) {
             // every lane stores: rows q >= T fall past the resources' ends; the four lanes of a query
-            // write the same lse value
-            const float inv = 1.0f / l;
+            // write the same lse value.  l >= 1 (the maximum's term), so v_rcp_f32 / v_log_f32 need no
+            // denormal handling (1 ulp; the outputs are rounded to bf16)
+            const float inv = __builtin_amdgcn_rcpf(l);
             const uint32_t off = (uint32_t)q * (uint32_t)(C * 2) + 8u * g;
 #pragma unroll
             for (int dt = 0; dt < G::DT; dt++) {
@@ -409,7 +410,7 @@ __global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* 
                                            pack_bf16x2(o[dt][2] * inv, o[dt][3] * inv));
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, v), ro, off + 32u * dt, 0, 0);
             }
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, mx + log2f(l)), rl, 4u * q, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, mx + __builtin_amdgcn_logf(l)), rl, 4u * q, 0, 0);
         } else if (q < T) {
             const float inv = 1.0f / l;
             bf16_t* dst = out + ((long long)b * T + q) * C + h * HS + 4 * g;
