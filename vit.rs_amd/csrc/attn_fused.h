@@ -1449,6 +1449,14 @@ __global__ __launch_bounds__(NKT / 2 * 64, 1) void attn_bwd1_k(bf16_t* __restric
             }
         }
         if (sl + 1 < NSLQ) put_slice(cur ^ 1);  // its buffer was last read in the previous slice
+#ifndef VIT_ATTN_BWD1_VMWAIT
+#define VIT_ATTN_BWD1_VMWAIT 1
+#endif
+        // every wave, every slice: the fetch's loads are complete here (put_slice waited for them on the
+        // owning waves; the others issued none).  Without a wait hipcc sees on every path, it kept
+        // the loads possibly pending on the non-owner path and waited vmcnt(0) before the next
+        // fetch — after phase B's dQ stores, so every slice waited for its own stores to complete
+        if constexpr (VIT_ATTN_BWD1_VMWAIT) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) only
         ATTN_STAMP(3);
         bwd_slice_b<HS, NSL, NW, XK>(Ks, dSs, dq, C3, q0, T, scale, w, lane, xds_s, xk_s);
         ATTN_STAMP(4);
