@@ -357,11 +357,12 @@ __global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* 
         mx *= c;
         float l = 0.f;
 #ifndef VIT_ATTN_FWD_PK
-#define VIT_ATTN_FWD_PK 1  // exponent arguments and the row sum as packed fp32 (v_pk_fma_f32 / v_pk_add_f32)
+#define VIT_ATTN_FWD_PK 1  // exponent arguments as packed fp32 (v_pk_fma_f32)
 #endif
         if constexpr (VIT_ATTN_FWD_PK) {
+            // (the row sum stays one serial chain: a pairwise sum changes its rounding, and the fp8
+            // loss-curve fixture's drift margin does not absorb that)
             typedef float f32x2_t __attribute__((ext_vector_type(2)));
-            f32x2_t l2 = {0.f, 0.f};
             const f32x2_t c2 = {c, c}, m2 = {-mx, -mx};
 #pragma unroll
             for (int kt = 0; kt < NS; kt++)
@@ -369,12 +370,11 @@ __global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* 
                 for (int r = 0; r < 4; r += 2) {
                     const f32x2_t x = {sacc[kt][r], sacc[kt][r + 1]};
                     const f32x2_t y = __builtin_elementwise_fma(x, c2, m2);
-                    const f32x2_t p = {fexp2(y.x), fexp2(y.y)};
-                    sacc[kt][r] = p.x;
-                    sacc[kt][r + 1] = p.y;
-                    l2 += p;
+                    sacc[kt][r] = fexp2(y.x);
+                    sacc[kt][r + 1] = fexp2(y.y);
+                    l += sacc[kt][r];
+                    l += sacc[kt][r + 1];
                 }
-            l = l2.x + l2.y;
         } else {
 #pragma unroll
             for (int kt = 0; kt < NS; kt++)
@@ -400,9 +400,9 @@ __global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* 
         ATTN_STAMP(3);
         if constexpr (VIT_ATTN_FWD_BUF) {
             // every lane stores: rows q >= T fall past the resources' ends; the four lanes of a query
-            // write the same lse value.  l >= 1 (the maximum's term), so v_rcp_f32 / v_log_f32 need no
-            // denormal handling (1 ulp; the outputs are rounded to bf16)
-            const float inv = __builtin_amdgcn_rcpf(l);
+            // write the same lse value (v_rcp_f32 / v_log_f32 for 1 / l and log2 l measured no faster and
+            // move the fp8 loss-curve fixture past its drift margin: the IEEE forms are kept)
+            const float inv = 1.0f / l;
             const uint32_t off = (uint32_t)q * (uint32_t)(C * 2) + 8u * g;
 #pragma unroll
             for (int dt = 0; dt < G::DT; dt++) {
@@ -410,7 +410,7 @@ __global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* 
                                            pack_bf16x2(o[dt][2] * inv, o[dt][3] * inv));
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, v), ro, off + 32u * dt, 0, 0);
             }
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, mx + __builtin_amdgcn_logf(l)), rl, 4u * q, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, mx + log2f(l)), rl, 4u * q, 0, 0);
         } else if (q < T) {
             const float inv = 1.0f / l;
             bf16_t* dst = out + ((long long)b * T + q) * C + h * HS + 4 * g;
