@@ -178,9 +178,19 @@ __device__ __forceinline__ float dot8_bf16(uint4 a, uint4 b) {
     }
     return s;
 }
+// four accumulator values (x mul) as four bf16: (v0, v1) and (v2, v3) as two float2 -> bf16x2
+// conversions, one v_cvt_pk_bf16_f32 each (hipcc vectorised the scalar pack_bf16x2 form as
+// (v0, v2) / (v1, v3) products and then needed six and / shift / or ops to put the halves back);
+// the same RNE rounding, bit-identical
+typedef float f32x2v_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint2 pack4_bf16(f32x4_t v, float mul) {
+    const f32x2v_t lo = f32x2v_t{v[0], v[1]} * mul, hi = f32x2v_t{v[2], v[3]} * mul;
+    return make_uint2(__builtin_bit_cast(uint32_t, __builtin_convertvector(lo, bf16x2v_t)),
+                      __builtin_bit_cast(uint32_t, __builtin_convertvector(hi, bf16x2v_t)));
+}
 __device__ __forceinline__ void store4(bf16_t* dst, f32x4_t v, float mul) {
-    *reinterpret_cast<uint2*>(dst) =
-        make_uint2(pack_bf16x2(v[0] * mul, v[1] * mul), pack_bf16x2(v[2] * mul, v[3] * mul));
+    *reinterpret_cast<uint2*>(dst) = pack4_bf16(v, mul);
 }
 
 // raw buffer loads: offsets past num_records (bytes) return 0, so zero-padded rows need no branch
@@ -406,9 +416,8 @@ __global__ __launch_bounds__(256, (fwd_occ<HS, NKT>())) void attn_fwd_k(bf16_t* 
             const uint32_t off = (uint32_t)q * (uint32_t)(C * 2) + 8u * g;
 #pragma unroll
             for (int dt = 0; dt < G::DT; dt++) {
-                const uint2 v = make_uint2(pack_bf16x2(o[dt][0] * inv, o[dt][1] * inv),
-                                           pack_bf16x2(o[dt][2] * inv, o[dt][3] * inv));
-                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, v), ro, off + 32u * dt, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, pack4_bf16(o[dt], inv)), ro,
+                                                      off + 32u * dt, 0, 0);
             }
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, mx + log2f(l)), rl, 4u * q, 0, 0);
         } else if (q < T) {
