@@ -43,6 +43,15 @@ def test_checker_follows_back_edges():
     assert len(v) == 1 and "v_mov" in v[0][1]
 
 
+def test_checker_flags_fma_in_colsum_epilogue():
+    dis = "0000000000001000 <_ZN3vit2g213gemm_kernel_sILi9ELb0EEEvNS_10GemmParamsE>:\n" + \
+        _ins(0x1000, "v_pk_fma_f32 v[4:5], v[0:1], v[2:3], v[4:5]") + _ins(0x1008, "s_endpgm") + \
+        "0000000000002000 <_ZN3vit2g213gemm_kernel_sILi8ELb0EEEvNS_10GemmParamsE>:\n" + \
+        _ins(0x2000, "v_fma_f32 v4, v0, v2, v4") + _ins(0x2008, "s_endpgm")
+    v = check_asm.colsum_fma_violations(dis)
+    assert v == [("_ZN3vit2g213gemm_kernel_sILi9ELb0EEEvNS_10GemmParamsE", 1)]
+
+
 def test_built_code_objects_have_no_early_asm_read_use():
     objs = sorted(glob.glob(os.path.join(ROOT, "vit.rs_amd", "build", "*.o")))
     if not objs or not os.path.exists(os.path.join(check_asm.LLVM, "llvm-objdump")):

@@ -4,6 +4,8 @@ fp32 ops: <= 1e-4 relative to the oracle's fp32 result (max-normalised), the par
 BASELINE.json.  bf16 ops: compared with the fp64 oracle run on the bf16-ROUNDED inputs, so only
 accumulation order / output rounding differ; tolerance 1e-2 (bf16 output rounding is 2^-9).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -356,12 +358,17 @@ def test_error_channel(gpu):
 
 
 # ------------------------------------------------------------------ generic bf16 GEMM engine
-@pytest.fixture(params=[2, 4, 5, 7, 9, 10])
+# The engines the trainer launches (2 = 256x256 one workgroup per CU, with the split-K weight gradients
+# on 256x128; 7 = persistent streaming 256x256, the production default).  The variants that measured
+# slower (4 = 256x128 everywhere, 5 = its software-pipelined form, 9 = one wave per SIMD, 10 = split
+# tail) run only with VIT_TEST_EXPERIMENTAL=1 against a `make EXPERIMENTAL=1` library.
+EXPERIMENTAL = os.environ.get("VIT_TEST_EXPERIMENTAL") == "1"
+ENGINES = [2, 7] + ([4, 5, 9, 10] if EXPERIMENTAL else [])
+
+
+@pytest.fixture(params=ENGINES)
 def engine(request, gpu):
-    """Run a test under each production GEMM engine (2 = 256x256 one workgroup per CU, with the split-K
-    weight gradients on 256x128; 4 = 256x128 two per CU everywhere; 5 = as 4 with the
-    software-pipelined main loop for K-contiguous operands; 7 = persistent streaming 256x256, 9 = its
-    one-wave-per-SIMD 128x128-per-wave form, 10 = 7 with the split tail round), then restore the default."""
+    """Run a test under each GEMM engine of ENGINES, then restore the default."""
     gpu.lib().gemm_bf16_set_variant(request.param)
     yield request.param
     gpu.lib().gemm_bf16_set_variant(0)
@@ -430,7 +437,7 @@ def test_gemm_bf16_tile_order_bit_identical(gpu, M, N, K, gm):
         assert np.array_equal(x, y)
 
 
-@pytest.mark.parametrize("pair", [(4, 5), (2, 7), (2, 9)])
+@pytest.mark.parametrize("pair", [(2, 7)] + ([(4, 5), (2, 9)] if EXPERIMENTAL else []))
 @pytest.mark.parametrize("M,N,K", [(6304, 3072, 768), (1576, 768, 3072), (520, 384, 256), (776, 1000, 128),
                                    (50432, 768, 768)])
 def test_gemm_bf16_pipelined_bit_identical(gpu, M, N, K, pair):
@@ -476,6 +483,7 @@ def test_gemm_bf16_pipelined_bit_identical(gpu, M, N, K, pair):
 
 @pytest.mark.parametrize("M,N,K", [(50432, 768, 768), (50432, 768, 3072), (25216, 768, 3072), (25216, 768, 2304),
                                    (2056, 768, 320), (1000, 520, 128)])
+@pytest.mark.skipif(not EXPERIMENTAL, reason="variant 10 is built with make EXPERIMENTAL=1 only")
 def test_gemm_bf16_tail_split(gpu, M, N, K):
     """Variant 10: the persistent engine with the last, partly filled round's tiles split along K
     (fp32 partial tiles + gemm_tail_fix_k) against variant 7 on the same inputs, at the trainer's

@@ -12,6 +12,12 @@ the read would use stale data.  This scans every kernel's disassembly in program
 A read is retired by `s_waitcnt lgkmcnt(N)` once at least N younger LDS instructions (ds_*) were
 issued after it (LDS operations complete in order), or by lgkmcnt(0).
 
+Second rule (engine bit-identity): the x-aux epilogue with column sums
+(EPI_BF16_MUL = 9, the fcproj dgrad) must round its products before summing them in every GEMM
+engine, so no kernel instantiated for it may contain a float FMA (gemm_common.h pins
+`#pragma clang fp contract(off)` there; hipcc contracted `v *= aux; cs += v` in some engines and
+not in others, and their column sums then differed in the last bits).
+
     python tools/check_asm.py [objects...]        exit status 1 on a violation
 """
 import glob
@@ -140,6 +146,21 @@ def check_text(dis):
     return kernels, violations
 
 
+FMA_OP = re.compile(r"v_(pk_)?fmac?_f32|v_fma_mix|v_mad_f32|v_mac_f32|v_fma_f16")
+EPI_MUL = re.compile(r"(I|E)Li9E")  # template argument EPI = 9 in the mangled kernel name
+
+
+def colsum_fma_violations(dis):
+    """-> [(kernel, count)] of EPI 9 GEMM kernels that contain float FMAs"""
+    out = []
+    for fn, ins in parse(dis).items():
+        if "gemm" in fn and EPI_MUL.search(fn):
+            n = sum(1 for _, op, _ in ins if FMA_OP.match(op))
+            if n:
+                out.append((fn, n))
+    return out
+
+
 def main(objs):
     objs = objs or sorted(glob.glob(os.path.join(ROOT, "vit.rs_amd", "build", "*.o")))
     total_k, total_v = 0, []
@@ -152,6 +173,8 @@ def main(objs):
             k, v = check_text(dis)
             total_k += len(k)
             total_v += [(os.path.basename(o),) + x for x in v]
+            total_v += [(os.path.basename(o), fn, f"{n} float FMA(s) in an EPI 9 (x aux + column sums) kernel")
+                        for fn, n in colsum_fma_violations(dis)]
     for o, fn, msg in total_v[:50]:
         print(f"{o}: {fn}: {msg}")
     print(f"{total_k} kernels with asm transposed LDS reads checked, {len(total_v)} violation(s)")

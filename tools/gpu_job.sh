@@ -13,7 +13,7 @@
 #   profile TAG           tools/profile.sh TAG (bench + rocprofv3 stats + PMC passes)
 #   ktrace TAG [bench args]  rocprofv3 --kernel-trace --stats of one bench.py run -> gpurun_out/TAG/
 #   py SCRIPT [args]      python3 SCRIPT args (any tool under tools/)
-set -u
+set -u -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp

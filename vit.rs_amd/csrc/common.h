@@ -60,8 +60,13 @@ void count_hit(int kind);  // VIT_HIT_* (include/vit_ops.h)
 // ---------------------------------------------------------------- device helpers
 __device__ __forceinline__ float bf2f(bf16_t h) { return __uint_as_float((uint32_t)h << 16); }
 __device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+// one float2 -> bf16x2 conversion (v_cvt_pk_bf16_f32 a, b; RNE like f2bf).  The scalar form
+// "f2bf(a) | f2bf(b) << 16" let hipcc pair the conversions of neighbouring calls its own way and
+// then spend an and, a shift and an or_sdwa per pack putting the halves back
 __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
-    return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+    typedef float f2_t __attribute__((ext_vector_type(2)));
+    typedef __bf16 b2_t __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f2_t{a, b}, b2_t));
 }
 
 // "bf16 + lo8": a value t kept as hi = bf16(t) plus one signed byte q = rint((t - hi) / (ulp(hi) / 256)),

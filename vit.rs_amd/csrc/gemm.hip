@@ -1278,7 +1278,13 @@ __global__ __launch_bounds__(256) void slab_reduce_k(float* __restrict__ C, long
 //   epilogues (main-loop-only timing; results are garbage).
 static int g_variant = -1;
 static int g_debug_flags = 0;
+// variants 5 (software-pipelined 256x128), 9 (one wave per SIMD, gemm_w4.hip) and 10 (split tail) measured
+// slower than 7 and are built only with `make EXPERIMENTAL=1`
+#if VIT_GEMM_EXPERIMENTAL
 static bool known_variant(int v) { return v == 1 || v == 2 || v == 4 || v == 5 || v == 7 || v == 9 || v == 10; }
+#else
+static bool known_variant(int v) { return v == 1 || v == 2 || v == 4 || v == 7; }
+#endif
 static constexpr int kDefaultVariant = 7;
 static int gemm_variant() {
     if (g_variant < 0) {
@@ -1452,12 +1458,13 @@ static void launch_bf16(const GemmArgs& a, const GemmParams& p, dim3 grid, hipSt
 template <bool AK, bool BKC>
 static void launch_g2(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStream_t s) {
     if constexpr (AK && BKC) {
+#if VIT_GEMM_EXPERIMENTAL
         // one-wave-per-SIMD persistent engine (gemm_w4.hip)
         if (gemm_variant() == 9 && grid.y == 1 && gemm_bf16_w4(a, p, (int)grid.x, s)) return;
         // persistent streaming engine with a split tail (variant 10): when the last round fills at
         // most half the CUs, its tiles run as K-ranges on all of them (bias / residual / bf16 store
         // epilogues; fp32 partial tiles in a.tail_ws or the thread workspace + gemm_tail_fix_k)
-        if (gemm_variant() == 10 && grid.y == 1 && p.K >= 2 * g2::BK && p.kchunk == p.K &&
+        if (gemm_variant() == 10 && a.tail_ws && grid.y == 1 && p.K >= 2 * g2::BK && p.kchunk == p.K &&
             (a.epi == EPI_F32_STORE || a.epi == EPI_BF16_STORE || a.epi == EPI_F32_RESID) &&
             (long long)p.M * p.lda * 2 < (1LL << 31) && (long long)p.N * p.ldb * 2 < (1LL << 31)) {
             const int cus = gemm_cu_count(), tiles = (int)grid.x;
@@ -1468,7 +1475,8 @@ static void launch_g2(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStre
                 const int kchunk = cdiv(cdiv(p.K, split), 2 * g2::BK) * (2 * g2::BK);  // even step count
                 split = cdiv(p.K, kchunk);
                 const size_t need = (size_t)tail * split * g2::BM * g2::BN * sizeof(float);
-                float* part = a.tail_ws ? (a.tail_ws_bytes >= need ? a.tail_ws : nullptr) : (float*)workspace(need);
+                // the caller's per-stream buffer only: the thread workspace is shared by concurrent streams
+                float* part = a.tail_ws_bytes >= need ? a.tail_ws : nullptr;
                 if (split >= 2 && part) {
                     GemmParams q = p;
                     q.tsplit = split;
@@ -1490,6 +1498,7 @@ static void launch_g2(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStre
                 }
             }
         }
+#endif
         // persistent streaming engine: one workgroup per CU (at most one per tile), no split-K;
         // its DMA ring runs two K-steps ahead across one tile boundary, so K >= 2 steps
         if ((gemm_variant() == 7 || gemm_variant() == 10) && grid.y == 1 && p.K >= 2 * g2::BK &&
@@ -1537,6 +1546,7 @@ static void launch_g4(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStre
         // software-pipelined main loop: an even step count per split and 32-bit DMA offsets
         const bool fits = p.kchunk % 64 == 0 && p.K % 64 == 0 && (long long)p.M * p.lda * 2 < (1LL << 32) &&
                           (long long)p.N * p.ldb * 2 < (1LL << 32);
+#if VIT_GEMM_EXPERIMENTAL
         if (gemm_variant() == 5 && fits) {
             switch (a.epi) {
 #define VIT_CASE(E) \
@@ -1554,6 +1564,9 @@ static void launch_g4(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStre
                 default: break;
             }
         }
+#else
+        (void)fits;
+#endif
     }
     switch (a.epi) {
 #define VIT_CASE(E) \

@@ -213,6 +213,7 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, int m, int n, f32x
         *reinterpret_cast<uint2*>((bf16_t*)p.C + off) = make_uint2(pack_bf16x2(d[0], d[1]), pack_bf16x2(d[2], d[3]));
         *reinterpret_cast<uint2*>((bf16_t*)p.C2 + off) = make_uint2(pack_bf16x2(g[0], g[1]), pack_bf16x2(g[2], g[3]));
     } else if constexpr (epi_aux16(EPI)) {
+#pragma clang fp contract(off)  // the products are rounded before the callers' column sums
         const uint2 h = *reinterpret_cast<const uint2*>((const bf16_t*)p.aux +
                                                         (long long)m * p.ldaux + n);
         const float x0 = __uint_as_float(h.x << 16), x1 = __uint_as_float(h.x & 0xffff0000u);
@@ -297,6 +298,8 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, flo
     } else if constexpr (epi_aux16(EPI)) {
         const uint4 h = *reinterpret_cast<const uint4*>((const bf16_t*)p.aux + (long long)m * p.ldaux + n);
         const uint32_t hw[4] = {h.x, h.y, h.z, h.w};
+        {  // products rounded before the column sums (no FMA contraction; see the staged epilogue)
+#pragma clang fp contract(off)
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const float lo = __uint_as_float(hw[j] << 16), hi = __uint_as_float(hw[j] & 0xffff0000u);
@@ -310,6 +313,7 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, flo
         }
 #pragma unroll
         for (int j = 0; j < 8; j++) cs[j] += v[j];
+        }
         const uint4 d8 = pack8(v);
         if (p.C) *reinterpret_cast<uint4*>((bf16_t*)p.C + off) = d8;
         if constexpr (MX) {
@@ -431,6 +435,10 @@ __device__ __forceinline__ void staged_pass_interior(const GemmParams& p, const 
             if (p.mx_q) mx_out8(p, mrow + r, n, g8[0], g8[1], g8[2], g8[3], cc_lane);
             if (p.mxc_q) stage_back8(const_cast<float*>(st) + r * STG_LD + cc, g8[0], g8[1], g8[2], g8[3]);
         } else if constexpr (AUX16) {
+            // the products are rounded before the column sums in every engine: no contraction of
+            // v *= aux; cs += v into an FMA (hipcc decided that per kernel, so two engines with the same
+            // arithmetic could differ in the sums' last bits)
+#pragma clang fp contract(off)
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const float lo = __uint_as_float(ax[it][j] << 16), hi = __uint_as_float(ax[it][j] & 0xffff0000u);
@@ -482,6 +490,7 @@ __device__ __forceinline__ void staged_pass(const GemmParams& p, const float* st
             f32x4_t t = lo;
             epilogue<EPI>(p, m, n, t);
             if constexpr (epi_aux16(EPI)) {  // the 4-wide form does not sum: the output it stored
+#pragma clang fp contract(off)
                 cs[0] += t[0];
                 cs[1] += t[1];
                 cs[2] += t[2];
@@ -735,6 +744,8 @@ __device__ __forceinline__ void staged_pass_interior_q(const GemmParams& p, floa
                 if (p.mxc_q) stage_back8_q(st, r, cc, g8[0], g8[1], g8[2], g8[3]);
             }
         } else if constexpr (AUX16) {
+            {  // products rounded before the column sums (no FMA contraction)
+#pragma clang fp contract(off)
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const float a0 = __uint_as_float(aux.ax[it][j] << 16), a1 = __uint_as_float(aux.ax[it][j] & 0xffff0000u);
@@ -748,6 +759,7 @@ __device__ __forceinline__ void staged_pass_interior_q(const GemmParams& p, floa
             }
 #pragma unroll
             for (int j = 0; j < 8; j++) cs[j] += v[j];
+            }
             const u32x4 d8 = pack8(v);
             if (p.C) epi_st16(p, (bf16_t*)p.C + off, d8);
             if constexpr (MX) {
@@ -826,6 +838,7 @@ __device__ __forceinline__ void staged_epilogue_q_any(const GemmParams& p, Stage
                     f32x4_t t = lo;
                     epilogue<EPI>(p, m, n, t);
                     if constexpr (epi_aux16(EPI)) {
+#pragma clang fp contract(off)
                         cs[0] += t[0]; cs[1] += t[1]; cs[2] += t[2]; cs[3] += t[3];
                     }
                 }
