@@ -60,6 +60,7 @@ enum {
     VIT_HIT_ATTN_GENERIC = 85,       /* generic VALU attention (T past the MFMA kernels' LDS) */
     VIT_HIT_ATTN_BWD_XKEY = 86,      /* one-pass backward + the last key's side path (T = 32k + 1) */
     VIT_HIT_QUANT_ROWCOL = 87,       /* fused row + column MX quantization */
+    VIT_HIT_GEMM_PP = 88,            /* bf16 two-group ping-pong 192x256 engine (variant 11; also counted as 256x256 + epi) */
     VIT_HIT_COUNT = 96
 };
 int vit_kernel_hits(long long* out, int n); /* copies min(n, VIT_HIT_COUNT); returns VIT_HIT_COUNT */

@@ -359,11 +359,11 @@ def test_error_channel(gpu):
 
 # ------------------------------------------------------------------ generic bf16 GEMM engine
 # The engines the trainer launches (2 = 256x256 one workgroup per CU, with the split-K weight gradients
-# on 256x128; 7 = persistent streaming 256x256, the production default).  The variants that measured
+# on 256x128; 7 = persistent streaming 256x256; 11 = 7 with the two-group ping-pong 192x256 engine).  The variants that measured
 # slower (4 = 256x128 everywhere, 5 = its software-pipelined form, 9 = one wave per SIMD, 10 = split
 # tail) run only with VIT_TEST_EXPERIMENTAL=1 against a `make EXPERIMENTAL=1` library.
 EXPERIMENTAL = os.environ.get("VIT_TEST_EXPERIMENTAL") == "1"
-ENGINES = [2, 7] + ([4, 5, 9, 10] if EXPERIMENTAL else [])
+ENGINES = [2, 7, 11] + ([4, 5, 9, 10] if EXPERIMENTAL else [])
 
 
 @pytest.fixture(params=ENGINES)
@@ -437,9 +437,9 @@ def test_gemm_bf16_tile_order_bit_identical(gpu, M, N, K, gm):
         assert np.array_equal(x, y)
 
 
-@pytest.mark.parametrize("pair", [(2, 7)] + ([(4, 5), (2, 9)] if EXPERIMENTAL else []))
+@pytest.mark.parametrize("pair", [(2, 7), (7, 11)] + ([(4, 5), (2, 9)] if EXPERIMENTAL else []))
 @pytest.mark.parametrize("M,N,K", [(6304, 3072, 768), (1576, 768, 3072), (520, 384, 256), (776, 1000, 128),
-                                   (50432, 768, 768)])
+                                   (50432, 768, 768), (25216, 3072, 768), (25216, 768, 3072), (25216, 768, 2304)])
 def test_gemm_bf16_pipelined_bit_identical(gpu, M, N, K, pair):
     """Engine variants that reorder only the schedule, not the arithmetic: the software-pipelined
     256x128 main loop (variant 5, g4::gemm_kernel_pipe) against the 256x128 engine (4), and the
@@ -451,6 +451,8 @@ def test_gemm_bf16_pipelined_bit_identical(gpu, M, N, K, pair):
     bit-identical, at the trainer's K (768, 3072), its M (50 432 = 197 full 256-row tiles: several
     tiles per CU) and ragged M / N."""
     v0, v1 = pair
+    if (v0, v1) == (2, 7) and M >= 25216 and K > 768:
+        pytest.skip("covered by the (2, 7) shapes above")
     v = gpu
     L = v.lib()
     rng = np.random.default_rng(M + 3 * N + K)
@@ -461,9 +463,11 @@ def test_gemm_bf16_pipelined_bit_identical(gpu, M, N, K, pair):
     res = D(v, rng.normal(size=(M, N)).astype(np.float32))
     aux = D(v, v.bf16_bits(rng.normal(size=(M, N)).astype(np.float32)), np.uint16)
     outs = {}
+    pp_hits = 0
     try:
         for var in (v0, v1):
             L.gemm_bf16_set_variant(var)
+            v.kernel_hits_reset()
             o = {}
             for epi in (3, 5, 8, 9):
                 c = Z(v, M * N, np.float32 if epi == 5 else np.uint16)
@@ -473,12 +477,21 @@ def test_gemm_bf16_pipelined_bit_identical(gpu, M, N, K, pair):
                        A, K, 1, W, K, 1, bias if epi in (3, 5, 8) else None, cs, M, N, K, epi)
                 o[epi] = [c.numpy()] + ([c2.numpy()] if c2 is not None else []) + ([cs.numpy()] if cs is not None else [])
             outs[var] = o
+            if var == 11:
+                pp_hits = int(v.kernel_hits()[v.HIT_GEMM_PP])
     finally:
         L.gemm_bf16_set_variant(0)
     for epi in outs[v0]:
-        for x, y in zip(outs[v0][epi], outs[v1][epi]):
-            assert np.array_equal(x, y), epi
+        for k, (x, y) in enumerate(zip(outs[v0][epi], outs[v1][epi])):
+            if v1 == 11 and epi == 9 and k == 1:
+                # the ping-pong engine sums columns per 96 output rows (128 elsewhere): the fp32 sums
+                # differ in association only
+                assert np.abs(x - y).max() <= 1e-5 * np.abs(x).max(), epi
+            else:
+                assert np.array_equal(x, y), epi
     assert np.abs(outs[v1][5][0]).max() > 0
+    if v1 == 11:  # the engine ran where it applies (N % 256 == 0, M >= 256, K >= 256)
+        assert pp_hits == (4 if (N % 256 == 0 and M >= 256 and K >= 256) else 0), pp_hits
 
 
 @pytest.mark.parametrize("M,N,K", [(50432, 768, 768), (50432, 768, 3072), (25216, 768, 3072), (25216, 768, 2304),

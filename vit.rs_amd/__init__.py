@@ -195,6 +195,7 @@ HIT_GEMM_128, HIT_GEMM_256x256, HIT_GEMM_256x128, HIT_GEMM_FP8, HIT_GEMM_F32 = 0
 HIT_SPLITK_REDUCE, HIT_ATTN_FWD_MFMA, HIT_ATTN_BWD_PERSISTENT = 80, 81, 82
 HIT_ATTN_BWD_ONEPASS, HIT_ATTN_BWD_PAIR, HIT_ATTN_GENERIC = 83, 84, 85
 HIT_ATTN_BWD_XKEY, HIT_QUANT_ROWCOL = 86, 87
+HIT_GEMM_PP = 88
 
 
 def kernel_hits():

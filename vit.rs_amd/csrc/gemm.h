@@ -48,8 +48,9 @@ struct GemmArgs {
     const float* bias = nullptr;
     float* dbias = nullptr;  // bf16 wgrad with an M-contig A: dbias[m] += sum_k A(m,k) (fused colsum)
     // EPI_BF16_DGELU / EPI_BF16_MUL column sums of the output, deterministic: the epilogue stores
-    // partial rows colsum_part[cdiv(M,128)][N] (row r = output rows 128r..128r+127; nullptr = thread
-    // workspace) and, with colsum_out set, the launcher adds them into colsum_out in a fixed order.
+    // partial rows colsum_part[gemm_colsum_rows(a)][N] (row r = output rows 128r..128r+127, 96r.. on the
+    // ping-pong engine; nullptr = thread workspace) and, with colsum_out set, the launcher adds them
+    // into colsum_out in a fixed order.
     // colsum_part without colsum_out: the caller reduces the rows (the trainer, across micro-batches).
     float* colsum_out = nullptr;
     float* colsum_part = nullptr;
@@ -107,6 +108,13 @@ struct GemmParams;
 // split-K (K % 64 == 0, K >= 128); false = shape not taken
 bool gemm_bf16_w4(const GemmArgs& a, const GemmParams& p, int tiles, hipStream_t s);
 void gemm_set_trace(unsigned long long* trace);
+// variant 11: the two-group ping-pong engine (gemm_pp.hip, 192x256 tiles) for the shapes it takes
+bool gemm_pp_shape(const GemmArgs& a);
+void gemm_bf16_pp(const GemmArgs& a, const GemmParams& p, hipStream_t s);
+// the number of column-sum partial rows gemm_bf16 (fp8 = false) or gemm_fp8 (true) writes for an
+// x-aux epilogue of these arguments (GemmArgs::colsum_part): cdiv(M, 96) on the ping-pong engine,
+// cdiv(M, 128) on every other engine
+int gemm_colsum_rows(const GemmArgs& a, bool fp8);
 bool gemm_streaming();  // the production variant: persistent streaming engines (bf16 and fp8)
 
 // fp8 (OCP e4m3) operands with MX block scales (one E8M0 per 32 k-elements), fp32 accumulate

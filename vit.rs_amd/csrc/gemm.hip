@@ -1225,14 +1225,23 @@ static void colsum_any(float* dbias, const TX* X, int M, int N, long long ld, hi
     RowsJob j{dbias, ws, nch, N, N};
     rows_reduce_add(&j, 1, s);
 }
+static int gemm_variant();
+// the ping-pong engine (variant 11) takes this bf16 GEMM: the big-tile path of gemm_bf16 without
+// split-K, on a shape gemm_pp_shape accepts
+static bool pp_taken(const GemmArgs& a) {
+    return gemm_variant() == 11 && !a.a_scale && a.epi != EPI_F32_ATOMIC && gemm_bf16_supported(a) &&
+           a.K % g2::KTILE == 0 && a.M >= 256 && a.N >= 256 && gemm_pp_shape(a);
+}
+int gemm_colsum_rows(const GemmArgs& a, bool fp8) { return cdiv(a.M, !fp8 && pp_taken(a) ? 96 : 128); }
 float* colsum_rows_begin(const GemmArgs& a) {
     if (!epi_aux16(a.epi) || !(a.colsum_out || a.colsum_part)) return nullptr;
-    float* r = a.colsum_part ? a.colsum_part : (float*)workspace((size_t)cdiv(a.M, 128) * a.N * sizeof(float));
+    float* r = a.colsum_part ? a.colsum_part
+                             : (float*)workspace((size_t)gemm_colsum_rows(a, a.a_scale != nullptr) * a.N * sizeof(float));
     return r;
 }
 void colsum_rows_end(const GemmArgs& a, float* rows, hipStream_t s) {
     if (!rows || !a.colsum_out) return;
-    RowsJob j{a.colsum_out, rows, cdiv(a.M, 128), a.N, a.N};
+    RowsJob j{a.colsum_out, rows, gemm_colsum_rows(a, a.a_scale != nullptr), a.N, a.N};
     rows_reduce_add(&j, 1, s);
 }
 
@@ -1274,16 +1283,17 @@ __global__ __launch_bounds__(256) void slab_reduce_k(float* __restrict__ C, long
 //   workgroup; split-K weight gradients on 256x128), 4 = 256x128 two per CU everywhere, 5 = as 4
 //   with the software-pipelined main loop (g4::gemm_kernel_pipe) for K-contiguous operands,
 //   7 = production: as 2 with the persistent streaming 256x256 engine (g2::gemm_kernel_s) for the
-//   K-contiguous GEMMs without split-K.  Debug flag 2 skips the
+//   K-contiguous GEMMs without split-K, 11 = as 7 with the two-group ping-pong
+//   192x256 engine (gemm_pp.hip) for the shapes it takes.  Debug flag 2 skips the
 //   epilogues (main-loop-only timing; results are garbage).
 static int g_variant = -1;
 static int g_debug_flags = 0;
 // variants 5 (software-pipelined 256x128), 9 (one wave per SIMD, gemm_w4.hip) and 10 (split tail) measured
 // slower than 7 and are built only with `make EXPERIMENTAL=1`
 #if VIT_GEMM_EXPERIMENTAL
-static bool known_variant(int v) { return v == 1 || v == 2 || v == 4 || v == 5 || v == 7 || v == 9 || v == 10; }
+static bool known_variant(int v) { return v == 1 || v == 2 || v == 4 || v == 5 || v == 7 || v == 9 || v == 10 || v == 11; }
 #else
-static bool known_variant(int v) { return v == 1 || v == 2 || v == 4 || v == 7; }
+static bool known_variant(int v) { return v == 1 || v == 2 || v == 4 || v == 7 || v == 11; }
 #endif
 static constexpr int kDefaultVariant = 7;
 static int gemm_variant() {
@@ -1307,7 +1317,7 @@ int gemm_cu_count() {
     return n;
 }
 int gemm_variant_selected() { return gemm_variant(); }
-bool gemm_streaming() { return gemm_variant() == 7 || gemm_variant() == 9 || gemm_variant() == 10; }
+bool gemm_streaming() { return gemm_variant() == 7 || gemm_variant() == 9 || gemm_variant() == 10 || gemm_variant() == 11; }
 void gemm_set_debug(int flags) { g_debug_flags = flags; }
 static unsigned long long* g_trace = nullptr;
 void gemm_set_trace(unsigned long long* trace) { g_trace = trace; }
@@ -1501,7 +1511,7 @@ static void launch_g2(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStre
 #endif
         // persistent streaming engine: one workgroup per CU (at most one per tile), no split-K;
         // its DMA ring runs two K-steps ahead across one tile boundary, so K >= 2 steps
-        if ((gemm_variant() == 7 || gemm_variant() == 10) && grid.y == 1 && p.K >= 2 * g2::BK &&
+        if ((gemm_variant() == 7 || gemm_variant() == 10 || gemm_variant() == 11) && grid.y == 1 && p.K >= 2 * g2::BK &&
             (long long)p.M * p.lda * 2 < (1LL << 31) &&
             (long long)p.N * p.ldb * 2 < (1LL << 31)) {
             const int cus = gemm_cu_count();
@@ -1658,7 +1668,8 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s) {
     // split-K weight gradients (M/N-contiguous operands, K = the token count) run on the 256x128
     // two-per-CU engine: 3-9 % faster than 256x256 on every ViT-B/16 wgrad shape (r02,
     // tools/bench_gemm.py), the other GEMMs are faster on 256x256
-    if ((gemm_variant() == 2 || gemm_variant() == 7 || gemm_variant() == 9 || gemm_variant() == 10) && a.epi == EPI_F32_ATOMIC && !a.a_kcontig && !a.b_kcontig &&
+    if ((gemm_variant() == 2 || gemm_variant() == 7 || gemm_variant() == 9 || gemm_variant() == 10 || gemm_variant() == 11) &&
+        a.epi == EPI_F32_ATOMIC && !a.a_kcontig && !a.b_kcontig &&
         a.K % g4::KTILE == 0 && a.M >= 256 && a.N >= 128 && a.N % 4 == 0 &&
         (a.splitk > 0 || !a.ws ||
          (size_t)choose_split_g4(cdiv(a.M, g4::BM) * cdiv(a.N, g4::BN), a.K / g4::KTILE) * a.M * a.N * sizeof(float) <=
@@ -1693,6 +1704,14 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s) {
         // fused bias gradient: one add per (column block, K-split), deterministic with one split
         const bool late_db = a.dbias && !a.a_kcontig && split > 1;
         if (late_db) p.dbias = nullptr;
+        if (split == 1 && pp_taken(b)) {  // variant 11: the ping-pong engine (gemm_pp.hip)
+            gemm_bf16_pp(b, p, s);
+            after_launch("gemm_bf16_pp");
+            count_hit(VIT_HIT_GEMM_256x256 + b.epi);
+            count_hit(VIT_HIT_GEMM_PP);
+            colsum_rows_end(a, cs_rows, s);
+            return;
+        }
         dim3 grid(tiles, split);
         if (a.a_kcontig && a.b_kcontig) launch_g2<true, true>(b, p, grid, s);
         else if (a.a_kcontig && !a.b_kcontig) launch_g2<true, false>(b, p, grid, s);

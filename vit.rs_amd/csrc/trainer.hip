@@ -318,6 +318,7 @@ struct Trainer {
     float* red_ws = nullptr;
     float* sg_part[2]{};
     long long sg_ln2 = 0, sg_ln1 = 0, sg_fcb = 0, sg_qkv = 0;  // offsets (floats) in sg_part[p]
+    int fcb_rows = 0;  // fc-bias column-sum partial rows per micro-batch (gemm_colsum_rows of the fcproj dgrad)
     bf16_t* dln_bf = nullptr;  // bf16 mode: LN-output gradient from the fc / qkv dgrad GEMMs
     bf16_t *dres_bf = nullptr, *dres_bf2 = nullptr, *dfch = nullptr, *datty = nullptr, *dqkv = nullptr, *dpatch_bf = nullptr;
     float* dpatch_f = nullptr;
@@ -670,7 +671,7 @@ struct Trainer {
             gemm_ws = alloc<float>((long long)(gemm_ws_bytes / sizeof(float)));
             attn_part = alloc<float>((long long)attn_backward_ws_floats(B, T, C, NH) + MAXMB * 3LL * C);  // bias partials | delta
             {  // per-layer small-gradient partial rows for up to MAXMB micro-batches
-                const long long lnr = (long long)MAXMB * ln_bwd_blocks(BT), fcr = cdiv(BT, 128) + MAXMB;
+                const long long lnr = (long long)MAXMB * ln_bwd_blocks(BT), fcr = cdiv(BT, 96) + MAXMB;  // (96: ping-pong engine)
                 sg_ln2 = 0;
                 sg_ln1 = sg_ln2 + lnr * 3 * C;
                 sg_fcb = sg_ln1 + lnr * 3 * C;
@@ -1101,7 +1102,7 @@ struct Trainer {
             {G(P_ATTPROJB, l), p2 + 2 * C, nb, 3 * C, C},
             {G(P_LN1W, l), p1, nb, w1, C},
             {G(P_LN1B, l), p1 + C, nb, w1, C},
-            {G(P_FCB, l), sg_rows(l, sg_fcb), nmb * cdiv(R, 128), 4 * C, 4 * C},
+            {G(P_FCB, l), sg_rows(l, sg_fcb), nmb * fcb_rows, 4 * C, 4 * C},
             {G(P_QKVB, l), sg_rows(l, sg_qkv), nmb, 3 * C, 3 * C},
             {l > 0 ? G(P_FCPROJB, l - 1) : nullptr, p1 + 2 * C, nb, w1, C},
         };
@@ -1148,7 +1149,8 @@ struct Trainer {
                 d1.A = rbA + r0 * C; d1.lda = C; dgrad_b(d1, P_FCPROJW, l, C, 4 * C);
                 d1.C = dfch + r0 * 4 * C; d1.ldc = 4 * C; d1.aux = a.fchd + r0 * 4 * C; d1.ldaux = 4 * C;
                 d1.M = (int)R; d1.N = 4 * C; d1.K = C; d1.epi = EPI_BF16_MUL;
-                d1.colsum_part = sg_rows(l, sg_fcb) + (long long)mb * cdiv(R, 128) * 4 * C;
+                fcb_rows = gemm_colsum_rows(d1, fp8());  // partial rows per micro-batch (engine-dependent)
+                d1.colsum_part = sg_rows(l, sg_fcb) + (long long)mb * fcb_rows * 4 * C;
                 if (ec) {  // dfch only as its row (mx_out) and column MX forms
                     d1.C = nullptr;
                     d1.mxc_q = dfchc.q; d1.mxc_s = dfchc.s; d1.mxc_ld = kp_tok; d1.mxc_off = r0;
