@@ -467,6 +467,7 @@ def test_gemm_bf16_pipelined_bit_identical(gpu, M, N, K, pair):
     try:
         for var in (v0, v1):
             L.gemm_bf16_set_variant(var)
+            L.gemm_bf16_set_debug(512 if var == 11 else 0)  # variant 11 on every shape it can take
             v.kernel_hits_reset()
             o = {}
             for epi in (3, 5, 8, 9):
@@ -480,6 +481,7 @@ def test_gemm_bf16_pipelined_bit_identical(gpu, M, N, K, pair):
             if var == 11:
                 pp_hits = int(v.kernel_hits()[v.HIT_GEMM_PP])
     finally:
+        L.gemm_bf16_set_debug(0)
         L.gemm_bf16_set_variant(0)
     for epi in outs[v0]:
         for k, (x, y) in enumerate(zip(outs[v0][epi], outs[v1][epi])):

@@ -1226,11 +1226,20 @@ static void colsum_any(float* dbias, const TX* X, int M, int N, long long ld, hi
     rows_reduce_add(&j, 1, s);
 }
 static int gemm_variant();
+// debug flag 512: variant 11 takes every shape gemm_pp_shape accepts (A/B measurements, tests)
+static int g_debug_flags_fwd();
+static bool pp_all() { return (g_debug_flags_fwd() & 512) != 0; }
 // the ping-pong engine (variant 11) takes this bf16 GEMM: the big-tile path of gemm_bf16 without
 // split-K, on a shape gemm_pp_shape accepts
+// (the output width C GEMMs only, N <= 1280: proj / fcproj forward and every input gradient.  Measured
+// per GEMM at ViT-B/16 against the streaming engine (tools/bench_gemm.py --variants 7,11): those run
+// 4-15 % faster — their N = 768 grids quantize better in 192-row tiles and the fp32-residual epilogue
+// hides behind the next tile — while the K = 768 GEMMs with the heavy GELU-pair / x-aux epilogues and
+// N = 2304 / 3072 run 5-15 % slower: the epilogue group then cannot keep pace with one MFMA wave per
+// SIMD)
 static bool pp_taken(const GemmArgs& a) {
     return gemm_variant() == 11 && !a.a_scale && a.epi != EPI_F32_ATOMIC && gemm_bf16_supported(a) &&
-           a.K % g2::KTILE == 0 && a.M >= 256 && a.N >= 256 && gemm_pp_shape(a);
+           a.K % g2::KTILE == 0 && a.M >= 256 && a.N >= 256 && (a.N <= 1280 || pp_all()) && gemm_pp_shape(a);
 }
 int gemm_colsum_rows(const GemmArgs& a, bool fp8) { return cdiv(a.M, !fp8 && pp_taken(a) ? 96 : 128); }
 float* colsum_rows_begin(const GemmArgs& a) {
@@ -1319,6 +1328,7 @@ int gemm_cu_count() {
 int gemm_variant_selected() { return gemm_variant(); }
 bool gemm_streaming() { return gemm_variant() == 7 || gemm_variant() == 9 || gemm_variant() == 10 || gemm_variant() == 11; }
 void gemm_set_debug(int flags) { g_debug_flags = flags; }
+static int g_debug_flags_fwd() { return g_debug_flags; }
 static unsigned long long* g_trace = nullptr;
 void gemm_set_trace(unsigned long long* trace) { g_trace = trace; }
 

@@ -45,6 +45,9 @@ constexpr int ST_WAVE = 16 * ST_LD * 4;   // 8,448 B: one 16-row pass of a 96 x 
 constexpr int LDS_BYTES = NS * SLOT + 4 * ST_WAVE;
 constexpr int NCHUNK = 24;                // epilogue chunks per wave tile: 6 passes x 4 row groups
 static_assert(LDS_BYTES <= 160 * 1024, "LDS");
+#ifndef VIT_PP_EPRIO
+#define VIT_PP_EPRIO 0  // s_setprio of the epilogue group (the main group runs at 1)
+#endif
 #ifndef VIT_PP_NOEPI
 #define VIT_PP_NOEPI 0  // diagnostic compile: no epilogue code (register-pressure experiments)
 #endif
@@ -134,6 +137,12 @@ __device__ __forceinline__ uint32_t frag_off(int lane) {
 __device__ __forceinline__ bf16x8_t frag(const char* img, int r0, uint32_t fo) {
     return *reinterpret_cast<const bf16x8_t*>(img + fo + r0 * 64);
 }
+#if VIT_PP_TRACE
+// trace build, debug flag 128 (timing only, wrong results): every main-loop fragment read hits row 0
+#define FRAG(img, r0, fo) frag(img, (p.dbg & 128) ? 0 : (r0), (p.dbg & 128) ? 0u : (fo))
+#else
+#define FRAG(img, r0, fo) frag(img, r0, fo)
+#endif
 #if VIT_PP_TRACE
 // trace build, debug flag 128 (timing only, wrong results): every main-loop fragment read hits row 0
 #define FRAG(img, r0, fo) frag(img, (p.dbg & 128) ? 0 : (r0), (p.dbg & 128) ? 0u : (fo))
@@ -366,6 +375,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_pp(GemmParams p) {
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         stamp();
+#if VIT_PP_TRACE
+        if (!(p.dbg & 32))  // (trace build, debug flag 32: no barriers at all, timing only)
+#endif
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         stamp();
@@ -376,6 +388,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_pp(GemmParams p) {
     auto ebar = [&]() {
         __builtin_amdgcn_sched_barrier(0);
         stamp();
+#if VIT_PP_TRACE
+        if (!(p.dbg & 32))  // (trace build, debug flag 32: no barriers at all, timing only)
+#endif
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         stamp();
@@ -489,7 +504,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_pp(GemmParams p) {
             __builtin_amdgcn_sched_barrier(0);
         }
         // ------------------------------------------------- epilogue of tile jj (+ DMA for jj + 2)
-        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_setprio(VIT_PP_EPRIO);
         const int m0 = t.tm0 + wm * 96, n0 = t.tn0 + wn * 128;
         if (jj + 1 < my_tiles) {  // beside the other group's tile jj + 1
             if (!VIT_PP_NOEPI && !(p.no_epi & 1)) {
