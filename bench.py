@@ -402,6 +402,7 @@ def main():
                     "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1) if v["flops"] and v["ms"] else None}
                 for k, v in sorted(kern.items(), key=lambda kv: -kv[1]["ms"])}
         metric = METRIC
+        step_peak = PEAK_FP8_TFLOPS if args.dtype == "fp8" else PEAK_BF16_TFLOPS
         if args.model != "vit_b16" or args.dtype != "bf16":
             metric = (f"images/sec (train step) {MODEL_NAMES.get(cfg.name, cfg.name)} {cfg.img}² {args.dtype} "
                       f"on MI355X; % MFMA roofline")
@@ -414,8 +415,12 @@ def main():
             "config": {"workload": f"{cfg.name} {cfg.img}x{cfg.img} train step (fwd+bwd+SGD), batch {B}/GPU, {args.dtype}",
                        "model": cfg.name, "global_batch": b_global, "seq_len": cfg.T,
                        "parallelism": f"dp{world}"},
-            "mfma_roofline_frac_step": round(ips * gflop_img / world / (PEAK_BF16_TFLOPS * 1e3), 4),
-            "mfma_roofline_frac_step_peak_tflops": PEAK_BF16_TFLOPS,
+            # the step's algorithmic flops against the dense peak of its GEMM dtype (fp8 mode: the
+            # 5 PF fp8 peak, though attention and the weight gradients' reduce stay bf16 / fp32)
+            "mfma_roofline_frac_step": round(ips * gflop_img / world / (step_peak * 1e3), 4),
+            "mfma_roofline_frac_step_peak_tflops": step_peak,
+            **({"mfma_roofline_frac_step_vs_bf16_peak": round(ips * gflop_img / world / (PEAK_BF16_TFLOPS * 1e3), 4)}
+               if args.dtype == "fp8" else {}),
             "train_gflop_per_image": round(gflop_img, 3),
             "loss_after_warmup": round(loss_w, 4),
             "roofline": roof, "kernels": ksum,
