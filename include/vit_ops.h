@@ -61,6 +61,7 @@ enum {
     VIT_HIT_ATTN_BWD_XKEY = 86,      /* one-pass backward + the last key's side path (T = 32k + 1) */
     VIT_HIT_QUANT_ROWCOL = 87,       /* fused row + column MX quantization */
     VIT_HIT_GEMM_PP = 88,            /* bf16 two-group ping-pong 192x256 engine (variant 11; also counted as 256x256 + epi) */
+    VIT_HIT_LN_MX = 89,              /* LayerNorm forward straight into the row + column MX forms (fp8) */
     VIT_HIT_COUNT = 96
 };
 int vit_kernel_hits(long long* out, int n); /* copies min(n, VIT_HIT_COUNT); returns VIT_HIT_COUNT */
@@ -209,6 +210,13 @@ void quantize_mx_cols_bf16_ex(uint8_t* q, uint8_t* scales, const uint16_t* x, lo
 void quantize_mx_rowcol_bf16_ex(uint8_t* qr, uint8_t* scales_r, uint8_t* qc, uint8_t* scales_c,
                                 const uint16_t* x, long long R, int C, long long ldx, long long ldqc,
                                 long long tok_off, long long ntok);
+/* LayerNorm forward (train_vit.rs:453-480) straight into both MX forms: exactly
+ * layernorm_forward_bf16 (mean / rstd as it writes them) followed by quantize_mx_rowcol_bf16_ex of
+ * its bf16 output, without the bf16 tensor; inp [R][C] fp32, C a multiple of 256 in 256 .. 2048
+ * (not 1792). */
+void layernorm_forward_mx(uint8_t* qr, uint8_t* scales_r, uint8_t* qc, uint8_t* scales_c, float* mean,
+                          float* rstd, const float* inp, const float* weight, const float* bias, long long R,
+                          int C, long long ldqc, long long tok_off, long long ntok);
 void gemm_fp8_fused(void* C, void* C2, long long ldc, const void* aux, long long ldaux,
                     const uint8_t* A, const uint8_t* a_scale, long long lda, const uint8_t* B,
                     const uint8_t* b_scale, long long ldb, const float* bias, float* colsum_out,

@@ -328,6 +328,58 @@ def test_quantize_mx_rowcol_bit_exact(gpu, R, C, parts):
     assert np.array_equal(qc.numpy(), qc_ref.numpy()), "column bytes differ"
 
 
+@pytest.mark.parametrize("R,C,parts", [(100, 256, 1), (197, 768, 1), (2 * 257 * 16, 1280, 2), (1000, 1024, 2),
+                                        (3 * 1024 + 70, 512, 3), (300, 2048, 1), (4001, 1536, 1)])
+def test_layernorm_forward_mx_bit_exact(gpu, R, C, parts):
+    """LayerNorm straight into the MX forms (the fp8 trainer's ln1 / ln2) equals the unfused pair it
+    replaces byte for byte: layernorm_forward_bf16 (its mean / rstd bit for bit too) and then
+    quantize_mx_rowcol_bf16_ex of the bf16 output, per micro-batch slice (row form, row scales incl.
+    the padding rows' zero scales), the column form assembled from `parts` slices (padding tokens
+    of the last) against the same assembled by the unfused pair.  Inputs: rows of widely varying
+    scale and offset, some constant rows (rstd = 1/sqrt(eps)), weights with zeros (zero blocks:
+    scale byte 127)."""
+    v = gpu
+    rng = np.random.default_rng(R + C + 5 * parts)
+    x = (rng.normal(size=(R, C)) * np.exp2(rng.integers(-6, 6, size=(R, 1))) + rng.normal(size=(R, 1)) * 3).astype(np.float32)
+    x[rng.integers(0, R, size=3)] = 1.5
+    w = rng.normal(size=C).astype(np.float32)
+    w[rng.integers(0, C, size=C // 16)] = 0.0
+    w[:32] = 0.0
+    b = (rng.normal(size=C) * 0.1).astype(np.float32)
+    b[:32] = 0.0
+    kp = int(v.lib().mx_cols_padded(R))
+    nsc = int(v.lib().mx_scale_size(C, kp))
+    qc_ref, sc_ref = Z(v, C * kp, np.uint8), Z(v, nsc, np.uint8)
+    qc = D(v, np.full(C * kp, 0x5A, np.uint8), np.uint8)
+    sc = D(v, np.full(nsc, 0x5A, np.uint8), np.uint8)
+    wd, bd = D(v, w), D(v, b)
+    step = ((R + parts - 1) // parts + 63) // 64 * 64 if parts > 1 else R
+    bounds = [min(i * step, R) for i in range(parts)] + [R]
+    v.kernel_hits_reset()
+    for lo, hi in zip(bounds[:-1], bounds[1:]):
+        n = hi - lo
+        if n <= 0:
+            continue
+        ntok = kp - lo if hi == R else n
+        nsr = int(v.lib().mx_scale_size(n, C))
+        xs = D(v, x[lo:hi].copy())
+        ln_bf, mu_ref, rs_ref = Z(v, n * C, np.uint16), Z(v, n), Z(v, n)
+        v.call("layernorm_forward_bf16", ln_bf, mu_ref, rs_ref, xs, wd, bd, 1, n, C)
+        qr_ref, sr_ref = Z(v, n * C, np.uint8), Z(v, nsr, np.uint8)
+        v.call("quantize_mx_rowcol_bf16_ex", qr_ref, sr_ref, qc_ref, sc_ref, ln_bf, n, C, C, kp, lo, ntok)
+        qr = D(v, np.full(n * C, 0x5A, np.uint8), np.uint8)
+        sr = D(v, np.full(nsr, 0x5A, np.uint8), np.uint8)
+        mu = D(v, np.full(n, np.nan, np.float32))
+        rs = D(v, np.full(n, np.nan, np.float32))
+        v.call("layernorm_forward_mx", qr, sr, qc, sc, mu, rs, xs, wd, bd, n, C, kp, lo, ntok)
+        assert np.array_equal(mu.numpy(), mu_ref.numpy()) and np.array_equal(rs.numpy(), rs_ref.numpy()), lo
+        assert np.array_equal(sr.numpy(), sr_ref.numpy()), f"row scales differ at slice {lo}"
+        assert np.array_equal(qr.numpy(), qr_ref.numpy()), f"row bytes differ at slice {lo}"
+    assert np.array_equal(sc.numpy(), sc_ref.numpy()), "column scales differ"
+    assert np.array_equal(qc.numpy(), qc_ref.numpy()), "column bytes differ"
+    assert v.kernel_hits()[v.HIT_LN_MX] == sum(1 for lo, hi in zip(bounds[:-1], bounds[1:]) if hi > lo)
+
+
 @pytest.mark.parametrize("OC,Cin,R", [(256, 256, 64), (768, 320, 1000), (1280, 5120, 4112), (512, 768, 6000)])
 def test_gemm_fp8_wgrad_splitk(gpu, OC, Cin, R):
     """The fp8 weight gradient dW += dout^T . inp (epi 2) on column-quantized operands: one split

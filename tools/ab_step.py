@@ -2,7 +2,7 @@
 applied between steps and interleaved round by round; the median ms/step per config is printed.
     python tools/ab_step.py "gemm_debug=0|gemm_debug=4" [--rounds 4 --steps 3]
 A config is `key=value` pairs joined by `,`: trainer options (microbatch, dgrad_transposed),
-concurrency (0/1), gemm_variant, gemm_debug."""
+concurrency (0/1), gemm_variant, gemm_debug.  --dtype fp8 for the MXFP8 step (option fp8_ln_mx)."""
 import argparse
 import os
 import sys
@@ -21,11 +21,12 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--model", default="vit_b16")
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
     args = ap.parse_args()
     L = vit.lib()
     assert L.vit_init(0) == 0
     cfg = vit.data.CONFIGS[args.model]
-    m = vit.ViT(cfg, args.batch, vit.VIT_BF16)
+    m = vit.ViT(cfg, args.batch, vit.VIT_FP8 if args.dtype == "fp8" else vit.VIT_BF16)
     m.set_params(vit.data.init_params(cfg, "ref", seed=1337))
     px, lab = vit.data.synthetic_batch(cfg, args.batch, seed=1337)
     m.set_batch(px, lab)

@@ -148,6 +148,12 @@ bool quantize_mx_rowcol_bf16(uint8_t* qr, uint8_t* slr, uint8_t* qc, uint8_t* sl
 long long mx_cols_kp(long long R);
 long long mx_rows_padded(long long rows);
 size_t mx_scale_bytes(long long rows, int K);
+// LayerNorm forward into both MX forms (no bf16 tensor): qr/slr as quantize_mx_rowcol_bf16's row
+// form of ln_forward_bf16's output, qc/slc its column form over [tok_off, tok_off + ntok)
+bool ln_forward_mx_supported(int C);
+bool ln_forward_mx(uint8_t* qr, uint8_t* slr, uint8_t* qc, uint8_t* slc, float* mean, float* rstd, const float* x,
+                   const float* w, const float* b, long long R, int C, long long ldqc, long long tok_off, long long ntok,
+                   hipStream_t s);
 
 // column sums: dbias[n] += sum_m X[m*ld + n]   (X fp32 or bf16), in a fixed order: one pass when
 // M <= 256, else per-256-row partial rows in ws (nullptr = thread workspace; cdiv(M,256) * N

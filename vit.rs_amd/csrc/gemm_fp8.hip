@@ -25,6 +25,7 @@
 #include <cstdlib>
 
 #include "gemm_common.h"
+#include "ln_common.h"
 
 namespace vit {
 namespace f8 {
@@ -650,6 +651,138 @@ __global__ __launch_bounds__(TOK * 2 * (COLS / 64)) void quantize_mx_rowcol_k(ui
     *reinterpret_cast<u32x4*>(dst) = u32x4{w[0], w[1], w[2], w[3]};
     *reinterpret_cast<u32x4*>(dst + 16) = u32x4{w[4], w[5], w[6], w[7]};
 }
+
+// LayerNorm forward straight into both MX forms.  In the fp8 trainer ln1 / ln2 feed only the qkv /
+// fc GEMM (row form) and the qkv / fc weight gradients (column form), so the bf16 tensor that
+// ln_forward_bf16 stored and quantize_mx_rowcol_bf16 read back (4 B per element) never exists.
+// A workgroup takes 32 tokens (8 waves x 4 rows; C = 256 NV): each wave normalises its rows with
+// ln_vec_stats / ln_vec_y (ln_common.h, the arithmetic of ln_fwd_vec_k), rounds to bf16, writes the row form
+// (8 lanes per 32-channel block: 3 xor-shuffles for the block amax; 256 consecutive bytes per wave
+// store) and puts the bf16 row into an LDS tile; after one barrier each thread takes a channel and
+// writes its column block of the 32 tokens (as quantize_mx_cols_k).  Both forms equal
+// ln_forward_bf16 + quantize_mx_rowcol_bf16 byte for byte.  Rows R .. Rpad-1 write zero row-form
+// scales; tokens R .. ntok-1 of the column form are zero padding (as quantize_mx_rowcol_k).
+// (two rows of loads in flight per wave: <= 128 VGPRs up to C = 1280, where two 80-KiB workgroups share a CU)
+// WB: the lane's LN weight / bias float4s held in registers for the wave's 4 rows (else re-read per row)
+// RPW: rows per wave (4: 8 waves, 512 threads, the default; 2: 16 waves, 1024 threads, every row's loads
+// issued at once: VIT_LNMX_RPW=2, measured 39.1 vs 36.4 us at 16448 x 1280, tools/bench_lnmx.py).
+// Standalone it is at par with the pair it replaces (36.4 vs 37.5 us per ViT-H/14 micro-batch; 64.6 vs
+// 67.7 us for B = 128): a 32-token tile holds 80 KiB of LDS, so two workgroups per CU and 514 tiles
+// for 512 slots; in the train step the other micro-batch stream fills the gaps.
+template <int NV, bool WB, int RPW>
+__global__ __launch_bounds__(64 * 32 / RPW, (RPW == 2 || NV <= 5 ? 4 : 2)) void ln_fwd_mx_k(uint8_t* __restrict__ qr, uint8_t* __restrict__ slr,
+                                                   uint8_t* __restrict__ qc, uint8_t* __restrict__ slc,
+                                                   float* __restrict__ mean, float* __restrict__ rstd,
+                                                   const float* __restrict__ x, const float* __restrict__ w,
+                                                   const float* __restrict__ b, int R, int rgr_tot, long long ldqc,
+                                                   int tok_off, int ntok, int rgc_tot, int xmap) {
+    constexpr int C = 256 * NV, TOK = 32, NT = 64 * TOK / RPW;
+    __shared__ __attribute__((aligned(16))) uint16_t tile[TOK * C];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    // xmap: within each group of 32 workgroups, the 4 tiles of one 128-token span go to workgroups
+    // 8 apart (the same XCD, dispatched together), so the column form's 32-B pieces of a 128-B line
+    // meet in one L2 instead of leaving four L2s as partial lines
+    int t = blockIdx.x;
+    if (xmap && (blockIdx.x | 31) < gridDim.x) t = (blockIdx.x & ~31) + (blockIdx.x & 7) * 4 + ((blockIdx.x >> 3) & 3);
+    const int tok0 = t * TOK;
+    // row i + 1 in flight while row i reduces, row i + 2 requested once row i's inputs are dead
+    // (clamped rows: unconditional loads).  A branch-free form (zero-selects, buffer stores that drop
+    // rows >= R, every lane storing the scale bytes) let hipcc count the waits per row instead of
+    // vmcnt(0), but spilled at 4 rows per wave and measured slower at 2 (39.1 vs 36.4 us, 16448 x 1280)
+    float4 v[2][NV];
+    auto load = [&](int i) {
+        const float4* x4 = reinterpret_cast<const float4*>(x + (long long)min(tok0 + wave * RPW + i, R - 1) * C);
+#pragma unroll
+        for (int j = 0; j < NV; j++) v[i & 1][j] = x4[lane + 64 * j];
+    };
+    load(0);
+    if (RPW > 1) load(1);
+    // the LN weight / bias float4s of this lane, once per wave (not a dependent load per row)
+    float4 w4[NV], b4[NV];
+    if constexpr (WB) {
+#pragma unroll
+        for (int j = 0; j < NV; j++) {
+            w4[j] = reinterpret_cast<const float4*>(w)[lane + 64 * j];
+            b4[j] = reinterpret_cast<const float4*>(b)[lane + 64 * j];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < RPW; i++) {
+        const int r = wave * RPW + i, tok = tok0 + r;
+        uint2* trow = reinterpret_cast<uint2*>(tile + r * C);
+        if (tok >= R) {  // padding row: zero tile row (the column form's padding tokens), scale 0
+            if (i + 2 < RPW) load(i + 2);
+#pragma unroll
+            for (int j = 0; j < NV; j++) {
+                const int k = lane + 64 * j, kb = k >> 3;
+                trow[k] = make_uint2(0u, 0u);
+                if ((lane & 7) == 0)
+                    slr[((long long)(kb >> 1) * rgr_tot + (tok >> 5)) * 64 + (kb & 1) * 32 + (tok & 31)] = 0;
+            }
+            continue;
+        }
+        float m, rs;
+        ln_vec_stats<NV>(v[i & 1], C, m, rs);
+        uint2 hv[NV];
+#pragma unroll
+        for (int j = 0; j < NV; j++) {
+            const int k = lane + 64 * j;
+            const float4 y = WB ? ln_vec_y(v[i & 1][j], w4[j], b4[j], m, rs)
+                                : ln_vec_y(v[i & 1][j], reinterpret_cast<const float4*>(w)[k],
+                                           reinterpret_cast<const float4*>(b)[k], m, rs);
+            hv[j] = make_uint2(pack_bf16x2(y.x, y.y), pack_bf16x2(y.z, y.w));
+        }
+        if (i + 2 < RPW) load(i + 2);  // row i's inputs are dead: its buffer takes row i + 2
+#pragma unroll
+        for (int j = 0; j < NV; j++) {
+            const int k = lane + 64 * j, kb = k >> 3;  // channels 4k .. 4k+3, MX block 4k / 32
+            const uint2 h = hv[j];
+            trow[k] = h;
+            const float f0 = __uint_as_float(h.x << 16), f1 = __uint_as_float(h.x & 0xffff0000u);
+            const float f2 = __uint_as_float(h.y << 16), f3 = __uint_as_float(h.y & 0xffff0000u);
+            float amax = fmaxf(fmaxf(fabsf(f0), fabsf(f1)), fmaxf(fabsf(f2), fabsf(f3)));
+            amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+            amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+            amax = fmaxf(amax, __shfl_xor(amax, 4, 64));
+            const int sb = mx_scale_byte(amax);
+            if ((lane & 7) == 0)
+                slr[((long long)(kb >> 1) * rgr_tot + (tok >> 5)) * 64 + (kb & 1) * 32 + (tok & 31)] = (uint8_t)sb;
+            const float inv = __uint_as_float((uint32_t)(254 - sb) << 23);  // 2^(127 - sb), exact
+            int t = __builtin_amdgcn_cvt_pk_fp8_f32(f0 * inv, f1 * inv, 0, false);
+            t = __builtin_amdgcn_cvt_pk_fp8_f32(f2 * inv, f3 * inv, t, true);
+            reinterpret_cast<uint32_t*>(qr + (long long)tok * C)[k] = (uint32_t)t;
+        }
+        if (lane == 0) {
+            mean[tok] = m;
+            rstd[tok] = rs;
+        }
+    }
+    __syncthreads();
+    if (tok0 >= ntok) return;
+    const int kb = (tok_off + tok0) >> 5;
+    for (int c = tid; c < C; c += NT) {
+        float cv[TOK];
+        float amax = 0.f;
+#pragma unroll
+        for (int t = 0; t < TOK; t++) {
+            cv[t] = __uint_as_float((uint32_t)tile[t * C + c] << 16);
+            amax = fmaxf(amax, fabsf(cv[t]));
+        }
+        const int sb = mx_scale_byte(amax);
+        slc[((long long)(kb >> 1) * rgc_tot + (c >> 5)) * 64 + (kb & 1) * 32 + (c & 31)] = (uint8_t)sb;
+        const float inv = __uint_as_float((uint32_t)(254 - sb) << 23);
+        uint32_t wd[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            int t = __builtin_amdgcn_cvt_pk_fp8_f32(cv[4 * j] * inv, cv[4 * j + 1] * inv, 0, false);
+            t = __builtin_amdgcn_cvt_pk_fp8_f32(cv[4 * j + 2] * inv, cv[4 * j + 3] * inv, t, true);
+            wd[j] = (uint32_t)t;
+        }
+        uint8_t* dst = qc + (long long)c * ldqc + tok_off + tok0;
+        *reinterpret_cast<u32x4*>(dst) = u32x4{wd[0], wd[1], wd[2], wd[3]};
+        *reinterpret_cast<u32x4*>(dst + 16) = u32x4{wd[4], wd[5], wd[6], wd[7]};
+    }
+}
 }  // namespace f8
 
 long long mx_rows_padded(long long rows) { return (rows + 255) / 256 * 256; }
@@ -825,6 +958,53 @@ bool quantize_mx_rowcol_bf16(uint8_t* qr, uint8_t* slr, uint8_t* qc, uint8_t* sl
     count_hit(VIT_HIT_QUANT_ROWCOL);
     return true;
 }
+bool ln_forward_mx_supported(int C) { return C % 256 == 0 && C >= 256 && C <= 2048 && C != 1792; }
+bool ln_forward_mx(uint8_t* qr, uint8_t* slr, uint8_t* qc, uint8_t* slc, float* mean, float* rstd, const float* x,
+                   const float* w, const float* b, long long R, int C, long long ldqc, long long tok_off, long long ntok,
+                   hipStream_t s) {
+    if (R <= 0) return true;
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    if (!ln_forward_mx_supported(C) || ldqc % 16 || tok_off % 64 || tok_off < 0 || ntok < R ||
+        ntok > mx_cols_kp(R) || tok_off + ntok > ldqc || !al16(x) || !al16(w) || !al16(b) || !al16(qr) ||
+        !al16(qc) || R >= (1LL << 30) || ldqc >= (1LL << 31)) {
+        set_error("ln_forward_mx: C in 256 .. 2048 (multiple of 256), tok_off %% 64, R <= ntok <= R rounded to 64 "
+                  "and 16-B aligned operands required (C=%d R=%lld tok_off=%lld ntok=%lld ldqc=%lld)",
+                  C, R, tok_off, ntok, ldqc);
+        return false;
+    }
+    const long long rp = mx_rows_padded(R);
+    const dim3 g((unsigned)(rp / 32));
+    const int rgr = (int)(rp / 32), rgc = (int)(mx_rows_padded(C) / 32);
+    static const int xmap = [] {
+        const char* e = getenv("VIT_LNMX_XMAP");
+        return e ? atoi(e) : 1;
+    }();
+    static const bool wb = [] {
+        const char* e = getenv("VIT_LNMX_WB");
+        return !(e && e[0] == '0');
+    }();
+    static const int rpw = [] {
+        const char* e = getenv("VIT_LNMX_RPW");
+        return e && atoi(e) == 2 ? 2 : 4;
+    }();
+    switch (C / 256) {
+#define VIT_LAUNCH(NV, WB, RPW) \
+    f8::ln_fwd_mx_k<NV, WB, RPW><<<g, 64 * 32 / RPW, 0, s>>>(qr, slr, qc, slc, mean, rstd, x, w, b, (int)R, rgr, ldqc, \
+                                                             (int)tok_off, (int)ntok, rgc, xmap)
+#define VIT_CASE(NV) \
+    case NV: \
+        if (rpw == 2) { if (wb) VIT_LAUNCH(NV, true, 2); else VIT_LAUNCH(NV, false, 2); } \
+        else { if (wb) VIT_LAUNCH(NV, true, 4); else VIT_LAUNCH(NV, false, 4); } \
+        break;
+        VIT_CASE(1) VIT_CASE(2) VIT_CASE(3) VIT_CASE(4) VIT_CASE(5) VIT_CASE(6) VIT_CASE(8)
+#undef VIT_CASE
+#undef VIT_LAUNCH
+        default: break;
+    }
+    after_launch("ln_forward_mx");
+    count_hit(VIT_HIT_LN_MX);
+    return true;
+}
 void quantize_mx_batched_bf16(uint8_t* q, uint8_t* sl, const bf16_t* x, long long R, int K, int count,
                               long long xs, long long qs, long long ss, hipStream_t s) {
     quantize_mx<bf16_t>(q, sl, x, R, K, K, K, count, xs, qs, ss, s);
@@ -855,6 +1035,11 @@ void quantize_mx_cols_bf16_ex(uint8_t* q, uint8_t* scales, const uint16_t* x, lo
 void quantize_mx_rowcol_bf16_ex(uint8_t* qr, uint8_t* scales_r, uint8_t* qc, uint8_t* scales_c, const uint16_t* x,
                                 long long R, int C, long long ldx, long long ldqc, long long tok_off, long long ntok) {
     quantize_mx_rowcol_bf16(qr, scales_r, qc, scales_c, (const bf16_t*)x, R, C, ldx, ldqc, tok_off, ntok, stream());
+}
+void layernorm_forward_mx(uint8_t* qr, uint8_t* scales_r, uint8_t* qc, uint8_t* scales_c, float* mean, float* rstd,
+                          const float* inp, const float* weight, const float* bias, long long R, int C, long long ldqc,
+                          long long tok_off, long long ntok) {
+    ln_forward_mx(qr, scales_r, qc, scales_c, mean, rstd, inp, weight, bias, R, C, ldqc, tok_off, ntok, stream());
 }
 void gemm_fp8_fused_mx(void* C, void* C2, long long ldc, const void* aux, long long ldaux, const uint8_t* A,
                        const uint8_t* a_scale, long long lda, const uint8_t* B, const uint8_t* b_scale,

@@ -4,6 +4,7 @@
 // grid-stride vectorised kernels; matmul_* go to the MFMA GEMMs of gemm.hip; attention to
 // attention.hip.  Each op cites the reference function it replaces.
 #include "ops_internal.h"
+#include "ln_common.h"
 
 namespace vit {
 
@@ -197,31 +198,18 @@ __global__ __launch_bounds__(256) void ln_fwd_vec_k(TO* __restrict__ out, float*
     if (row >= rows) return;
     const float4* x4 = reinterpret_cast<const float4*>(inp + row * C);
     float4 v[NV];
-    float s = 0.f;
 #pragma unroll
-    for (int j = 0; j < NV; j++) {
-        v[j] = x4[lane + 64 * j];
-        s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
-    }
-    const float m = warp_sum(s) / (float)C;
-    float q = 0.f;
-#pragma unroll
-    for (int j = 0; j < NV; j++) {
-        const float a = v[j].x - m, bb = v[j].y - m, c = v[j].z - m, d = v[j].w - m;
-        q += (a * a + bb * bb) + (c * c + d * d);
-    }
-    const float r = 1.0f / sqrtf(warp_sum(q) / (float)C + 1e-5f);
+    for (int j = 0; j < NV; j++) v[j] = x4[lane + 64 * j];
+    float m, r;
+    ln_vec_stats<NV>(v, C, m, r);  // ln_common.h (shared with ln_fwd_mx_k)
 #pragma unroll
     for (int j = 0; j < NV; j++) {
         const int k = lane + 64 * j;
-        const float4 w4 = reinterpret_cast<const float4*>(w)[k];
-        const float4 b4 = reinterpret_cast<const float4*>(b)[k];
-        const float y0 = (r * (v[j].x - m)) * w4.x + b4.x, y1 = (r * (v[j].y - m)) * w4.y + b4.y;
-        const float y2 = (r * (v[j].z - m)) * w4.z + b4.z, y3 = (r * (v[j].w - m)) * w4.w + b4.w;
+        const float4 y = ln_vec_y(v[j], reinterpret_cast<const float4*>(w)[k], reinterpret_cast<const float4*>(b)[k], m, r);
         if constexpr (sizeof(TO) == 2)
-            reinterpret_cast<uint2*>(out + row * C)[k] = make_uint2(pack_bf16x2(y0, y1), pack_bf16x2(y2, y3));
+            reinterpret_cast<uint2*>(out + row * C)[k] = make_uint2(pack_bf16x2(y.x, y.y), pack_bf16x2(y.z, y.w));
         else
-            reinterpret_cast<float4*>(out + row * C)[k] = make_float4(y0, y1, y2, y3);
+            reinterpret_cast<float4*>(out + row * C)[k] = y;
     }
     if (lane == 0) {
         mean[row] = m;

@@ -401,6 +401,11 @@ struct Trainer {
     QMat fchgc, dfchc;
     bool rowcol_on() const { return fp8() && rowcol_ok && ((long long)(B / nmb) * T) % 64 == 0; }
     bool epicol_on() const { return rowcol_on() && fuse_mx && (4 * C) % 64 == 0; }
+    // fp8: LayerNorm forward straight into the MX forms (ln_forward_mx; VIT_FP8_LN_MX=0: bf16 + rowcol)
+    bool ln_mx = true;
+    bool lnmx_on() const { return rowcol_on() && ln_mx && ln_forward_mx_supported(C); }
+    // the column-form span of micro-batch mb (R rows): the last one carries the padding tokens
+    long long mb_ntok(int mb, long long R) const { return mb == nmb - 1 ? kp_tok - (long long)mb * R : R; }
     QMat fchgc_of(int l) const {
         return {fchgc.q + (long long)l * 4 * C * kp_tok, fchgc.s + (long long)l * mx_scale_bytes(4LL * C, (int)kp_tok)};
     }
@@ -715,7 +720,9 @@ struct Trainer {
                     wg_a.s = alloc<uint8_t>((long long)mx_scale_bytes(4LL * C, (int)kp));
                     wg_b.q = alloc<uint8_t>(4LL * C * kp);
                     wg_b.s = alloc<uint8_t>((long long)mx_scale_bytes(4LL * C, (int)kp));
-                    const char* rc = getenv("VIT_FP8_ROWCOL");
+                    const char* lx = getenv("VIT_FP8_LN_MX");
+                ln_mx = !(lx && lx[0] == '0');
+                const char* rc = getenv("VIT_FP8_ROWCOL");
                     rowcol_ok = !(rc && rc[0] == '0');
                     kp_tok = kp;
                     if (rowcol_ok) {
@@ -864,20 +871,22 @@ struct Trainer {
     // here.  mx_out: ask this GEMM's epilogue for the MX copy of its bf16 output (fp8 mode, fused)
     // colq: also write the column form of this micro-batch's A rows into colq (rowcol_on());
     // rec_ev: then record micro-batch event rec_ev (the weight gradient that reads colq waits on it)
-    void gemm_w(int cls, GemmArgs a, int ti, int l, bool transposed, int mb, hipStream_t st, bool pre = false,
+    // pre: PRE_EPI = in act_q2 (a fused GEMM epilogue wrote it), PRE_LN = in act_q (ln_forward_mx)
+    enum { PRE_NONE = 0, PRE_EPI = 1, PRE_LN = 2 };
+    void gemm_w(int cls, GemmArgs a, int ti, int l, bool transposed, int mb, hipStream_t st, int pre = PRE_NONE,
                 bool mx_out = false, const QMat* colq = nullptr, int rec_ev = -1) {
         if (!fp8()) { gemm(cls, a, true, st); return; }
         if (mx_out) { a.mx_q = act_q2[mb]; a.mx_s = act_s2[mb]; }
         const uint8_t* aq = act_q[mb];
         const uint8_t* as = act_s[mb];
-        if (pre) {
+        if (pre == PRE_EPI) {
             aq = act_q2[mb];
             as = act_s2[mb];
-        } else {
+        } else if (pre == PRE_NONE) {
             tbeg(TC_QUANT, 0, st);
             if (colq) {
                 const long long r0 = (long long)mb * (B / nmb) * T;
-                const long long ntok = mb == nmb - 1 ? kp_tok - r0 : a.M;
+                const long long ntok = mb_ntok(mb, a.M);
                 quantize_mx_rowcol_bf16(act_q[mb], act_s[mb], colq->q, colq->s, (const bf16_t*)a.A, a.M, a.K, a.lda,
                                         kp_tok, r0, ntok, st);
             } else {
@@ -991,16 +1000,21 @@ struct Trainer {
                 hipStream_t st = ms[mb];
                 const long long r0 = (long long)mb * R;
                 const float* x = xl + r0 * C;
+                const bool rc = rowcol_on(), lm = lnmx_on();
+                QMat c_ln1 = rc ? actc_of(0, l) : QMat{}, c_atty = rc ? actc_of(1, l) : QMat{},
+                     c_ln2 = rc ? actc_of(2, l) : QMat{};
                 tbeg(TC_LN_FWD, 0, st);
-                ln_forward_bf16(a.ln1 + r0 * C, a.ln1_mean + r0, a.ln1_rstd + r0, x, P(P_LN1W, l), P(P_LN1B, l), R, C, st);
+                if (lm)  // ln1 only in its two MX forms (the qkv GEMM's A operand, the qkv wgrad's B)
+                    ln_forward_mx(act_q[mb], act_s[mb], c_ln1.q, c_ln1.s, a.ln1_mean + r0, a.ln1_rstd + r0, x,
+                                  P(P_LN1W, l), P(P_LN1B, l), R, C, kp_tok, r0, mb_ntok(mb, R), st);
+                else
+                    ln_forward_bf16(a.ln1 + r0 * C, a.ln1_mean + r0, a.ln1_rstd + r0, x, P(P_LN1W, l), P(P_LN1B, l), R, C, st);
                 tend();
                 GemmArgs q;
                 q.A = a.ln1 + r0 * C; q.lda = C; q.B = W(P_QKVW, l); q.ldb = C; q.C = a.qkv + r0 * 3 * C;
                 q.ldc = 3 * C; q.bias = P(P_QKVB, l); q.M = (int)R; q.N = 3 * C; q.K = C; q.epi = EPI_BF16_STORE;
-                const bool rc = rowcol_on();
-                QMat c_ln1 = rc ? actc_of(0, l) : QMat{}, c_atty = rc ? actc_of(1, l) : QMat{},
-                     c_ln2 = rc ? actc_of(2, l) : QMat{};
-                gemm_w(TC_QKV_FWD, q, P_QKVW, l, false, mb, st, false, false, rc ? &c_ln1 : nullptr);
+                gemm_w(TC_QKV_FWD, q, P_QKVW, l, false, mb, st, lm ? PRE_LN : PRE_NONE, false,
+                       rc && !lm ? &c_ln1 : nullptr);
                 tbeg(TC_ATTN_FWD, 4.0 * Bm * (double)T * T * C, st);
                 attn_forward_fused(a.atty + r0 * C, a.lse + (long long)mb * Bm * NH * T, a.qkv + r0 * 3 * C, Bm, T, C, NH, st);
                 tend();
@@ -1008,10 +1022,14 @@ struct Trainer {
                 pr.A = a.atty + r0 * C; pr.lda = C; pr.B = W(P_ATTPROJW, l); pr.ldb = C; pr.C = a.res2 + r0 * C;
                 pr.ldc = C; pr.bias = P(P_ATTPROJB, l); pr.aux = x; pr.ldaux = C;
                 pr.M = (int)R; pr.N = C; pr.K = C; pr.epi = EPI_F32_RESID;
-                gemm_w(TC_PROJ_FWD, pr, P_ATTPROJW, l, false, mb, st, false, false, rc ? &c_atty : nullptr);
+                gemm_w(TC_PROJ_FWD, pr, P_ATTPROJW, l, false, mb, st, PRE_NONE, false, rc ? &c_atty : nullptr);
                 tbeg(TC_LN_FWD, 0, st);
-                ln_forward_bf16(a.ln2 + r0 * C, a.ln2_mean + r0, a.ln2_rstd + r0, a.res2 + r0 * C, P(P_LN2W, l),
-                                P(P_LN2B, l), R, C, st);
+                if (lm)
+                    ln_forward_mx(act_q[mb], act_s[mb], c_ln2.q, c_ln2.s, a.ln2_mean + r0, a.ln2_rstd + r0,
+                                  a.res2 + r0 * C, P(P_LN2W, l), P(P_LN2B, l), R, C, kp_tok, r0, mb_ntok(mb, R), st);
+                else
+                    ln_forward_bf16(a.ln2 + r0 * C, a.ln2_mean + r0, a.ln2_rstd + r0, a.res2 + r0 * C, P(P_LN2W, l),
+                                    P(P_LN2B, l), R, C, st);
                 tend();
                 GemmArgs f;
                 // fc: fchg = gelu(pre) for fcproj, fchd = gelu'(pre) for the fcproj dgrad (one sigmoid)
@@ -1023,12 +1041,13 @@ struct Trainer {
                     f.C2 = nullptr;
                     f.mxc_q = g.q; f.mxc_s = g.s; f.mxc_ld = kp_tok; f.mxc_off = r0;
                 }
-                gemm_w(TC_FC_FWD, f, P_FCW, l, false, mb, st, false, fuse_mx, rc ? &c_ln2 : nullptr);
+                gemm_w(TC_FC_FWD, f, P_FCW, l, false, mb, st, lm ? PRE_LN : PRE_NONE, fuse_mx,
+                       rc && !lm ? &c_ln2 : nullptr);
                 GemmArgs fp;
                 fp.A = a.fchg + r0 * 4 * C; fp.lda = 4 * C; fp.B = W(P_FCPROJW, l); fp.ldb = 4 * C;
                 fp.C = a.res3 + r0 * C; fp.ldc = C; fp.bias = P(P_FCPROJB, l); fp.aux = a.res2 + r0 * C;
                 fp.ldaux = C; fp.M = (int)R; fp.N = C; fp.K = 4 * C; fp.epi = EPI_F32_RESID;
-                gemm_w(TC_FCPROJ_FWD, fp, P_FCPROJW, l, false, mb, st, fuse_mx);
+                gemm_w(TC_FCPROJ_FWD, fp, P_FCPROJW, l, false, mb, st, fuse_mx ? PRE_EPI : PRE_NONE);
             }
         }
         mb_join();
@@ -1155,7 +1174,7 @@ struct Trainer {
                     d1.C = nullptr;
                     d1.mxc_q = dfchc.q; d1.mxc_s = dfchc.s; d1.mxc_ld = kp_tok; d1.mxc_off = r0;
                 }
-                gemm_w(TC_FCPROJ_DGRAD, d1, P_FCPROJW, l, true, mb, ms[mb], false, fuse_mx, rc ? &dcol[0] : nullptr, EV_RESA);
+                gemm_w(TC_FCPROJ_DGRAD, d1, P_FCPROJW, l, true, mb, ms[mb], PRE_NONE, fuse_mx, rc ? &dcol[0] : nullptr, EV_RESA);
                 if (ec && two_streams) VIT_HIP(hipEventRecord(mev[mb][EV_DFCH], ms[mb]));  // dfchc final
             }
             if (rc) wgrad(TC_FCPROJ_WGRAD, rbA, C, a.fchg, 4 * C, G(P_FCPROJW, l), EV_RESA, EV_W1, &dcol[0],
@@ -1168,7 +1187,7 @@ struct Trainer {
                 GemmArgs d2;
                 d2.A = dfch + r0 * 4 * C; d2.lda = 4 * C; dgrad_b(d2, P_FCW, l, 4 * C, C);
                 d2.C = dln_bf + r0 * C; d2.ldc = C; d2.M = (int)R; d2.N = C; d2.K = 4 * C; d2.epi = EPI_BF16_STORE;
-                gemm_w(TC_FC_DGRAD, d2, P_FCW, l, true, mb, ms[mb], fuse_mx);
+                gemm_w(TC_FC_DGRAD, d2, P_FCW, l, true, mb, ms[mb], fuse_mx ? PRE_EPI : PRE_NONE);
                 // ln2 backward + residual: dres2 = dres3 + LN2'(dln2); attproj_b += colsum(dres2)
                 after_wgrad(EV_W3, ms[mb]);  // the previous layer's attproj wgrad has read rbB
                 tbeg(TC_LN_BWD, 0, ms[mb]);
@@ -1185,7 +1204,7 @@ struct Trainer {
                 GemmArgs d3;
                 d3.A = rbB + r0 * C; d3.lda = C; dgrad_b(d3, P_ATTPROJW, l, C, C);
                 d3.C = datty + r0 * C; d3.ldc = C; d3.M = (int)R; d3.N = C; d3.K = C; d3.epi = EPI_BF16_STORE;
-                gemm_w(TC_PROJ_DGRAD, d3, P_ATTPROJW, l, true, mb, ms[mb], false, false, rc ? &dcol[1] : nullptr, EV_RESB);
+                gemm_w(TC_PROJ_DGRAD, d3, P_ATTPROJW, l, true, mb, ms[mb], PRE_NONE, false, rc ? &dcol[1] : nullptr, EV_RESB);
                 // attention (+ qkv_b)
                 after_wgrad(EV_W4, ms[mb]);  // the previous layer's qkv wgrad has read dqkv
                 tbeg(TC_ATTN_BWD, 8.0 * Bm * (double)T * T * C, ms[mb]);
@@ -1203,7 +1222,7 @@ struct Trainer {
                 GemmArgs d4;
                 d4.A = dqkv + r0 * 3 * C; d4.lda = 3 * C; dgrad_b(d4, P_QKVW, l, 3 * C, C);
                 d4.C = dln_bf + r0 * C; d4.ldc = C; d4.M = (int)R; d4.N = C; d4.K = 3 * C; d4.epi = EPI_BF16_STORE;
-                gemm_w(TC_QKV_DGRAD, d4, P_QKVW, l, true, mb, ms[mb], false, false, rc ? &dcol[2] : nullptr, EV_DQKV);
+                gemm_w(TC_QKV_DGRAD, d4, P_QKVW, l, true, mb, ms[mb], PRE_NONE, false, rc ? &dcol[2] : nullptr, EV_DQKV);
                 // ln1 backward: dres = dres2 + LN1'(dln1); fcproj_b of layer l-1 += colsum(dres)
                 after_wgrad(EV_W1, ms[mb]);  // this layer's fcproj wgrad has read rbA
                 tbeg(TC_LN_BWD, 0, ms[mb]);
@@ -1797,6 +1816,8 @@ int vit_trainer_set_option(vit_trainer_t* h, const char* name, int value) {
         t.nmb = t.pick_nmb(value);
     } else if (n == "dgrad_transposed") {
         t.dgrad_wt = value != 0;
+    } else if (n == "fp8_ln_mx") {  // fp8: LayerNorm forward into the MX forms (default 1)
+        t.ln_mx = value != 0;
     } else if (n == "dp_probe") {
         if (value && !t.dp_snap) {  // allocated once, kept until destroy
             t.dp_snap = t.alloc<float>(t.arena_elems);
