@@ -17,6 +17,13 @@
 #include <algorithm>
 #include <cstdlib>
 
+// one phase per K-step in the persistent engine (the fp8 engine's r06 form): measured slower for bf16
+// (per ViT-B/16 layer 2.595 / 2.601 vs 2.544 / 2.545 ms, step 36.13 / 36.02 vs 35.88 / 35.80 ms,
+// two interleaved rounds, profiles/r06_onephase.txt), so off
+#ifndef VIT_G2_ONEPHASE
+#define VIT_G2_ONEPHASE 0
+#endif
+
 namespace vit {
 
 // ============================================================================ bf16 MFMA GEMM
@@ -601,6 +608,26 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_s(GemmParams p) {
             for (int b = 0; b < 4; b++) fb[b] = frag<true>(img + IMG_BYTES, wn * 64 + b * 16, lane);
 #pragma unroll
             for (int a = 0; a < 4; a++) alo[a] = frag<true>(img, wm * 128 + a * 16, lane);
+#if VIT_G2_ONEPHASE
+            // one phase per step: all 12 fragments read before one barrier, the 32 MFMAs after it
+            // (two barriers per step instead of four)
+#pragma unroll
+            for (int a = 0; a < 4; a++) ahi[a] = frag<true>(img, wm * 128 + (4 + a) * 16, lane);
+            issue_a(kt + 2, sl2, more);
+            issue_b(kt + 2, sl2, more);
+            // own pieces of the next step landed (the one after, 4 pieces, in flight); in a later
+            // tile's first step they were retired before the previous epilogue
+            if (kt > 0 || j == 0) {
+                if (kt + 2 < nk || more) wait_vm(4);
+                else wait_vm(0);
+            }
+            bar();
+            mfma_half(0, alo, fb);
+            mfma_half(1, ahi, fb);
+            bar();
+            sl = (sl + 1) & 3;
+            continue;
+#endif
             issue_a(kt + 2, sl2, more);
             bar();
             mfma_half(0, alo, fb);

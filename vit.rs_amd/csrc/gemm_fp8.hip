@@ -27,6 +27,17 @@
 #include "gemm_common.h"
 #include "ln_common.h"
 
+#ifndef VIT_F8_TRACE
+#define VIT_F8_TRACE 0
+#endif
+// one phase per K-step in the streaming engine (two barriers per step instead of four): faster alone
+// (ViT-H/14 micro-batch GEMMs, tools/f8_trace.py: qkv fwd 146 -> 128 us, fc dgrad 187 -> 170, qkv dgrad
+// 152 -> 137) but slower in the sustained train step (117.0 vs 115.7 ms/step, two interleaved rounds;
+// profiles/r06_onephase.txt), so off
+#ifndef VIT_F8_ONEPHASE
+#define VIT_F8_ONEPHASE 0
+#endif
+
 namespace vit {
 namespace f8 {
 constexpr int BM = 256, BN = 256, NT = 512;
@@ -87,6 +98,7 @@ __device__ __forceinline__ void wait_vm(int n) {
         case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
         case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
         case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
         default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     }
 }
@@ -333,12 +345,30 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_s(F8Params fp) {
 #pragma unroll
         for (int q = 0; q < 2; q++) glds16(B + (long long)k * KB + (c ? cur.b[q] : nxt.b[q]), dst + (q * 8 + wave) * 1024);
     };
+#if VIT_F8_TRACE
+    // diagnostic build (tools/f8_trace.py): lane 0 of every wave of workgroups 0..7 sums the shader
+    // cycles (s_memtime, sampled at issue) spent waiting for LDS reads before each barrier, in the
+    // barrier, in the counted vmcnt waits of the main loop, in main loops and in epilogues
+    unsigned long long tr_lgk = 0, tr_bar = 0, tr_vm = 0, tr_main = 0, tr_epi = 0, tr_t = 0;
+    const unsigned long long tr_mt0 = __builtin_amdgcn_s_memtime(), tr_rt0 = __builtin_amdgcn_s_memrealtime();
+#define F8T(x) x
+#else
+#define F8T(x)
+#endif
     auto bar = [&]() {
         __builtin_amdgcn_sched_barrier(0);
+        F8T(const unsigned long long t0 = __builtin_amdgcn_s_memtime();)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        F8T(const unsigned long long t1 = __builtin_amdgcn_s_memtime();)
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
+        F8T(const unsigned long long t2 = __builtin_amdgcn_s_memtime(); tr_lgk += t1 - t0; tr_bar += t2 - t1;)
         __builtin_amdgcn_sched_barrier(0);
+    };
+    auto wait_vm_t = [&](int n) {
+        F8T(const unsigned long long t0 = __builtin_amdgcn_s_memtime();)
+        wait_vm(n);
+        F8T(tr_vm += __builtin_amdgcn_s_memtime() - t0;)
     };
     auto mfma_half = [&](int half, const v8i (&fa)[2], const int (&sa)[2], const v8i (&fb)[2], const int (&sb)[2]) {
 #pragma unroll
@@ -361,6 +391,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_s(F8Params fp) {
     int sb_[2], sa0[2], sa1[2];
     for (int j = 0; j < my_tiles; j++) {
         const bool more = j + 1 < my_tiles;
+        F8T(tr_t = __builtin_amdgcn_s_memtime();)
         bar();
         if (lagging) {
             __builtin_amdgcn_s_setprio(1);
@@ -380,6 +411,29 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_s(F8Params fp) {
                 fa0[a] = frag(img, wm * 128 + a * 32, lane);
                 sa0[a] = scale_of(sc, wm * 4 + a, lane);
             }
+#if VIT_F8_ONEPHASE
+            // one phase per step: every fragment of the step read before one barrier, the 8 MFMAs
+            // after it (two barriers per step instead of four; 48 fragment VGPRs live at once)
+#pragma unroll
+            for (int a = 0; a < 2; a++) {
+                fa1[a] = frag(img, wm * 128 + (2 + a) * 32, lane);
+                sa1[a] = scale_of(sc, wm * 4 + 2 + a, lane);
+            }
+            issue_a(kt + 2, sl2, more);
+            issue_b(kt + 2, sl2, more);
+            // own pieces of the next step landed (the one after, 5 pieces, in flight); in a later
+            // tile's first step they were retired before the previous epilogue
+            if (kt > 0 || j == 0) {
+                if (kt + 2 < nk || more) wait_vm_t(5);
+                else wait_vm_t(0);
+            }
+            bar();
+            mfma_half(0, fa0, sa0, fb, sb_);
+            mfma_half(1, fa1, sa1, fb, sb_);
+            bar();
+            sl = (sl + 1) & 3;
+            continue;
+#endif
             issue_a(kt + 2, sl2, more);
             bar();
             mfma_half(0, fa0, sa0, fb, sb_);
@@ -392,8 +446,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_s(F8Params fp) {
             // own pieces of the next step landed (the A half of the one after, 3 pieces, in flight);
             // in a later tile's first step they were retired before the previous epilogue
             if (kt > 0 || j == 0) {
-                if (kt + 2 < nk || more) wait_vm(3);
-                else wait_vm(0);
+                if (kt + 2 < nk || more) wait_vm_t(3);
+                else wait_vm_t(0);
             }
             issue_b(kt + 2, sl2, more);
             bar();
@@ -402,6 +456,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_s(F8Params fp) {
             sl = (sl + 1) & 3;
         }
         if (!lagging) bar();  // balance the stagger barrier
+        F8T(const unsigned long long te = __builtin_amdgcn_s_memtime(); tr_main += te - tr_t; tr_t = te;)
         float bpre[8];
         staged_bias_prefetch<EPI>(p, lane, cur.tn0 + wn * 64, bpre);
         // through the builtin so hipcc knows no LDS-DMA is pending afterwards (as g2::gemm_kernel_s)
@@ -428,11 +483,22 @@ __global__ __launch_bounds__(NT, 1) void gemm_kernel_s(F8Params fp) {
                 }
         };
         staged_epilogue_q_any<EPI, true>(p, stage_pass, st, lane, cur.tm0 + wm * 128, cur.tn0 + wn * 64, bpre);
+        F8T(tr_epi += __builtin_amdgcn_s_memtime() - tr_t;)
         zero_acc();
         // recomputed rather than carried: nothing of the next tiles' sources stays live through the epilogue
         if (more) tile_src(j + 1, cur);
         if (j + 2 < my_tiles) tile_src(j + 2, nxt);
     }
+#if VIT_F8_TRACE
+    if (p.trace && blockIdx.x < 8 && lane == 0) {
+        unsigned long long* r = p.trace + (blockIdx.x * 8 + wave) * 16;
+        r[0] = tr_main; r[1] = tr_lgk; r[2] = tr_bar; r[3] = tr_vm; r[4] = tr_epi;
+        r[5] = (unsigned long long)my_tiles; r[6] = (unsigned long long)nk;
+        // the in-kernel shader clock: shader cycles over 100 MHz real-time ticks (MI355X guide, DVFS item 6)
+        r[8] = __builtin_amdgcn_s_memtime() - tr_mt0; r[9] = __builtin_amdgcn_s_memrealtime() - tr_rt0;
+    }
+#endif
+#undef F8T
 }
 
 // ------------------------------------------------------------------------------- quantizer
