@@ -62,6 +62,7 @@ enum {
     VIT_HIT_QUANT_ROWCOL = 87,       /* fused row + column MX quantization */
     VIT_HIT_GEMM_PP = 88,            /* bf16 two-group ping-pong 192x256 engine (variant 11; also counted as 256x256 + epi) */
     VIT_HIT_LN_MX = 89,              /* LayerNorm forward straight into the row + column MX forms (fp8) */
+    VIT_HIT_LNB_MX = 90,             /* LayerNorm backward (residual-gradient stream) + both MX forms (fp8) */
     VIT_HIT_COUNT = 96
 };
 int vit_kernel_hits(long long* out, int n); /* copies min(n, VIT_HIT_COUNT); returns VIT_HIT_COUNT */
@@ -214,6 +215,20 @@ void quantize_mx_rowcol_bf16_ex(uint8_t* qr, uint8_t* scales_r, uint8_t* qc, uin
  * layernorm_forward_bf16 (mean / rstd as it writes them) followed by quantize_mx_rowcol_bf16_ex of
  * its bf16 output, without the bf16 tensor; inp [R][C] fp32, C a multiple of 256 in 256 .. 2048
  * (not 1792). */
+/* the trainer's residual-gradient LayerNorm backward (train_vit.rs:603-637 + the residual add,
+ * "bf16 + lo8" planes: dres_out = dres_in + LN_dinp(dout); dweight / dbias / dres_colsum (nullable)
+ * += the column sums of dout * xhat / dout / dres_out in a fixed order) ... */
+void layernorm_backward_stream(uint16_t* dres_out, uint8_t* lo_out, const uint16_t* dres_in, const uint8_t* lo_in,
+                               float* dweight, float* dbias, float* dres_colsum, const uint16_t* dout, const float* inp,
+                               const float* weight, const float* mean, const float* rstd, long long R, int C);
+/* ... and the same with both MX forms of dres_out's bf16 plane written beside it (exactly
+ * quantize_mx_rowcol_bf16_ex of dres_out; the column sums group rows differently: equal within fp32
+ * rounding, not bitwise); C a multiple of 256 in 256 .. 1280 */
+void layernorm_backward_stream_mx(uint16_t* dres_out, uint8_t* lo_out, const uint16_t* dres_in, const uint8_t* lo_in,
+                                  float* dweight, float* dbias, float* dres_colsum, const uint16_t* dout,
+                                  const float* inp, const float* weight, const float* mean, const float* rstd,
+                                  long long R, int C, uint8_t* qr, uint8_t* scales_r, uint8_t* qc, uint8_t* scales_c,
+                                  long long ldqc, long long tok_off, long long ntok);
 void layernorm_forward_mx(uint8_t* qr, uint8_t* scales_r, uint8_t* qc, uint8_t* scales_c, float* mean,
                           float* rstd, const float* inp, const float* weight, const float* bias, long long R,
                           int C, long long ldqc, long long tok_off, long long ntok);

@@ -116,6 +116,7 @@ int vit_trainer_set_concurrency(vit_trainer_t* t, int on);
  *      "microbatch" = number of micro-batch streams wanted (1 .. 4; the largest divisor of B),
  *      "dgrad_transposed" = 1 (default): dgrad GEMMs read the transposed weight copy,
  *      "fp8_ln_mx" = 1 (default): fp8 mode's LayerNorm forwards write the MX forms directly,
+ *      "fp8_lnb_mx" = 1 (default): ... and its residual-gradient LayerNorm backwards those of dres,
  *      "dp_probe" = 1: every gradient chunk is also copied, on the all-reduce stream right after
  *      its all-reduce, into a snapshot arena (read with vit_trainer_get_dp_snapshot) — a check
  *      that each overlapped chunk was final when it was reduced.

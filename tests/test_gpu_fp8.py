@@ -380,6 +380,68 @@ def test_layernorm_forward_mx_bit_exact(gpu, R, C, parts):
     assert v.kernel_hits()[v.HIT_LN_MX] == sum(1 for lo, hi in zip(bounds[:-1], bounds[1:]) if hi > lo)
 
 
+@pytest.mark.parametrize("R,C,parts,dsum", [(100, 256, 1, True), (197, 768, 1, False), (2 * 257 * 16, 1280, 2, True),
+                                             (1000, 1024, 2, True), (3 * 1024 + 70, 512, 3, True), (4001, 1280, 1, False)])
+def test_layernorm_backward_mx_bit_exact(gpu, R, C, parts, dsum):
+    """The residual-gradient LayerNorm backward with both MX forms of its bf16 plane (the fp8 trainer's
+    dres2 / dres3) against the unfused pair it replaces: layernorm_backward_stream (the trainer's
+    ln_bwd_vec_k) then quantize_mx_rowcol_bf16_ex of its bf16 output.  The bf16 and lo8 planes, the
+    row form (with the padding rows' zero scales) and the column form assembled over `parts`
+    micro-batch slices are equal byte for byte; dW / db / dres column sums group their rows
+    differently (fixed order), so they agree to fp32 rounding (1e-5 of the column's magnitude)."""
+    v = gpu
+    rng = np.random.default_rng(R + 3 * C + parts)
+    x = (rng.normal(size=(R, C)) * 2 + rng.normal(size=(R, 1))).astype(np.float32)
+    mu = x.mean(1).astype(np.float32)
+    rs = (1.0 / np.sqrt(x.var(1) + 1e-5)).astype(np.float32)
+    w = rng.normal(size=C).astype(np.float32)
+    dyb = v.bf16_bits((rng.normal(size=(R, C)) * np.exp2(rng.integers(-6, 6, size=(R, 1)))).astype(np.float32))
+    hib = v.bf16_bits(rng.normal(size=(R, C)).astype(np.float32))
+    lo = rng.integers(0, 256, size=(R, C), dtype=np.uint8)
+    kp = int(v.lib().mx_cols_padded(R))
+    nsc = int(v.lib().mx_scale_size(C, kp))
+    qc_ref, sc_ref = Z(v, C * kp, np.uint8), Z(v, nsc, np.uint8)
+    qc = D(v, np.full(C * kp, 0x5A, np.uint8), np.uint8)
+    sc = D(v, np.full(nsc, 0x5A, np.uint8), np.uint8)
+    sums_ref = [Z(v, C), Z(v, C), Z(v, C)]
+    sums = [Z(v, C), Z(v, C), Z(v, C)]
+    step = ((R + parts - 1) // parts + 63) // 64 * 64 if parts > 1 else R
+    bounds = [min(i * step, R) for i in range(parts)] + [R]
+    wd = D(v, w)
+    v.kernel_hits_reset()
+    nlaunch = 0
+    for lo_, hi_ in zip(bounds[:-1], bounds[1:]):
+        n = hi_ - lo_
+        if n <= 0:
+            continue
+        nlaunch += 1
+        ntok = kp - lo_ if hi_ == R else n
+        args = (D(v, hib[lo_:hi_].copy(), np.uint16), D(v, lo[lo_:hi_].copy(), np.uint8))
+        com = (D(v, dyb[lo_:hi_].copy(), np.uint16), D(v, x[lo_:hi_].copy()), wd, D(v, mu[lo_:hi_].copy()),
+               D(v, rs[lo_:hi_].copy()), n, C)
+        ho_ref, lo_ref = Z(v, n * C, np.uint16), Z(v, n * C, np.uint8)
+        v.call("layernorm_backward_stream", ho_ref, lo_ref, *args, sums_ref[0], sums_ref[1],
+               sums_ref[2] if dsum else None, *com)
+        nsr = int(v.lib().mx_scale_size(n, C))
+        qr_ref, sr_ref = Z(v, n * C, np.uint8), Z(v, nsr, np.uint8)
+        v.call("quantize_mx_rowcol_bf16_ex", qr_ref, sr_ref, qc_ref, sc_ref, ho_ref, n, C, C, kp, lo_, ntok)
+        ho, lo8 = D(v, np.full(n * C, 0x5A5A, np.uint16), np.uint16), D(v, np.full(n * C, 0x5A, np.uint8), np.uint8)
+        qr = D(v, np.full(n * C, 0x5A, np.uint8), np.uint8)
+        sr = D(v, np.full(nsr, 0x5A, np.uint8), np.uint8)
+        v.call("layernorm_backward_stream_mx", ho, lo8, *args, sums[0], sums[1], sums[2] if dsum else None, *com,
+               qr, sr, qc, sc, kp, lo_, ntok)
+        assert np.array_equal(ho.numpy(), ho_ref.numpy()), f"bf16 plane differs at slice {lo_}"
+        assert np.array_equal(lo8.numpy(), lo_ref.numpy()), f"lo8 plane differs at slice {lo_}"
+        assert np.array_equal(sr.numpy(), sr_ref.numpy()), f"row scales differ at slice {lo_}"
+        assert np.array_equal(qr.numpy(), qr_ref.numpy()), f"row bytes differ at slice {lo_}"
+    assert np.array_equal(sc.numpy(), sc_ref.numpy()), "column scales differ"
+    assert np.array_equal(qc.numpy(), qc_ref.numpy()), "column bytes differ"
+    for k in range(3 if dsum else 2):
+        a, b = sums[k].numpy(), sums_ref[k].numpy()
+        assert np.max(np.abs(a - b)) <= 1e-5 * max(np.max(np.abs(b)), 1e-30), k
+    assert v.kernel_hits()[v.HIT_LNB_MX] == nlaunch
+
+
 @pytest.mark.parametrize("OC,Cin,R", [(256, 256, 64), (768, 320, 1000), (1280, 5120, 4112), (512, 768, 6000)])
 def test_gemm_fp8_wgrad_splitk(gpu, OC, Cin, R):
     """The fp8 weight gradient dW += dout^T . inp (epi 2) on column-quantized operands: one split

@@ -578,7 +578,7 @@ def test_vit_h14_fp8_config5_shard_full_step(gpu):
     as bench.py runs it (two micro-batch streams, stream concurrency on): one full step has a finite
     loss near ln(1000), finite non-zero gradients in every tensor family, and the loss drops after
     one SGD step.  The launch counters prove the kernels that only appear at this size ran: the
-    MXFP8 engine (every GEMM of every layer), the fused row+column quantizer, and the one-pass
+    MXFP8 engine (every GEMM of every layer), the MX writers (row+column quantizer, LayerNorm -> MX), and the one-pass
     attention backward with the T = 32k+1 last-key side path over 2048 (b, h) items.
     Replaces train_vit.rs:188-373 (forward / backward), :543-555 (weight gradients), :559-601
     (attention_backward) at this size; size-independent properties, not an oracle comparison
@@ -611,7 +611,10 @@ def test_vit_h14_fp8_config5_shard_full_step(gpu):
     L = cfg.num_layers
     # fp8 engine: qkv / proj / fc / fcproj forward + input gradients (+ weight gradients) per layer
     assert hits[v.HIT_GEMM_FP8:v.HIT_GEMM_FP8 + 16].sum() >= 8 * L, hits[v.HIT_GEMM_FP8:v.HIT_GEMM_FP8 + 16]
-    assert hits[v.HIT_QUANT_ROWCOL] >= 6 * L, hits[v.HIT_QUANT_ROWCOL]
+    # both MX forms of ln1 / atty / ln2 / dres3 / dres2 / dqkv per layer: from the row+column quantizer
+    # or (r06) written by the LayerNorm forward / residual-gradient backward kernels themselves
+    assert hits[v.HIT_QUANT_ROWCOL] + hits[v.HIT_LN_MX] + hits[v.HIT_LNB_MX] >= 6 * L, hits[v.HIT_QUANT_ROWCOL]
+    assert hits[v.HIT_LN_MX] >= 2 * L and hits[v.HIT_LNB_MX] >= 2 * L - 1, (hits[v.HIT_LN_MX], hits[v.HIT_LNB_MX])
     assert hits[v.HIT_ATTN_BWD_XKEY] >= L, hits[v.HIT_ATTN_BWD_XKEY]
     assert hits[v.HIT_ATTN_FWD_MFMA] >= L
     assert hits[v.HIT_ATTN_GENERIC] == 0 and hits[v.HIT_ATTN_BWD_PAIR] == 0

@@ -108,6 +108,8 @@ _SIGS = {
     "quantize_mx_cols_bf16_ex": (None, [P, P, P, LL, I, LL]),
     "quantize_mx_rowcol_bf16_ex": (None, [P, P, P, P, P, LL, I, LL, LL, LL, LL]),
     "layernorm_forward_mx": (None, [P, P, P, P, P, P, P, P, P, LL, I, LL, LL, LL]),
+    "layernorm_backward_stream": (None, [P, P, P, P, P, P, P, P, P, P, P, P, LL, I]),
+    "layernorm_backward_stream_mx": (None, [P, P, P, P, P, P, P, P, P, P, P, P, LL, I, P, P, P, P, LL, LL, LL]),
     "gemm_fp8_fused": (None, [P, P, LL, P, LL, P, P, LL, P, P, LL, P, P, I, I, I, I]),
     "gemm_fp8_fused_mx": (None, [P, P, LL, P, LL, P, P, LL, P, P, LL, P, P, I, I, I, I, P, P]),
     "gemm_fp8_fused_mxc": (None, [P, P, LL, P, LL, P, P, LL, P, P, LL, P, P, I, I, I, I, P, P, P, P, LL, LL]),
@@ -198,6 +200,7 @@ HIT_ATTN_BWD_ONEPASS, HIT_ATTN_BWD_PAIR, HIT_ATTN_GENERIC = 83, 84, 85
 HIT_ATTN_BWD_XKEY, HIT_QUANT_ROWCOL = 86, 87
 HIT_GEMM_PP = 88
 HIT_LN_MX = 89
+HIT_LNB_MX = 90
 
 
 def kernel_hits():

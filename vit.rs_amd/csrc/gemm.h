@@ -151,6 +151,15 @@ size_t mx_scale_bytes(long long rows, int K);
 // LayerNorm forward into both MX forms (no bf16 tensor): qr/slr as quantize_mx_rowcol_bf16's row
 // form of ln_forward_bf16's output, qc/slc its column form over [tok_off, tok_off + ntok)
 bool ln_forward_mx_supported(int C);
+// LayerNorm backward of the bf16 + lo8 residual-gradient stream (as ln_backward_bf16_stream, part rows
+// [ln_bwd_blocks(R)][2C | 3C] or, part == nullptr, reduced into dw / db / dres_colsum) plus both MX
+// forms of its bf16 plane (as quantize_mx_rowcol_bf16); C a multiple of 256 up to 1280
+bool ln_backward_mx_supported(int C);
+bool ln_backward_bf16_stream_mx(bf16_t* dres_out, uint8_t* lo_out, const bf16_t* dres_in, const uint8_t* lo_in,
+                                float* dw, float* db, float* dres_colsum, const bf16_t* dout, const float* inp,
+                                const float* w, const float* mean, const float* rstd, long long R, int C,
+                                hipStream_t s, float* part, uint8_t* qr, uint8_t* slr, uint8_t* qc, uint8_t* slc,
+                                long long ldqc, long long tok_off, long long ntok);
 bool ln_forward_mx(uint8_t* qr, uint8_t* slr, uint8_t* qc, uint8_t* slc, float* mean, float* rstd, const float* x,
                    const float* w, const float* b, long long R, int C, long long ldqc, long long tok_off, long long ntok,
                    hipStream_t s);

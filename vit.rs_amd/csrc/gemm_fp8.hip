@@ -22,10 +22,12 @@
 // h*32 + r of row group g at step s is the scale of row 32g + r, k-block 2s + h.  Per slot the
 // tile's scales are 512 contiguous bytes per operand, staged by one 4-byte LDS-DMA per wave;
 // each MFMA reads its lane's byte with one ds_read_u8.  Padding rows carry scale 0 (2^-127).
+#include <algorithm>
 #include <cstdlib>
 
 #include "gemm_common.h"
 #include "ln_common.h"
+#include "ops_internal.h"
 
 #ifndef VIT_F8_TRACE
 #define VIT_F8_TRACE 0
@@ -849,6 +851,200 @@ __global__ __launch_bounds__(64 * 32 / RPW, (RPW == 2 || NV <= 5 ? 4 : 2)) void 
         *reinterpret_cast<u32x4*>(dst + 16) = u32x4{wd[4], wd[5], wd[6], wd[7]};
     }
 }
+
+// LayerNorm backward of the residual-gradient stream straight into both MX forms of its bf16 plane
+// (fp8 trainer: dres3 / dres2 feed the fcproj / attproj input-gradient GEMMs (row form) and weight
+// gradients (column form), so the row + column quantizer's read of the bf16 plane goes away; the
+// bf16 + lo8 planes are still written, the next LayerNorm backward reads them).  Per row exactly
+// ln_bwd_vec_k<NV, bf16, true> (ln_bwd_row, ln_common.h): dres_out = dres_in + LN'(dy) as bf16 + lo8.
+// A persistent workgroup (8 waves) walks 32-token tiles (4 rows per wave, the next row's loads in
+// flight); each wave keeps its dW / db column partials in its LDS rows and its dres column sums in
+// registers (the lane's 4 NV columns),
+// writes the row form of each row (8 lanes per 32-channel block) and the bf16 row into an LDS tile,
+// and after the tile's barrier every thread writes a channel's 32-token column block (as
+// ln_fwd_mx_k).  At the end the 8 waves' partials are summed in wave order into the workgroup's
+// partial row part[blockIdx.x][2C | 3C] (dw | db | dsum); rows gridDim.x .. nparts-1 are zeroed, so
+// the caller reduces the same nparts rows as for ln_bwd_vec_k.  hi / lo and both MX forms equal
+// ln_backward_bf16_stream + quantize_mx_rowcol_bf16 byte for byte; the partial sums group rows
+// differently (a deterministic fixed order, not the same fp32 association).
+struct LnbMx {
+    bf16_t* hi_out;
+    uint8_t* lo_out;
+    const bf16_t* hi_in;
+    const uint8_t* lo_in;
+    const bf16_t* dout;
+    const float* inp;
+    const float* w;
+    const float* mean;
+    const float* rstd;
+    float* part;
+    int nsum, nparts;
+    uint8_t *qr, *slr, *qc, *slc;
+    int R, ntiles, rgr_tot, tok_off, ntok, rgc_tot;
+    long long ldqc;
+};
+__device__ __forceinline__ float4 bf4_f32(uint2 u) {
+    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                       __uint_as_float(u.y & 0xffff0000u));
+}
+template <int NV>
+__global__ __launch_bounds__(512, 2) void ln_bwd_mx_k(LnbMx a) {
+    constexpr int C = 256 * NV, TOK = 32, RPW = 4, NT = 512;
+    __shared__ __attribute__((aligned(16))) uint16_t tile[TOK * C];  // 80 KiB at C = 1280 (ps partials at the end)
+    // dW / db column partials per wave in LDS (lane-owned entries: no synchronisation until the end),
+    // dres column sums in registers: 80 + 80 KiB = the whole LDS at C = 1280
+    __shared__ __attribute__((aligned(16))) float4 sp[8][2][NV * 64];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    float4 ps[NV];
+#pragma unroll
+    for (int j = 0; j < NV; j++) {
+        ps[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        sp[wave][0][lane + 64 * j] = sp[wave][1][lane + 64 * j] = ps[j];
+    }
+    // the wave's row sequence: tile t = blockIdx.x + n * gridDim.x, rows t * 32 + wave * 4 + i
+    uint2 pdy[NV], pri[NV];
+    float4 px[NV];
+    uint32_t plo[NV];
+    float pmu = 0.f, prs = 0.f;
+    auto fetch = [&](int row) {
+        const int r = min(row, a.R - 1);
+        const long long o = (long long)r * C;
+#pragma unroll
+        for (int j = 0; j < NV; j++) {
+            const int k = lane + 64 * j;
+            pdy[j] = reinterpret_cast<const uint2*>(a.dout + o)[k];
+            px[j] = reinterpret_cast<const float4*>(a.inp + o)[k];
+            pri[j] = reinterpret_cast<const uint2*>(a.hi_in + o)[k];
+            plo[j] = reinterpret_cast<const uint32_t*>(a.lo_in + o)[k];
+        }
+        pmu = a.mean[r];
+        prs = a.rstd[r];
+    };
+    int t = blockIdx.x;
+    if (t < a.ntiles) fetch(t * TOK + wave * RPW);
+    for (; t < a.ntiles; t += gridDim.x) {
+        const int tok0 = t * TOK;
+#pragma unroll
+        for (int i = 0; i < RPW; i++) {
+            const int r = wave * RPW + i, tok = tok0 + r;
+            float4 dy[NV], xr[NV], ri[NV];
+#pragma unroll
+            for (int j = 0; j < NV; j++) {
+                dy[j] = bf4_f32(pdy[j]);
+                xr[j] = px[j];
+                const float4 h = bf4_f32(pri[j]);
+                const uint32_t q = plo[j];
+                ri[j] = make_float4(lo8_decode(h.x, q), lo8_decode(h.y, q >> 8), lo8_decode(h.z, q >> 16),
+                                    lo8_decode(h.w, q >> 24));
+            }
+            const float mu = pmu, rs = prs;
+            {  // the next row of the sequence (the last one re-fetches itself: every load unconditional)
+                const int nt = i + 1 < RPW ? t : t + (int)gridDim.x;
+                const int nr_ = i + 1 < RPW ? i + 1 : 0;
+                fetch(nt < a.ntiles ? nt * TOK + wave * RPW + nr_ : tok);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            uint2* trow = reinterpret_cast<uint2*>(tile + r * C);
+            if (tok >= a.R) {  // padding row: zero tile row, zero row-form scales, no outputs
+#pragma unroll
+                for (int j = 0; j < NV; j++) {
+                    const int k = lane + 64 * j, kb = k >> 3;
+                    trow[k] = make_uint2(0u, 0u);
+                    if ((lane & 7) == 0)
+                        a.slr[((long long)(kb >> 1) * a.rgr_tot + (tok >> 5)) * 64 + (kb & 1) * 32 + (tok & 31)] = 0;
+                }
+                continue;
+            }
+            float4 nr[NV], dv[NV], w4[NV];  // the LN weight re-read per row (L1): registers go to the partials
+#pragma unroll
+            for (int j = 0; j < NV; j++) w4[j] = reinterpret_cast<const float4*>(a.w)[lane + 64 * j];
+            ln_bwd_row<NV>(dy, xr, w4, mu, rs, C, nr, dv);
+            const long long o = (long long)tok * C;
+#pragma unroll
+            for (int j = 0; j < NV; j++) {
+                const int k = lane + 64 * j, kb = k >> 3;
+                {
+                    float4 b = sp[wave][1][k], w = sp[wave][0][k];
+                    b.x += dy[j].x; b.y += dy[j].y; b.z += dy[j].z; b.w += dy[j].w;
+                    w.x += nr[j].x * dy[j].x; w.y += nr[j].y * dy[j].y;
+                    w.z += nr[j].z * dy[j].z; w.w += nr[j].w * dy[j].w;
+                    sp[wave][1][k] = b;
+                    sp[wave][0][k] = w;
+                }
+                const float4 tv = make_float4(ri[j].x + dv[j].x, ri[j].y + dv[j].y, ri[j].z + dv[j].z, ri[j].w + dv[j].w);
+                ps[j].x += tv.x; ps[j].y += tv.y; ps[j].z += tv.z; ps[j].w += tv.w;
+                const uint2 h = make_uint2(pack_bf16x2(tv.x, tv.y), pack_bf16x2(tv.z, tv.w));
+                reinterpret_cast<uint2*>(a.hi_out + o)[k] = h;
+                reinterpret_cast<uint32_t*>(a.lo_out + o)[k] =
+                    lo8_encode(tv.x, __uint_as_float(h.x << 16)) | (lo8_encode(tv.y, __uint_as_float(h.x & 0xffff0000u)) << 8) |
+                    (lo8_encode(tv.z, __uint_as_float(h.y << 16)) << 16) |
+                    (lo8_encode(tv.w, __uint_as_float(h.y & 0xffff0000u)) << 24);
+                trow[k] = h;
+                const float4 f = bf4_f32(h);
+                float amax = fmaxf(fmaxf(fabsf(f.x), fabsf(f.y)), fmaxf(fabsf(f.z), fabsf(f.w)));
+                amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+                amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+                amax = fmaxf(amax, __shfl_xor(amax, 4, 64));
+                const int sb = mx_scale_byte(amax);
+                if ((lane & 7) == 0)
+                    a.slr[((long long)(kb >> 1) * a.rgr_tot + (tok >> 5)) * 64 + (kb & 1) * 32 + (tok & 31)] = (uint8_t)sb;
+                const float inv = __uint_as_float((uint32_t)(254 - sb) << 23);
+                int q8 = __builtin_amdgcn_cvt_pk_fp8_f32(f.x * inv, f.y * inv, 0, false);
+                q8 = __builtin_amdgcn_cvt_pk_fp8_f32(f.z * inv, f.w * inv, q8, true);
+                reinterpret_cast<uint32_t*>(a.qr + o)[k] = (uint32_t)q8;
+            }
+        }
+        __syncthreads();
+        if (tok0 < a.ntok) {
+            const int kb = (a.tok_off + tok0) >> 5;
+            for (int c = tid; c < C; c += NT) {
+                float cv[TOK];
+                float amax = 0.f;
+#pragma unroll
+                for (int u = 0; u < TOK; u++) {
+                    cv[u] = __uint_as_float((uint32_t)tile[u * C + c] << 16);
+                    amax = fmaxf(amax, fabsf(cv[u]));
+                }
+                const int sb = mx_scale_byte(amax);
+                a.slc[((long long)(kb >> 1) * a.rgc_tot + (c >> 5)) * 64 + (kb & 1) * 32 + (c & 31)] = (uint8_t)sb;
+                const float inv = __uint_as_float((uint32_t)(254 - sb) << 23);
+                uint32_t wd[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    int q8 = __builtin_amdgcn_cvt_pk_fp8_f32(cv[4 * j] * inv, cv[4 * j + 1] * inv, 0, false);
+                    q8 = __builtin_amdgcn_cvt_pk_fp8_f32(cv[4 * j + 2] * inv, cv[4 * j + 3] * inv, q8, true);
+                    wd[j] = (uint32_t)q8;
+                }
+                uint8_t* dst = a.qc + (long long)c * a.ldqc + a.tok_off + tok0;
+                *reinterpret_cast<u32x4*>(dst) = u32x4{wd[0], wd[1], wd[2], wd[3]};
+                *reinterpret_cast<u32x4*>(dst + 16) = u32x4{wd[4], wd[5], wd[6], wd[7]};
+            }
+        }
+        __syncthreads();  // the tile is rewritten by the next one
+    }
+    // the 8 waves' column partials -> the workgroup's partial row, waves added in order 0 .. 7
+    float4* sps = reinterpret_cast<float4*>(tile);  // dres sums [8][NV * 64] (the tile is free after the loop)
+#pragma unroll
+    for (int j = 0; j < NV; j++) sps[wave * NV * 64 + lane + 64 * j] = ps[j];
+    __syncthreads();
+    float* prow = a.part + (long long)blockIdx.x * a.nsum;
+    for (int k = tid; k < NV * 64; k += NT) {
+        float4 w = sp[0][0][k], b = sp[0][1][k], z = sps[k];
+#pragma unroll
+        for (int u = 1; u < 8; u++) {
+            const float4 w2 = sp[u][0][k], b2 = sp[u][1][k], z2 = sps[u * NV * 64 + k];
+            w.x += w2.x; w.y += w2.y; w.z += w2.z; w.w += w2.w;
+            b.x += b2.x; b.y += b2.y; b.z += b2.z; b.w += b2.w;
+            z.x += z2.x; z.y += z2.y; z.z += z2.z; z.w += z2.w;
+        }
+        reinterpret_cast<float4*>(prow)[k] = w;
+        reinterpret_cast<float4*>(prow + C)[k] = b;
+        if (a.nsum == 3 * C) reinterpret_cast<float4*>(prow + 2 * C)[k] = z;
+    }
+    // the partial rows no workgroup owns (gridDim.x .. nparts-1) are zeros
+    for (int rr = (int)gridDim.x + (int)blockIdx.x; rr < a.nparts; rr += gridDim.x)
+        for (int i = tid; i < a.nsum; i += NT) a.part[(long long)rr * a.nsum + i] = 0.f;
+}
 }  // namespace f8
 
 long long mx_rows_padded(long long rows) { return (rows + 255) / 256 * 256; }
@@ -1071,6 +1267,51 @@ bool ln_forward_mx(uint8_t* qr, uint8_t* slr, uint8_t* qc, uint8_t* slc, float* 
     count_hit(VIT_HIT_LN_MX);
     return true;
 }
+bool ln_backward_mx_supported(int C) { return C % 256 == 0 && C >= 256 && C <= 1280; }
+bool ln_backward_bf16_stream_mx(bf16_t* dres_out, uint8_t* lo_out, const bf16_t* dres_in, const uint8_t* lo_in,
+                                float* dw, float* db, float* dres_colsum, const bf16_t* dout, const float* inp,
+                                const float* w, const float* mean, const float* rstd, long long R, int C,
+                                hipStream_t s, float* part, uint8_t* qr, uint8_t* slr, uint8_t* qc, uint8_t* slc,
+                                long long ldqc, long long tok_off, long long ntok) {
+    if (R <= 0) return true;
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    if (!ln_backward_mx_supported(C) || !dres_out || !lo_out || !dres_in || !lo_in || ldqc % 16 || tok_off % 64 ||
+        tok_off < 0 || ntok < R || ntok > mx_cols_kp(R) || tok_off + ntok > ldqc || !al16(dres_out) || !al16(dres_in) ||
+        !al16(dout) || !al16(inp) || !al16(w) || !al16(qr) || !al16(qc) || (((uintptr_t)lo_in | (uintptr_t)lo_out) & 3) ||
+        R >= (1LL << 30) || ldqc >= (1LL << 31)) {
+        set_error("layernorm_backward_mx: C in 256 .. 1280 (multiple of 256), tok_off %% 64, R <= ntok <= R rounded "
+                  "to 64, aligned planes required (C=%d R=%lld tok_off=%lld ntok=%lld ldqc=%lld)", C, R, tok_off, ntok, ldqc);
+        return false;
+    }
+    const int nsum = dres_colsum ? 3 * C : 2 * C, nparts = ln_bwd_blocks(R);
+    const bool reduce = part == nullptr;
+    if (reduce && !(part = (float*)workspace((size_t)nparts * nsum * sizeof(float)))) return false;
+    f8::LnbMx a;
+    a.hi_out = dres_out; a.lo_out = lo_out; a.hi_in = dres_in; a.lo_in = lo_in;
+    a.dout = dout; a.inp = inp; a.w = w; a.mean = mean; a.rstd = rstd;
+    a.part = part; a.nsum = nsum; a.nparts = nparts;
+    a.qr = qr; a.slr = slr; a.qc = qc; a.slc = slc;
+    const long long rp = mx_rows_padded(R);
+    a.R = (int)R; a.ntiles = (int)(rp / 32); a.rgr_tot = (int)(rp / 32);
+    a.tok_off = (int)tok_off; a.ntok = (int)ntok; a.rgc_tot = (int)(mx_rows_padded(C) / 32); a.ldqc = ldqc;
+    // one 8-wave workgroup per CU (80 KiB of LDS at C = 1280), persistent over the 32-token tiles
+    const int g = std::min(std::min(a.ntiles, gemm_cu_count()), nparts);
+    switch (C / 256) {
+        case 1: f8::ln_bwd_mx_k<1><<<g, 512, 0, s>>>(a); break;
+        case 2: f8::ln_bwd_mx_k<2><<<g, 512, 0, s>>>(a); break;
+        case 3: f8::ln_bwd_mx_k<3><<<g, 512, 0, s>>>(a); break;
+        case 4: f8::ln_bwd_mx_k<4><<<g, 512, 0, s>>>(a); break;
+        default: f8::ln_bwd_mx_k<5><<<g, 512, 0, s>>>(a); break;
+    }
+    after_launch("layernorm_backward_mx");
+    count_hit(VIT_HIT_LNB_MX);
+    if (reduce) {
+        const RowsJob jobs[3] = {{dw, part, nparts, nsum, C}, {db, part + C, nparts, nsum, C},
+                                 {dres_colsum, part + 2 * C, nparts, nsum, C}};
+        rows_reduce_add(jobs, dres_colsum ? 3 : 2, s);
+    }
+    return true;
+}
 void quantize_mx_batched_bf16(uint8_t* q, uint8_t* sl, const bf16_t* x, long long R, int K, int count,
                               long long xs, long long qs, long long ss, hipStream_t s) {
     quantize_mx<bf16_t>(q, sl, x, R, K, K, K, count, xs, qs, ss, s);
@@ -1101,6 +1342,21 @@ void quantize_mx_cols_bf16_ex(uint8_t* q, uint8_t* scales, const uint16_t* x, lo
 void quantize_mx_rowcol_bf16_ex(uint8_t* qr, uint8_t* scales_r, uint8_t* qc, uint8_t* scales_c, const uint16_t* x,
                                 long long R, int C, long long ldx, long long ldqc, long long tok_off, long long ntok) {
     quantize_mx_rowcol_bf16(qr, scales_r, qc, scales_c, (const bf16_t*)x, R, C, ldx, ldqc, tok_off, ntok, stream());
+}
+void layernorm_backward_stream(uint16_t* dres_out, uint8_t* lo_out, const uint16_t* dres_in, const uint8_t* lo_in,
+                               float* dweight, float* dbias, float* dres_colsum, const uint16_t* dout, const float* inp,
+                               const float* weight, const float* mean, const float* rstd, long long R, int C) {
+    ln_backward_bf16_stream((bf16_t*)dres_out, lo_out, (const bf16_t*)dres_in, lo_in, dweight, dbias, dres_colsum,
+                            (const bf16_t*)dout, inp, weight, mean, rstd, R, C, stream());
+}
+void layernorm_backward_stream_mx(uint16_t* dres_out, uint8_t* lo_out, const uint16_t* dres_in, const uint8_t* lo_in,
+                                  float* dweight, float* dbias, float* dres_colsum, const uint16_t* dout,
+                                  const float* inp, const float* weight, const float* mean, const float* rstd,
+                                  long long R, int C, uint8_t* qr, uint8_t* scales_r, uint8_t* qc, uint8_t* scales_c,
+                                  long long ldqc, long long tok_off, long long ntok) {
+    ln_backward_bf16_stream_mx((bf16_t*)dres_out, lo_out, (const bf16_t*)dres_in, lo_in, dweight, dbias, dres_colsum,
+                               (const bf16_t*)dout, inp, weight, mean, rstd, R, C, stream(), nullptr, qr, scales_r, qc,
+                               scales_c, ldqc, tok_off, ntok);
 }
 void layernorm_forward_mx(uint8_t* qr, uint8_t* scales_r, uint8_t* qc, uint8_t* scales_c, float* mean, float* rstd,
                           const float* inp, const float* weight, const float* bias, long long R, int C, long long ldqc,

@@ -289,16 +289,8 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_k(LnbIo io, const TD* __restri
         // keep the prefetch at the top: the scheduler otherwise sinks it to the end of the row to
         // reuse this row's registers, and the next iteration waits a full HBM round trip
         __builtin_amdgcn_sched_barrier(0);
-        float a = 0.f, bs = 0.f;
-#pragma unroll
-        for (int j = 0; j < NV; j++) {
-            const float4 x = xr[j];
-            nr[j] = make_float4((x.x - mu) * rs, (x.y - mu) * rs, (x.z - mu) * rs, (x.w - mu) * rs);
-            const float d0 = w4[j].x * dy[j].x, d1 = w4[j].y * dy[j].y, d2 = w4[j].z * dy[j].z, d3 = w4[j].w * dy[j].w;
-            a += (d0 + d1) + (d2 + d3);
-            bs += (d0 * nr[j].x + d1 * nr[j].y) + (d2 * nr[j].z + d3 * nr[j].w);
-        }
-        const float dm = warp_sum(a) / (float)C, dnm = warp_sum(bs) / (float)C;
+        float4 dvv[NV];
+        ln_bwd_row<NV>(dy, xr, w4, mu, rs, C, nr, dvv);  // ln_common.h (shared with ln_bwd_mx_k)
 #pragma unroll
         for (int j = 0; j < NV; j++) {
             const int k = lane + 64 * j;
@@ -310,11 +302,7 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_k(LnbIo io, const TD* __restri
                 pb[k] = b;
                 pw[k] = w;
             }
-            float4 dv;
-            dv.x = ((w4[j].x * dy[j].x - dm) - nr[j].x * dnm) * rs;
-            dv.y = ((w4[j].y * dy[j].y - dm) - nr[j].y * dnm) * rs;
-            dv.z = ((w4[j].z * dy[j].z - dm) - nr[j].z * dnm) * rs;
-            dv.w = ((w4[j].w * dy[j].w - dm) - nr[j].w * dnm) * rs;
+            const float4 dv = dvv[j];
             const float4 t = make_float4(ri[j].x + dv.x, ri[j].y + dv.y, ri[j].z + dv.z, ri[j].w + dv.w);
             if constexpr (ST) {
                 float4 u = ps[k];

@@ -404,6 +404,10 @@ struct Trainer {
     // fp8: LayerNorm forward straight into the MX forms (ln_forward_mx; VIT_FP8_LN_MX=0: bf16 + rowcol)
     bool ln_mx = true;
     bool lnmx_on() const { return rowcol_on() && ln_mx && ln_forward_mx_supported(C); }
+    // fp8: the residual-gradient LayerNorm backwards also write both MX forms of dres2 / dres3
+    // (ln_backward_bf16_stream_mx; VIT_FP8_LNB_MX=0 / option fp8_lnb_mx: the rowcol quantize instead)
+    bool lnb_mx = true;
+    bool lnbmx_on() const { return rowcol_on() && lnb_mx && ln_backward_mx_supported(C); }
     // the column-form span of micro-batch mb (R rows): the last one carries the padding tokens
     long long mb_ntok(int mb, long long R) const { return mb == nmb - 1 ? kp_tok - (long long)mb * R : R; }
     QMat fchgc_of(int l) const {
@@ -722,6 +726,8 @@ struct Trainer {
                     wg_b.s = alloc<uint8_t>((long long)mx_scale_bytes(4LL * C, (int)kp));
                     const char* lx = getenv("VIT_FP8_LN_MX");
                 ln_mx = !(lx && lx[0] == '0');
+                const char* lbx = getenv("VIT_FP8_LNB_MX");
+                lnb_mx = !(lbx && lbx[0] == '0');
                 const char* rc = getenv("VIT_FP8_ROWCOL");
                     rowcol_ok = !(rc && rc[0] == '0');
                     kp_tok = kp;
@@ -1157,6 +1163,9 @@ struct Trainer {
             // are issued after those dgrads (s2 waits on the event recorded after the quantize)
             const bool rc = rowcol_on();
             QMat c_ln1 = rc ? actc_of(0, l) : QMat{}, c_atty = rc ? actc_of(1, l) : QMat{}, c_ln2 = rc ? actc_of(2, l) : QMat{};
+            // lbm: the LayerNorm backwards write dres2 / dres3's MX forms (dres3 of the last layer comes
+            // from the head and is quantized by the fcproj dgrad as before)
+            const bool lbm = lnbmx_on(), resa_pre = lbm && l < L - 1;
             // fcproj: dfch = (dres3 . fcprojw) * gelu'(fch) (stored as fchd);  fcprojw += dres3^T . fchg
             const bool ec = epicol_on();
             QMat c_fchg = ec ? fchgc_of(l) : QMat{};
@@ -1174,7 +1183,8 @@ struct Trainer {
                     d1.C = nullptr;
                     d1.mxc_q = dfchc.q; d1.mxc_s = dfchc.s; d1.mxc_ld = kp_tok; d1.mxc_off = r0;
                 }
-                gemm_w(TC_FCPROJ_DGRAD, d1, P_FCPROJW, l, true, mb, ms[mb], PRE_NONE, fuse_mx, rc ? &dcol[0] : nullptr, EV_RESA);
+                gemm_w(TC_FCPROJ_DGRAD, d1, P_FCPROJW, l, true, mb, ms[mb], resa_pre ? PRE_LN : PRE_NONE, fuse_mx,
+                       rc && !resa_pre ? &dcol[0] : nullptr, resa_pre ? -1 : EV_RESA);
                 if (ec && two_streams) VIT_HIP(hipEventRecord(mev[mb][EV_DFCH], ms[mb]));  // dfchc final
             }
             if (rc) wgrad(TC_FCPROJ_WGRAD, rbA, C, a.fchg, 4 * C, G(P_FCPROJW, l), EV_RESA, EV_W1, &dcol[0],
@@ -1191,10 +1201,19 @@ struct Trainer {
                 // ln2 backward + residual: dres2 = dres3 + LN2'(dln2); attproj_b += colsum(dres2)
                 after_wgrad(EV_W3, ms[mb]);  // the previous layer's attproj wgrad has read rbB
                 tbeg(TC_LN_BWD, 0, ms[mb]);
-                ln_backward_bf16_stream(rbB + r0 * C, loB + r0 * C, rbA + r0 * C, loA + r0 * C, G(P_LN2W, l), G(P_LN2B, l),
-                                        G(P_ATTPROJB, l), dln_bf + r0 * C, a.res2 + r0 * C, P(P_LN2W, l),
-                                        a.ln2_mean + r0, a.ln2_rstd + r0, R, C, ms[mb],
-                                        sg_rows(l, sg_ln2) + (long long)mb * ln_bwd_blocks(R) * 3 * C);
+                if (lbm) {  // + dres2's MX forms (the attproj dgrad's A operand, the attproj wgrad's dout)
+                    ln_backward_bf16_stream_mx(rbB + r0 * C, loB + r0 * C, rbA + r0 * C, loA + r0 * C, G(P_LN2W, l),
+                                               G(P_LN2B, l), G(P_ATTPROJB, l), dln_bf + r0 * C, a.res2 + r0 * C,
+                                               P(P_LN2W, l), a.ln2_mean + r0, a.ln2_rstd + r0, R, C, ms[mb],
+                                               sg_rows(l, sg_ln2) + (long long)mb * ln_bwd_blocks(R) * 3 * C,
+                                               act_q[mb], act_s[mb], dcol[1].q, dcol[1].s, kp_tok, r0, mb_ntok(mb, R));
+                    if (two_streams) VIT_HIP(hipEventRecord(mev[mb][EV_RESB], ms[mb]));
+                } else {
+                    ln_backward_bf16_stream(rbB + r0 * C, loB + r0 * C, rbA + r0 * C, loA + r0 * C, G(P_LN2W, l),
+                                            G(P_LN2B, l), G(P_ATTPROJB, l), dln_bf + r0 * C, a.res2 + r0 * C,
+                                            P(P_LN2W, l), a.ln2_mean + r0, a.ln2_rstd + r0, R, C, ms[mb],
+                                            sg_rows(l, sg_ln2) + (long long)mb * ln_bwd_blocks(R) * 3 * C);
+                }
                 tend();
             }
             // attproj
@@ -1204,7 +1223,8 @@ struct Trainer {
                 GemmArgs d3;
                 d3.A = rbB + r0 * C; d3.lda = C; dgrad_b(d3, P_ATTPROJW, l, C, C);
                 d3.C = datty + r0 * C; d3.ldc = C; d3.M = (int)R; d3.N = C; d3.K = C; d3.epi = EPI_BF16_STORE;
-                gemm_w(TC_PROJ_DGRAD, d3, P_ATTPROJW, l, true, mb, ms[mb], PRE_NONE, false, rc ? &dcol[1] : nullptr, EV_RESB);
+                gemm_w(TC_PROJ_DGRAD, d3, P_ATTPROJW, l, true, mb, ms[mb], lbm ? PRE_LN : PRE_NONE, false,
+                       rc && !lbm ? &dcol[1] : nullptr, lbm ? -1 : EV_RESB);
                 // attention (+ qkv_b)
                 after_wgrad(EV_W4, ms[mb]);  // the previous layer's qkv wgrad has read dqkv
                 tbeg(TC_ATTN_BWD, 8.0 * Bm * (double)T * T * C, ms[mb]);
@@ -1226,10 +1246,19 @@ struct Trainer {
                 // ln1 backward: dres = dres2 + LN1'(dln1); fcproj_b of layer l-1 += colsum(dres)
                 after_wgrad(EV_W1, ms[mb]);  // this layer's fcproj wgrad has read rbA
                 tbeg(TC_LN_BWD, 0, ms[mb]);
-                ln_backward_bf16_stream(rbA + r0 * C, loA + r0 * C, rbB + r0 * C, loB + r0 * C, G(P_LN1W, l), G(P_LN1B, l),
-                                        l > 0 ? G(P_FCPROJB, l - 1) : nullptr, dln_bf + r0 * C, xl + r0 * C,
-                                        P(P_LN1W, l), a.ln1_mean + r0, a.ln1_rstd + r0, R, C, ms[mb],
-                                        sg_rows(l, sg_ln1) + (long long)mb * ln_bwd_blocks(R) * (l > 0 ? 3 : 2) * C);
+                if (lbm && l > 0) {  // + dres3's MX forms for layer l-1's fcproj dgrad / wgrad
+                    ln_backward_bf16_stream_mx(rbA + r0 * C, loA + r0 * C, rbB + r0 * C, loB + r0 * C, G(P_LN1W, l),
+                                               G(P_LN1B, l), G(P_FCPROJB, l - 1), dln_bf + r0 * C, xl + r0 * C,
+                                               P(P_LN1W, l), a.ln1_mean + r0, a.ln1_rstd + r0, R, C, ms[mb],
+                                               sg_rows(l, sg_ln1) + (long long)mb * ln_bwd_blocks(R) * 3 * C,
+                                               act_q[mb], act_s[mb], dcol[0].q, dcol[0].s, kp_tok, r0, mb_ntok(mb, R));
+                    if (two_streams) VIT_HIP(hipEventRecord(mev[mb][EV_RESA], ms[mb]));
+                } else {
+                    ln_backward_bf16_stream(rbA + r0 * C, loA + r0 * C, rbB + r0 * C, loB + r0 * C, G(P_LN1W, l),
+                                            G(P_LN1B, l), l > 0 ? G(P_FCPROJB, l - 1) : nullptr, dln_bf + r0 * C,
+                                            xl + r0 * C, P(P_LN1W, l), a.ln1_mean + r0, a.ln1_rstd + r0, R, C, ms[mb],
+                                            sg_rows(l, sg_ln1) + (long long)mb * ln_bwd_blocks(R) * (l > 0 ? 3 : 2) * C);
+                }
                 tend();
             }
             if (rc) wgrad(TC_QKV_WGRAD, dqkv, 3 * C, a.ln1, C, G(P_QKVW, l), EV_DQKV, EV_W4, &dcol[2], &c_ln1);
@@ -1818,6 +1847,8 @@ int vit_trainer_set_option(vit_trainer_t* h, const char* name, int value) {
         t.dgrad_wt = value != 0;
     } else if (n == "fp8_ln_mx") {  // fp8: LayerNorm forward into the MX forms (default 1)
         t.ln_mx = value != 0;
+    } else if (n == "fp8_lnb_mx") {  // fp8: the residual-gradient LayerNorm backwards write dres' MX forms (default 1)
+        t.lnb_mx = value != 0;
     } else if (n == "dp_probe") {
         if (value && !t.dp_snap) {  // allocated once, kept until destroy
             t.dp_snap = t.alloc<float>(t.arena_elems);
