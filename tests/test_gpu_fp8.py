@@ -381,14 +381,18 @@ def test_layernorm_forward_mx_bit_exact(gpu, R, C, parts):
 
 
 @pytest.mark.parametrize("R,C,parts,dsum", [(100, 256, 1, True), (197, 768, 1, False), (2 * 257 * 16, 1280, 2, True),
-                                             (1000, 1024, 2, True), (3 * 1024 + 70, 512, 3, True), (4001, 1280, 1, False)])
+                                             (1000, 1024, 2, True), (3 * 1024 + 70, 512, 3, True), (4001, 1280, 1, False),
+                                             (64 * 257, 1280, 1, True), (128 * 257, 768, 2, True)])
 def test_layernorm_backward_mx_bit_exact(gpu, R, C, parts, dsum):
     """The residual-gradient LayerNorm backward with both MX forms of its bf16 plane (the fp8 trainer's
     dres2 / dres3) against the unfused pair it replaces: layernorm_backward_stream (the trainer's
     ln_bwd_vec_k) then quantize_mx_rowcol_bf16_ex of its bf16 output.  The bf16 and lo8 planes, the
     row form (with the padding rows' zero scales) and the column form assembled over `parts`
     micro-batch slices are equal byte for byte; dW / db / dres column sums group their rows
-    differently (fixed order), so they agree to fp32 rounding (1e-5 of the column's magnitude)."""
+    differently (fixed order), so they agree to fp32 rounding (1e-5 of the column's magnitude).  The
+    ViT-H/14 micro-batch (16 448 rows: 520 tiles, more than one round on 256 CUs) and 32 896 rows in two
+    slices take the leftover-row path (the last partial round's rows spread over all workgroups, their
+    column form from the follow-up quantize)."""
     v = gpu
     rng = np.random.default_rng(R + 3 * C + parts)
     x = (rng.normal(size=(R, C)) * 2 + rng.normal(size=(R, 1))).astype(np.float32)

@@ -159,7 +159,10 @@ bool ln_backward_bf16_stream_mx(bf16_t* dres_out, uint8_t* lo_out, const bf16_t*
                                 float* dw, float* db, float* dres_colsum, const bf16_t* dout, const float* inp,
                                 const float* w, const float* mean, const float* rstd, long long R, int C,
                                 hipStream_t s, float* part, uint8_t* qr, uint8_t* slr, uint8_t* qc, uint8_t* slc,
-                                long long ldqc, long long tok_off, long long ntok);
+                                long long ldqc, long long tok_off, long long ntok, uint8_t* scratch);
+// bytes of the scratch ln_backward_bf16_stream_mx needs (nullptr there: the thread workspace; a caller
+// with work in flight on other streams passes its own)
+size_t ln_backward_mx_scratch_bytes(int C);
 bool ln_forward_mx(uint8_t* qr, uint8_t* slr, uint8_t* qc, uint8_t* slc, float* mean, float* rstd, const float* x,
                    const float* w, const float* b, long long R, int C, long long ldqc, long long tok_off, long long ntok,
                    hipStream_t s);

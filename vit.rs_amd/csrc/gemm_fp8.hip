@@ -880,7 +880,7 @@ struct LnbMx {
     float* part;
     int nsum, nparts;
     uint8_t *qr, *slr, *qc, *slc;
-    int R, ntiles, rgr_tot, tok_off, ntok, rgc_tot;
+    int R, ntiles, nmain, rgr_tot, tok_off, ntok, rgc_tot;
     long long ldqc;
 };
 __device__ __forceinline__ float4 bf4_f32(uint2 u) {
@@ -920,79 +920,83 @@ __global__ __launch_bounds__(512, 2) void ln_bwd_mx_k(LnbMx a) {
         pmu = a.mean[r];
         prs = a.rstd[r];
     };
+    // one row from the fetched registers (fetch() for the next row is issued by the caller's `next`
+    // before this row's arithmetic); trow: the row's LDS tile row, or nullptr (leftover rows)
+    auto do_row = [&](int tok, uint2* trow, int next) {
+        float4 dy[NV], xr[NV], ri[NV];
+#pragma unroll
+        for (int j = 0; j < NV; j++) {
+            dy[j] = bf4_f32(pdy[j]);
+            xr[j] = px[j];
+            const float4 h = bf4_f32(pri[j]);
+            const uint32_t q = plo[j];
+            ri[j] = make_float4(lo8_decode(h.x, q), lo8_decode(h.y, q >> 8), lo8_decode(h.z, q >> 16),
+                                lo8_decode(h.w, q >> 24));
+        }
+        const float mu = pmu, rs = prs;
+        if (next >= 0) fetch(next);
+        __builtin_amdgcn_sched_barrier(0);
+        if (tok >= a.R) {  // padding row: zero tile row, zero row-form scales, no outputs
+#pragma unroll
+            for (int j = 0; j < NV; j++) {
+                const int k = lane + 64 * j, kb = k >> 3;
+                if (trow) trow[k] = make_uint2(0u, 0u);
+                if ((lane & 7) == 0)
+                    a.slr[((long long)(kb >> 1) * a.rgr_tot + (tok >> 5)) * 64 + (kb & 1) * 32 + (tok & 31)] = 0;
+            }
+            return;
+        }
+        float4 nr[NV], dv[NV], w4[NV];  // the LN weight re-read per row (L1): registers go to the partials
+#pragma unroll
+        for (int j = 0; j < NV; j++) w4[j] = reinterpret_cast<const float4*>(a.w)[lane + 64 * j];
+        ln_bwd_row<NV>(dy, xr, w4, mu, rs, C, nr, dv);
+        const long long o = (long long)tok * C;
+#pragma unroll
+        for (int j = 0; j < NV; j++) {
+            const int k = lane + 64 * j, kb = k >> 3;
+            {
+                float4 b = sp[wave][1][k], w = sp[wave][0][k];
+                b.x += dy[j].x; b.y += dy[j].y; b.z += dy[j].z; b.w += dy[j].w;
+                w.x += nr[j].x * dy[j].x; w.y += nr[j].y * dy[j].y;
+                w.z += nr[j].z * dy[j].z; w.w += nr[j].w * dy[j].w;
+                sp[wave][1][k] = b;
+                sp[wave][0][k] = w;
+            }
+            const float4 tv = make_float4(ri[j].x + dv[j].x, ri[j].y + dv[j].y, ri[j].z + dv[j].z, ri[j].w + dv[j].w);
+            ps[j].x += tv.x; ps[j].y += tv.y; ps[j].z += tv.z; ps[j].w += tv.w;
+            const uint2 h = make_uint2(pack_bf16x2(tv.x, tv.y), pack_bf16x2(tv.z, tv.w));
+            reinterpret_cast<uint2*>(a.hi_out + o)[k] = h;
+            reinterpret_cast<uint32_t*>(a.lo_out + o)[k] =
+                lo8_encode(tv.x, __uint_as_float(h.x << 16)) | (lo8_encode(tv.y, __uint_as_float(h.x & 0xffff0000u)) << 8) |
+                (lo8_encode(tv.z, __uint_as_float(h.y << 16)) << 16) |
+                (lo8_encode(tv.w, __uint_as_float(h.y & 0xffff0000u)) << 24);
+            if (trow) trow[k] = h;
+            const float4 f = bf4_f32(h);
+            float amax = fmaxf(fmaxf(fabsf(f.x), fabsf(f.y)), fmaxf(fabsf(f.z), fabsf(f.w)));
+            amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+            amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+            amax = fmaxf(amax, __shfl_xor(amax, 4, 64));
+            const int sb = mx_scale_byte(amax);
+            if ((lane & 7) == 0)
+                a.slr[((long long)(kb >> 1) * a.rgr_tot + (tok >> 5)) * 64 + (kb & 1) * 32 + (tok & 31)] = (uint8_t)sb;
+            const float inv = __uint_as_float((uint32_t)(254 - sb) << 23);
+            int q8 = __builtin_amdgcn_cvt_pk_fp8_f32(f.x * inv, f.y * inv, 0, false);
+            q8 = __builtin_amdgcn_cvt_pk_fp8_f32(f.z * inv, f.w * inv, q8, true);
+            reinterpret_cast<uint32_t*>(a.qr + o)[k] = (uint32_t)q8;
+        }
+    };
+    // whole tiles: the first nmain (a multiple of gridDim.x: every workgroup takes the same number)
     int t = blockIdx.x;
-    if (t < a.ntiles) fetch(t * TOK + wave * RPW);
-    for (; t < a.ntiles; t += gridDim.x) {
+    if (t < a.nmain) fetch(t * TOK + wave * RPW);
+    for (; t < a.nmain; t += gridDim.x) {
         const int tok0 = t * TOK;
 #pragma unroll
         for (int i = 0; i < RPW; i++) {
             const int r = wave * RPW + i, tok = tok0 + r;
-            float4 dy[NV], xr[NV], ri[NV];
-#pragma unroll
-            for (int j = 0; j < NV; j++) {
-                dy[j] = bf4_f32(pdy[j]);
-                xr[j] = px[j];
-                const float4 h = bf4_f32(pri[j]);
-                const uint32_t q = plo[j];
-                ri[j] = make_float4(lo8_decode(h.x, q), lo8_decode(h.y, q >> 8), lo8_decode(h.z, q >> 16),
-                                    lo8_decode(h.w, q >> 24));
-            }
-            const float mu = pmu, rs = prs;
-            {  // the next row of the sequence (the last one re-fetches itself: every load unconditional)
-                const int nt = i + 1 < RPW ? t : t + (int)gridDim.x;
-                const int nr_ = i + 1 < RPW ? i + 1 : 0;
-                fetch(nt < a.ntiles ? nt * TOK + wave * RPW + nr_ : tok);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            uint2* trow = reinterpret_cast<uint2*>(tile + r * C);
-            if (tok >= a.R) {  // padding row: zero tile row, zero row-form scales, no outputs
-#pragma unroll
-                for (int j = 0; j < NV; j++) {
-                    const int k = lane + 64 * j, kb = k >> 3;
-                    trow[k] = make_uint2(0u, 0u);
-                    if ((lane & 7) == 0)
-                        a.slr[((long long)(kb >> 1) * a.rgr_tot + (tok >> 5)) * 64 + (kb & 1) * 32 + (tok & 31)] = 0;
-                }
-                continue;
-            }
-            float4 nr[NV], dv[NV], w4[NV];  // the LN weight re-read per row (L1): registers go to the partials
-#pragma unroll
-            for (int j = 0; j < NV; j++) w4[j] = reinterpret_cast<const float4*>(a.w)[lane + 64 * j];
-            ln_bwd_row<NV>(dy, xr, w4, mu, rs, C, nr, dv);
-            const long long o = (long long)tok * C;
-#pragma unroll
-            for (int j = 0; j < NV; j++) {
-                const int k = lane + 64 * j, kb = k >> 3;
-                {
-                    float4 b = sp[wave][1][k], w = sp[wave][0][k];
-                    b.x += dy[j].x; b.y += dy[j].y; b.z += dy[j].z; b.w += dy[j].w;
-                    w.x += nr[j].x * dy[j].x; w.y += nr[j].y * dy[j].y;
-                    w.z += nr[j].z * dy[j].z; w.w += nr[j].w * dy[j].w;
-                    sp[wave][1][k] = b;
-                    sp[wave][0][k] = w;
-                }
-                const float4 tv = make_float4(ri[j].x + dv[j].x, ri[j].y + dv[j].y, ri[j].z + dv[j].z, ri[j].w + dv[j].w);
-                ps[j].x += tv.x; ps[j].y += tv.y; ps[j].z += tv.z; ps[j].w += tv.w;
-                const uint2 h = make_uint2(pack_bf16x2(tv.x, tv.y), pack_bf16x2(tv.z, tv.w));
-                reinterpret_cast<uint2*>(a.hi_out + o)[k] = h;
-                reinterpret_cast<uint32_t*>(a.lo_out + o)[k] =
-                    lo8_encode(tv.x, __uint_as_float(h.x << 16)) | (lo8_encode(tv.y, __uint_as_float(h.x & 0xffff0000u)) << 8) |
-                    (lo8_encode(tv.z, __uint_as_float(h.y << 16)) << 16) |
-                    (lo8_encode(tv.w, __uint_as_float(h.y & 0xffff0000u)) << 24);
-                trow[k] = h;
-                const float4 f = bf4_f32(h);
-                float amax = fmaxf(fmaxf(fabsf(f.x), fabsf(f.y)), fmaxf(fabsf(f.z), fabsf(f.w)));
-                amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
-                amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
-                amax = fmaxf(amax, __shfl_xor(amax, 4, 64));
-                const int sb = mx_scale_byte(amax);
-                if ((lane & 7) == 0)
-                    a.slr[((long long)(kb >> 1) * a.rgr_tot + (tok >> 5)) * 64 + (kb & 1) * 32 + (tok & 31)] = (uint8_t)sb;
-                const float inv = __uint_as_float((uint32_t)(254 - sb) << 23);
-                int q8 = __builtin_amdgcn_cvt_pk_fp8_f32(f.x * inv, f.y * inv, 0, false);
-                q8 = __builtin_amdgcn_cvt_pk_fp8_f32(f.z * inv, f.w * inv, q8, true);
-                reinterpret_cast<uint32_t*>(a.qr + o)[k] = (uint32_t)q8;
-            }
+            // the next row of the sequence (the last one re-fetches itself: every load unconditional)
+            const int nt = i + 1 < RPW ? t : t + (int)gridDim.x;
+            const int nr_ = i + 1 < RPW ? i + 1 : 0;
+            do_row(tok, reinterpret_cast<uint2*>(tile + r * C), nt < a.nmain ? nt * TOK + wave * RPW + nr_ : tok);
         }
         __syncthreads();
         if (tok0 < a.ntok) {
@@ -1021,6 +1025,12 @@ __global__ __launch_bounds__(512, 2) void ln_bwd_mx_k(LnbMx a) {
             }
         }
         __syncthreads();  // the tile is rewritten by the next one
+    }
+    // the rows of the last, partial round of tiles: one row per wave across all workgroups (their
+    // column form is written by the launcher's follow-up quantize over these rows)
+    for (int q = a.nmain * TOK + (int)blockIdx.x * 8 + wave; q < a.ntiles * TOK; q += (int)gridDim.x * 8) {
+        fetch(q);
+        do_row(q, nullptr, -1);
     }
     // the 8 waves' column partials -> the workgroup's partial row, waves added in order 0 .. 7
     float4* sps = reinterpret_cast<float4*>(tile);  // dres sums [8][NV * 64] (the tile is free after the loop)
@@ -1268,11 +1278,17 @@ bool ln_forward_mx(uint8_t* qr, uint8_t* slr, uint8_t* qc, uint8_t* slc, float* 
     return true;
 }
 bool ln_backward_mx_supported(int C) { return C % 256 == 0 && C >= 256 && C <= 1280; }
+// the leftover rows' discarded row form (the follow-up quantize writes both forms): < 2 rounds of tiles
+static long long lnb_mx_scratch_rows() { return 2LL * gemm_cu_count() * 32; }
+size_t ln_backward_mx_scratch_bytes(int C) {
+    const long long r = lnb_mx_scratch_rows();
+    return (size_t)(r * C) + mx_scale_bytes(r, C) + 256;
+}
 bool ln_backward_bf16_stream_mx(bf16_t* dres_out, uint8_t* lo_out, const bf16_t* dres_in, const uint8_t* lo_in,
                                 float* dw, float* db, float* dres_colsum, const bf16_t* dout, const float* inp,
                                 const float* w, const float* mean, const float* rstd, long long R, int C,
                                 hipStream_t s, float* part, uint8_t* qr, uint8_t* slr, uint8_t* qc, uint8_t* slc,
-                                long long ldqc, long long tok_off, long long ntok) {
+                                long long ldqc, long long tok_off, long long ntok, uint8_t* scratch) {
     if (R <= 0) return true;
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     if (!ln_backward_mx_supported(C) || !dres_out || !lo_out || !dres_in || !lo_in || ldqc % 16 || tok_off % 64 ||
@@ -1285,7 +1301,13 @@ bool ln_backward_bf16_stream_mx(bf16_t* dres_out, uint8_t* lo_out, const bf16_t*
     }
     const int nsum = dres_colsum ? 3 * C : 2 * C, nparts = ln_bwd_blocks(R);
     const bool reduce = part == nullptr;
-    if (reduce && !(part = (float*)workspace((size_t)nparts * nsum * sizeof(float)))) return false;
+    const size_t part_bytes = ((size_t)nparts * nsum * sizeof(float) + 255) / 256 * 256;
+    if (reduce || !scratch) {  // the C-ABI path: partial rows and / or the scratch from the thread workspace
+        char* ws = (char*)workspace(part_bytes + (scratch ? 0 : ln_backward_mx_scratch_bytes(C)));
+        if (!ws) return false;
+        if (reduce) part = (float*)ws;
+        if (!scratch) scratch = (uint8_t*)(ws + part_bytes);
+    }
     f8::LnbMx a;
     a.hi_out = dres_out; a.lo_out = lo_out; a.hi_in = dres_in; a.lo_in = lo_in;
     a.dout = dout; a.inp = inp; a.w = w; a.mean = mean; a.rstd = rstd;
@@ -1294,8 +1316,16 @@ bool ln_backward_bf16_stream_mx(bf16_t* dres_out, uint8_t* lo_out, const bf16_t*
     const long long rp = mx_rows_padded(R);
     a.R = (int)R; a.ntiles = (int)(rp / 32); a.rgr_tot = (int)(rp / 32);
     a.tok_off = (int)tok_off; a.ntok = (int)ntok; a.rgc_tot = (int)(mx_rows_padded(C) / 32); a.ldqc = ldqc;
-    // one 8-wave workgroup per CU (80 KiB of LDS at C = 1280), persistent over the 32-token tiles
+    // one 8-wave workgroup per CU (160 KiB of LDS at C = 1280), persistent over the 32-token tiles.
+    // Whole rounds of tiles only (nmain, a multiple of g): the tiles of a last partial round would
+    // leave every other CU idle for a tile time (16 448 rows: 514 tiles on 256 CUs), so their rows are
+    // spread one per wave over all workgroups and their column form comes from a follow-up quantize.
     const int g = std::min(std::min(a.ntiles, gemm_cu_count()), nparts);
+    int nmain = a.ntiles / g * g;
+    // the follow-up needs at least one real row (it writes the padding tokens' zero blocks only then)
+    if (nmain < a.ntiles && (long long)nmain * 32 >= R && ntok > (long long)nmain * 32) nmain -= g;
+    a.nmain = nmain;
+    const long long r_left = (long long)nmain * 32;
     switch (C / 256) {
         case 1: f8::ln_bwd_mx_k<1><<<g, 512, 0, s>>>(a); break;
         case 2: f8::ln_bwd_mx_k<2><<<g, 512, 0, s>>>(a); break;
@@ -1305,6 +1335,16 @@ bool ln_backward_bf16_stream_mx(bf16_t* dres_out, uint8_t* lo_out, const bf16_t*
     }
     after_launch("layernorm_backward_mx");
     count_hit(VIT_HIT_LNB_MX);
+    if (r_left < R && r_left < ntok) {  // column form of the leftover rows (row form into the scratch)
+        if (R - r_left > lnb_mx_scratch_rows()) {
+            set_error("layernorm_backward_mx: %lld leftover rows exceed the scratch", R - r_left);
+            return false;
+        }
+        const long long rs = R - r_left;
+        if (!quantize_mx_rowcol_bf16(scratch, scratch + ((rs * C + 255) / 256 * 256), qc, slc, dres_out + r_left * C, rs,
+                                     C, C, ldqc, tok_off + r_left, ntok - r_left, s))
+            return false;
+    }
     if (reduce) {
         const RowsJob jobs[3] = {{dw, part, nparts, nsum, C}, {db, part + C, nparts, nsum, C},
                                  {dres_colsum, part + 2 * C, nparts, nsum, C}};
@@ -1356,7 +1396,7 @@ void layernorm_backward_stream_mx(uint16_t* dres_out, uint8_t* lo_out, const uin
                                   long long ldqc, long long tok_off, long long ntok) {
     ln_backward_bf16_stream_mx((bf16_t*)dres_out, lo_out, (const bf16_t*)dres_in, lo_in, dweight, dbias, dres_colsum,
                                (const bf16_t*)dout, inp, weight, mean, rstd, R, C, stream(), nullptr, qr, scales_r, qc,
-                               scales_c, ldqc, tok_off, ntok);
+                               scales_c, ldqc, tok_off, ntok, nullptr);
 }
 void layernorm_forward_mx(uint8_t* qr, uint8_t* scales_r, uint8_t* qc, uint8_t* scales_c, float* mean, float* rstd,
                           const float* inp, const float* weight, const float* bias, long long R, int C, long long ldqc,

@@ -407,6 +407,7 @@ struct Trainer {
     // fp8: the residual-gradient LayerNorm backwards also write both MX forms of dres2 / dres3
     // (ln_backward_bf16_stream_mx; VIT_FP8_LNB_MX=0 / option fp8_lnb_mx: the rowcol quantize instead)
     bool lnb_mx = true;
+    uint8_t* lnb_scr[4]{};  // per micro-batch stream: ln_backward_bf16_stream_mx's scratch
     bool lnbmx_on() const { return rowcol_on() && lnb_mx && ln_backward_mx_supported(C); }
     // the column-form span of micro-batch mb (R rows): the last one carries the padding tokens
     long long mb_ntok(int mb, long long R) const { return mb == nmb - 1 ? kp_tok - (long long)mb * R : R; }
@@ -743,6 +744,8 @@ struct Trainer {
                         fchgc.s = alloc<uint8_t>((long long)L * mx_scale_bytes(4LL * C, (int)kp));
                         dfchc.q = alloc<uint8_t>(4LL * C * kp);
                         dfchc.s = alloc<uint8_t>((long long)mx_scale_bytes(4LL * C, (int)kp));
+                        if (ln_backward_mx_supported(C))
+                            for (int k = 0; k < MAXMB; k++) lnb_scr[k] = alloc<uint8_t>((long long)ln_backward_mx_scratch_bytes(C));
                     }
                 }
             }
@@ -1206,7 +1209,8 @@ struct Trainer {
                                                G(P_LN2B, l), G(P_ATTPROJB, l), dln_bf + r0 * C, a.res2 + r0 * C,
                                                P(P_LN2W, l), a.ln2_mean + r0, a.ln2_rstd + r0, R, C, ms[mb],
                                                sg_rows(l, sg_ln2) + (long long)mb * ln_bwd_blocks(R) * 3 * C,
-                                               act_q[mb], act_s[mb], dcol[1].q, dcol[1].s, kp_tok, r0, mb_ntok(mb, R));
+                                               act_q[mb], act_s[mb], dcol[1].q, dcol[1].s, kp_tok, r0, mb_ntok(mb, R),
+                                               lnb_scr[mb]);
                     if (two_streams) VIT_HIP(hipEventRecord(mev[mb][EV_RESB], ms[mb]));
                 } else {
                     ln_backward_bf16_stream(rbB + r0 * C, loB + r0 * C, rbA + r0 * C, loA + r0 * C, G(P_LN2W, l),
@@ -1251,7 +1255,8 @@ struct Trainer {
                                                G(P_LN1B, l), G(P_FCPROJB, l - 1), dln_bf + r0 * C, xl + r0 * C,
                                                P(P_LN1W, l), a.ln1_mean + r0, a.ln1_rstd + r0, R, C, ms[mb],
                                                sg_rows(l, sg_ln1) + (long long)mb * ln_bwd_blocks(R) * 3 * C,
-                                               act_q[mb], act_s[mb], dcol[0].q, dcol[0].s, kp_tok, r0, mb_ntok(mb, R));
+                                               act_q[mb], act_s[mb], dcol[0].q, dcol[0].s, kp_tok, r0, mb_ntok(mb, R),
+                                               lnb_scr[mb]);
                     if (two_streams) VIT_HIP(hipEventRecord(mev[mb][EV_RESA], ms[mb]));
                 } else {
                     ln_backward_bf16_stream(rbA + r0 * C, loA + r0 * C, rbB + r0 * C, loB + r0 * C, G(P_LN1W, l),
