@@ -1541,9 +1541,18 @@ __global__ __launch_bounds__(NKT / KK * 64, 1) void attn_bwdp_k(bf16_t* __restri
                                                                const bf16_t* __restrict__ qkv,
                                                                const bf16_t* __restrict__ out,
                                                                const float* __restrict__ lse, int T,
-                                                               int C, int NH, int BH, float* __restrict__ dsum) {
+                                                               int C, int NH, int BH, float* __restrict__ dsum,
+                                                               int stagger) {
     using G = Geo<HS>;
     using Z = Bwdp<HS, NKT, KK>;
+    // stagger (100 MHz ticks, VIT_ATTN_STAGGER): every other CU of each XCD starts that much later, so
+    // the CUs' items do not all end (dK / dV store burst) at the same moment.  Measured (VERDICT r05
+    // item 3, B/16, two rounds): 0: 239.5 / 245.0 us, 400: 245.8 / 240.6, 870 (half an item): 248.0 /
+    // 248.0, 1300: 253.3 / 247.3 -- no gain (profiles/r06_attn_bwd_stagger.txt), so 0
+    if (stagger > 0 && ((blockIdx.x >> 3) & 1)) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)stagger) __builtin_amdgcn_s_sleep(8);
+    }
     constexpr int TP = Z::TP, NW = Z::NW, NT = Z::NT, NSL = Z::NSL, SK = Z::SK, SV = Z::SV, SL = Z::SL;
     static_assert((32 * G::CH) % 64 == 0 && NT % 64 == 0, "slice pieces are whole waves");
     constexpr int KS = G::KS, CH = G::CH, PER = Z::PER, PERS = Z::PERS;
@@ -1775,15 +1784,19 @@ int launch_bwd(bf16_t* dqkv, const bf16_t* dout, const bf16_t* qkv, const bf16_t
     if constexpr (bwdp_fits<HS, NK4, 4>()) {
         if (v == 4) {
             attn_bwdp_k<HS, NK4, 4><<<std::min(BH, attn_cu_count()), NK4 / 4 * 64, 0, s>>>(dqkv, dout, qkv, out, lse,
-                                                                                          T, C, NH, BH, part);
+                                                                                          T, C, NH, BH, part, 0);
             count_hit(VIT_HIT_ATTN_BWD_PERSISTENT);
             return NK4 / 4;
         }
     }
     if constexpr (bwdp_fits<HS, NKT, 2>()) {
         if (v == 0) {
+            static const int stagger = [] {
+                const char* e = getenv("VIT_ATTN_STAGGER");
+                return e ? atoi(e) : 0;
+            }();
             attn_bwdp_k<HS, NKT, 2><<<std::min(BH, attn_cu_count()), NKT / 2 * 64, 0, s>>>(dqkv, dout, qkv, out, lse,
-                                                                                         T, C, NH, BH, part);
+                                                                                         T, C, NH, BH, part, stagger);
             count_hit(VIT_HIT_ATTN_BWD_PERSISTENT);
             return NKT / 2;
         }
