@@ -329,7 +329,8 @@ def test_quantize_mx_rowcol_bit_exact(gpu, R, C, parts):
 
 
 @pytest.mark.parametrize("R,C,parts", [(100, 256, 1), (197, 768, 1), (2 * 257 * 16, 1280, 2), (1000, 1024, 2),
-                                        (3 * 1024 + 70, 512, 3), (300, 2048, 1), (4001, 1536, 1)])
+                                        (3 * 1024 + 70, 512, 3), (300, 2048, 1), (4001, 1536, 1), (64 * 257, 1280, 1),
+                                        (128 * 257, 768, 2)])
 def test_layernorm_forward_mx_bit_exact(gpu, R, C, parts):
     """LayerNorm straight into the MX forms (the fp8 trainer's ln1 / ln2) equals the unfused pair it
     replaces byte for byte: layernorm_forward_bf16 (its mean / rstd bit for bit too) and then
@@ -337,7 +338,9 @@ def test_layernorm_forward_mx_bit_exact(gpu, R, C, parts):
     the padding rows' zero scales), the column form assembled from `parts` slices (padding tokens
     of the last) against the same assembled by the unfused pair.  Inputs: rows of widely varying
     scale and offset, some constant rows (rstd = 1/sqrt(eps)), weights with zeros (zero blocks:
-    scale byte 127)."""
+    scale byte 127).  16 448 rows (520 tiles: more than the 512 slots) and 32 896 in two slices take
+    the leftover-row path (the last partial round's rows one per wave, their column form from a
+    follow-up quantize of their bf16 rows)."""
     v = gpu
     rng = np.random.default_rng(R + C + 5 * parts)
     x = (rng.normal(size=(R, C)) * np.exp2(rng.integers(-6, 6, size=(R, 1))) + rng.normal(size=(R, 1)) * 3).astype(np.float32)

@@ -163,9 +163,12 @@ bool ln_backward_bf16_stream_mx(bf16_t* dres_out, uint8_t* lo_out, const bf16_t*
 // bytes of the scratch ln_backward_bf16_stream_mx needs (nullptr there: the thread workspace; a caller
 // with work in flight on other streams passes its own)
 size_t ln_backward_mx_scratch_bytes(int C);
+// scratch: ln_mx_scratch_bytes(C) (the last partial round's rows; nullptr: no leftover path, every
+// tile through the LDS-tile kernel)
 bool ln_forward_mx(uint8_t* qr, uint8_t* slr, uint8_t* qc, uint8_t* slc, float* mean, float* rstd, const float* x,
                    const float* w, const float* b, long long R, int C, long long ldqc, long long tok_off, long long ntok,
-                   hipStream_t s);
+                   hipStream_t s, uint8_t* scratch);
+size_t ln_mx_scratch_bytes(int C);
 
 // column sums: dbias[n] += sum_m X[m*ld + n]   (X fp32 or bf16), in a fixed order: one pass when
 // M <= 256, else per-256-row partial rows in ws (nullptr = thread workspace; cdiv(M,256) * N

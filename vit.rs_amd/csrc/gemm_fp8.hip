@@ -743,15 +743,61 @@ __global__ __launch_bounds__(64 * 32 / RPW, (RPW == 2 || NV <= 5 ? 4 : 2)) void 
                                                    float* __restrict__ mean, float* __restrict__ rstd,
                                                    const float* __restrict__ x, const float* __restrict__ w,
                                                    const float* __restrict__ b, int R, int rgr_tot, long long ldqc,
-                                                   int tok_off, int ntok, int rgc_tot, int xmap) {
+                                                   int tok_off, int ntok, int rgc_tot, int xmap, int nmain,
+                                                   int ntiles, uint16_t* __restrict__ ybf) {
     constexpr int C = 256 * NV, TOK = 32, NT = 64 * TOK / RPW;
     __shared__ __attribute__((aligned(16))) uint16_t tile[TOK * C];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    if ((int)blockIdx.x >= nmain) {
+        // the rows of the last, partial round of tiles (one per wave; no tile): row form, mean /
+        // rstd, and the bf16 row into ybf for the launcher's follow-up column quantize
+        const int q = nmain * TOK + ((int)blockIdx.x - nmain) * (NT / 64) + wave;
+        if (q >= ntiles * TOK) return;
+        if (q >= R) {
+#pragma unroll
+            for (int j = 0; j < NV; j++) {
+                const int kb = (lane + 64 * j) >> 3;
+                if ((lane & 7) == 0) slr[((long long)(kb >> 1) * rgr_tot + (q >> 5)) * 64 + (kb & 1) * 32 + (q & 31)] = 0;
+            }
+            return;
+        }
+        float4 xv[NV];
+        const float4* x4 = reinterpret_cast<const float4*>(x + (long long)q * C);
+#pragma unroll
+        for (int j = 0; j < NV; j++) xv[j] = x4[lane + 64 * j];
+        float m, rs;
+        ln_vec_stats<NV>(xv, C, m, rs);
+#pragma unroll
+        for (int j = 0; j < NV; j++) {
+            const int k = lane + 64 * j, kb = k >> 3;
+            const float4 y = ln_vec_y(xv[j], reinterpret_cast<const float4*>(w)[k], reinterpret_cast<const float4*>(b)[k], m, rs);
+            const uint2 h = make_uint2(pack_bf16x2(y.x, y.y), pack_bf16x2(y.z, y.w));
+            reinterpret_cast<uint2*>(ybf + (long long)(q - nmain * TOK) * C)[k] = h;
+            const float f0 = __uint_as_float(h.x << 16), f1 = __uint_as_float(h.x & 0xffff0000u);
+            const float f2 = __uint_as_float(h.y << 16), f3 = __uint_as_float(h.y & 0xffff0000u);
+            float amax = fmaxf(fmaxf(fabsf(f0), fabsf(f1)), fmaxf(fabsf(f2), fabsf(f3)));
+            amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+            amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+            amax = fmaxf(amax, __shfl_xor(amax, 4, 64));
+            const int sb = mx_scale_byte(amax);
+            if ((lane & 7) == 0)
+                slr[((long long)(kb >> 1) * rgr_tot + (q >> 5)) * 64 + (kb & 1) * 32 + (q & 31)] = (uint8_t)sb;
+            const float inv = __uint_as_float((uint32_t)(254 - sb) << 23);
+            int t8 = __builtin_amdgcn_cvt_pk_fp8_f32(f0 * inv, f1 * inv, 0, false);
+            t8 = __builtin_amdgcn_cvt_pk_fp8_f32(f2 * inv, f3 * inv, t8, true);
+            reinterpret_cast<uint32_t*>(qr + (long long)q * C)[k] = (uint32_t)t8;
+        }
+        if (lane == 0) {
+            mean[q] = m;
+            rstd[q] = rs;
+        }
+        return;
+    }
     // xmap: within each group of 32 workgroups, the 4 tiles of one 128-token span go to workgroups
     // 8 apart (the same XCD, dispatched together), so the column form's 32-B pieces of a 128-B line
     // meet in one L2 instead of leaving four L2s as partial lines
     int t = blockIdx.x;
-    if (xmap && (blockIdx.x | 31) < gridDim.x) t = (blockIdx.x & ~31) + (blockIdx.x & 7) * 4 + ((blockIdx.x >> 3) & 3);
+    if (xmap && (int)(blockIdx.x | 31) < nmain) t = (blockIdx.x & ~31) + (blockIdx.x & 7) * 4 + ((blockIdx.x >> 3) & 3);
     const int tok0 = t * TOK;
     // row i + 1 in flight while row i reduces, row i + 2 requested once row i's inputs are dead
     // (clamped rows: unconditional loads).  A branch-free form (zero-selects, buffer stores that drop
@@ -1230,10 +1276,17 @@ bool quantize_mx_rowcol_bf16(uint8_t* qr, uint8_t* slr, uint8_t* qc, uint8_t* sl
     count_hit(VIT_HIT_QUANT_ROWCOL);
     return true;
 }
+// the leftover rows of the LayerNorm -> MX kernels (< 2 rounds of tiles on 2 workgroups per CU): their
+// bf16 rows (forward), the follow-up quantize's discarded row form and its scales
+static long long ln_mx_scratch_rows() { return 4LL * gemm_cu_count() * 32; }
+size_t ln_mx_scratch_bytes(int C) {
+    const long long r = ln_mx_scratch_rows();
+    return (size_t)(2 * r * C + 256) + (size_t)(r * C + 256) + mx_scale_bytes(r, C) + 256;
+}
 bool ln_forward_mx_supported(int C) { return C % 256 == 0 && C >= 256 && C <= 2048 && C != 1792; }
 bool ln_forward_mx(uint8_t* qr, uint8_t* slr, uint8_t* qc, uint8_t* slc, float* mean, float* rstd, const float* x,
                    const float* w, const float* b, long long R, int C, long long ldqc, long long tok_off, long long ntok,
-                   hipStream_t s) {
+                   hipStream_t s, uint8_t* scratch) {
     if (R <= 0) return true;
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     if (!ln_forward_mx_supported(C) || ldqc % 16 || tok_off % 64 || tok_off < 0 || ntok < R ||
@@ -1245,8 +1298,21 @@ bool ln_forward_mx(uint8_t* qr, uint8_t* slr, uint8_t* qc, uint8_t* slc, float* 
         return false;
     }
     const long long rp = mx_rows_padded(R);
-    const dim3 g((unsigned)(rp / 32));
     const int rgr = (int)(rp / 32), rgc = (int)(mx_rows_padded(C) / 32);
+    // whole rounds of tiles only (two 80-KiB workgroups per CU at 4 rows per wave, one at 2): 16 448 rows
+    // are 514 tiles for 512 slots, and the 2 of a second round would cost a whole tile time; the rows of
+    // a last partial round go one per wave to extra workgroups (row form, bf16 row into the scratch) and
+    // their column form comes from a follow-up quantize of those rows
+    static const int rpw_env = [] {
+        const char* e = getenv("VIT_LNMX_RPW");
+        return e && atoi(e) == 2 ? 2 : 4;
+    }();
+    const int ntiles = (int)(rp / 32), slots = gemm_cu_count() * (rpw_env == 2 ? 1 : 2);
+    int nmain = ntiles <= slots || !scratch ? ntiles : ntiles / slots * slots;
+    if (nmain < ntiles && (long long)nmain * 32 >= R && ntok > (long long)nmain * 32) nmain -= slots;
+    const long long r_left = (long long)nmain * 32;  // leftover rows: < 2 rounds of tiles <= ln_mx_scratch_rows()
+    uint16_t* ybf = reinterpret_cast<uint16_t*>(scratch);
+    const dim3 g((unsigned)(nmain + (ntiles - nmain) * 32 / (64 * 32 / rpw_env / 64)));
     static const int xmap = [] {
         const char* e = getenv("VIT_LNMX_XMAP");
         return e ? atoi(e) : 1;
@@ -1255,14 +1321,11 @@ bool ln_forward_mx(uint8_t* qr, uint8_t* slr, uint8_t* qc, uint8_t* slc, float* 
         const char* e = getenv("VIT_LNMX_WB");
         return !(e && e[0] == '0');
     }();
-    static const int rpw = [] {
-        const char* e = getenv("VIT_LNMX_RPW");
-        return e && atoi(e) == 2 ? 2 : 4;
-    }();
+    const int rpw = rpw_env;
     switch (C / 256) {
 #define VIT_LAUNCH(NV, WB, RPW) \
     f8::ln_fwd_mx_k<NV, WB, RPW><<<g, 64 * 32 / RPW, 0, s>>>(qr, slr, qc, slc, mean, rstd, x, w, b, (int)R, rgr, ldqc, \
-                                                             (int)tok_off, (int)ntok, rgc, xmap)
+                                                             (int)tok_off, (int)ntok, rgc, xmap, nmain, ntiles, ybf)
 #define VIT_CASE(NV) \
     case NV: \
         if (rpw == 2) { if (wb) VIT_LAUNCH(NV, true, 2); else VIT_LAUNCH(NV, false, 2); } \
@@ -1275,15 +1338,17 @@ bool ln_forward_mx(uint8_t* qr, uint8_t* slr, uint8_t* qc, uint8_t* slc, float* 
     }
     after_launch("ln_forward_mx");
     count_hit(VIT_HIT_LN_MX);
+    if (r_left < R && r_left < ntok) {  // column form of the leftover rows (their row form again into the scratch)
+        const long long rs = R - r_left;
+        uint8_t* sq = scratch + ((2 * rs * C + 255) / 256 * 256);
+        if (!quantize_mx_rowcol_bf16(sq, sq + ((rs * C + 255) / 256 * 256), qc, slc, reinterpret_cast<bf16_t*>(ybf), rs,
+                                     C, C, ldqc, tok_off + r_left, ntok - r_left, s))
+            return false;
+    }
     return true;
 }
 bool ln_backward_mx_supported(int C) { return C % 256 == 0 && C >= 256 && C <= 1280; }
-// the leftover rows' discarded row form (the follow-up quantize writes both forms): < 2 rounds of tiles
-static long long lnb_mx_scratch_rows() { return 2LL * gemm_cu_count() * 32; }
-size_t ln_backward_mx_scratch_bytes(int C) {
-    const long long r = lnb_mx_scratch_rows();
-    return (size_t)(r * C) + mx_scale_bytes(r, C) + 256;
-}
+size_t ln_backward_mx_scratch_bytes(int C) { return ln_mx_scratch_bytes(C); }
 bool ln_backward_bf16_stream_mx(bf16_t* dres_out, uint8_t* lo_out, const bf16_t* dres_in, const uint8_t* lo_in,
                                 float* dw, float* db, float* dres_colsum, const bf16_t* dout, const float* inp,
                                 const float* w, const float* mean, const float* rstd, long long R, int C,
@@ -1336,7 +1401,7 @@ bool ln_backward_bf16_stream_mx(bf16_t* dres_out, uint8_t* lo_out, const bf16_t*
     after_launch("layernorm_backward_mx");
     count_hit(VIT_HIT_LNB_MX);
     if (r_left < R && r_left < ntok) {  // column form of the leftover rows (row form into the scratch)
-        if (R - r_left > lnb_mx_scratch_rows()) {
+        if (R - r_left > ln_mx_scratch_rows()) {
             set_error("layernorm_backward_mx: %lld leftover rows exceed the scratch", R - r_left);
             return false;
         }
@@ -1401,7 +1466,8 @@ void layernorm_backward_stream_mx(uint16_t* dres_out, uint8_t* lo_out, const uin
 void layernorm_forward_mx(uint8_t* qr, uint8_t* scales_r, uint8_t* qc, uint8_t* scales_c, float* mean, float* rstd,
                           const float* inp, const float* weight, const float* bias, long long R, int C, long long ldqc,
                           long long tok_off, long long ntok) {
-    ln_forward_mx(qr, scales_r, qc, scales_c, mean, rstd, inp, weight, bias, R, C, ldqc, tok_off, ntok, stream());
+    ln_forward_mx(qr, scales_r, qc, scales_c, mean, rstd, inp, weight, bias, R, C, ldqc, tok_off, ntok, stream(),
+                  (uint8_t*)workspace(ln_mx_scratch_bytes(C)));
 }
 void gemm_fp8_fused_mx(void* C, void* C2, long long ldc, const void* aux, long long ldaux, const uint8_t* A,
                        const uint8_t* a_scale, long long lda, const uint8_t* B, const uint8_t* b_scale,

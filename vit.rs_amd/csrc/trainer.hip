@@ -407,7 +407,11 @@ struct Trainer {
     // fp8: the residual-gradient LayerNorm backwards also write both MX forms of dres2 / dres3
     // (ln_backward_bf16_stream_mx; VIT_FP8_LNB_MX=0 / option fp8_lnb_mx: the rowcol quantize instead)
     bool lnb_mx = true;
-    uint8_t* lnb_scr[4]{};  // per micro-batch stream: ln_backward_bf16_stream_mx's scratch
+    // option fp8_ln_leftover: the LayerNorm -> MX forward's leftover-row path.  Alone 36.4 -> 32.5 us per
+    // ViT-H/14 micro-batch (tools/bench_lnmx.py), in the step 119.70 vs 119.47 ms without it (the other
+    // micro-batch stream already fills the partial round): off
+    bool ln_left = false;
+    uint8_t* lnb_scr[4]{};  // per micro-batch stream: the LayerNorm -> MX kernels' scratch (ln_mx_scratch_bytes)
     bool lnbmx_on() const { return rowcol_on() && lnb_mx && ln_backward_mx_supported(C); }
     // the column-form span of micro-batch mb (R rows): the last one carries the padding tokens
     long long mb_ntok(int mb, long long R) const { return mb == nmb - 1 ? kp_tok - (long long)mb * R : R; }
@@ -744,8 +748,8 @@ struct Trainer {
                         fchgc.s = alloc<uint8_t>((long long)L * mx_scale_bytes(4LL * C, (int)kp));
                         dfchc.q = alloc<uint8_t>(4LL * C * kp);
                         dfchc.s = alloc<uint8_t>((long long)mx_scale_bytes(4LL * C, (int)kp));
-                        if (ln_backward_mx_supported(C))
-                            for (int k = 0; k < MAXMB; k++) lnb_scr[k] = alloc<uint8_t>((long long)ln_backward_mx_scratch_bytes(C));
+                        if (ln_backward_mx_supported(C) || ln_forward_mx_supported(C))
+                            for (int k = 0; k < MAXMB; k++) lnb_scr[k] = alloc<uint8_t>((long long)ln_mx_scratch_bytes(C));
                     }
                 }
             }
@@ -1015,7 +1019,8 @@ struct Trainer {
                 tbeg(TC_LN_FWD, 0, st);
                 if (lm)  // ln1 only in its two MX forms (the qkv GEMM's A operand, the qkv wgrad's B)
                     ln_forward_mx(act_q[mb], act_s[mb], c_ln1.q, c_ln1.s, a.ln1_mean + r0, a.ln1_rstd + r0, x,
-                                  P(P_LN1W, l), P(P_LN1B, l), R, C, kp_tok, r0, mb_ntok(mb, R), st);
+                                  P(P_LN1W, l), P(P_LN1B, l), R, C, kp_tok, r0, mb_ntok(mb, R), st,
+                                  ln_left ? lnb_scr[mb] : nullptr);
                 else
                     ln_forward_bf16(a.ln1 + r0 * C, a.ln1_mean + r0, a.ln1_rstd + r0, x, P(P_LN1W, l), P(P_LN1B, l), R, C, st);
                 tend();
@@ -1035,7 +1040,8 @@ struct Trainer {
                 tbeg(TC_LN_FWD, 0, st);
                 if (lm)
                     ln_forward_mx(act_q[mb], act_s[mb], c_ln2.q, c_ln2.s, a.ln2_mean + r0, a.ln2_rstd + r0,
-                                  a.res2 + r0 * C, P(P_LN2W, l), P(P_LN2B, l), R, C, kp_tok, r0, mb_ntok(mb, R), st);
+                                  a.res2 + r0 * C, P(P_LN2W, l), P(P_LN2B, l), R, C, kp_tok, r0, mb_ntok(mb, R), st,
+                                  ln_left ? lnb_scr[mb] : nullptr);
                 else
                     ln_forward_bf16(a.ln2 + r0 * C, a.ln2_mean + r0, a.ln2_rstd + r0, a.res2 + r0 * C, P(P_LN2W, l),
                                     P(P_LN2B, l), R, C, st);
@@ -1852,6 +1858,8 @@ int vit_trainer_set_option(vit_trainer_t* h, const char* name, int value) {
         t.dgrad_wt = value != 0;
     } else if (n == "fp8_ln_mx") {  // fp8: LayerNorm forward into the MX forms (default 1)
         t.ln_mx = value != 0;
+    } else if (n == "fp8_ln_leftover") {  // fp8: LayerNorm -> MX forward, last partial round as rows (default 0)
+        t.ln_left = value != 0;
     } else if (n == "fp8_lnb_mx") {  // fp8: the residual-gradient LayerNorm backwards write dres' MX forms (default 1)
         t.lnb_mx = value != 0;
     } else if (n == "dp_probe") {
