@@ -565,16 +565,35 @@ struct Trainer {
             return false;
         }
         if (hipSetDevice(dev) != hipSuccess) { set_error("trainer: hipSetDevice(%d)", dev); return false; }
-        VIT_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        // stream priorities (VIT_STREAM_PRIO overrides): 1 = micro-batch streams high, weight-gradient
+        // stream low; 2 = the reverse; 0 = all equal.  Measured (bench.py, three interleaved rounds each,
+        // profiles/r06_stream_prio.txt): ViT-B/16 bf16 2 vs 0: 7102-7106 vs 7059-7062 img/s (+0.65 %),
+        // 1: -0.2 %; ViT-H/14 fp8 2 vs 0: 1088 vs 1098 img/s (-0.8 %), 1: -2 %.  So 2 in bf16 mode
+        // (the weight gradients, which the next layer's all-reduce chunk waits for, go first), 0 in fp8
+        int prio_mode = prec == VIT_BF16 ? 2 : 0, p_lo = 0, p_hi = 0;
+        {
+            const char* e = getenv("VIT_STREAM_PRIO");
+            if (e) prio_mode = atoi(e);
+            if (prio_mode) VIT_HIP(hipDeviceGetStreamPriorityRange(&p_lo, &p_hi));
+        }
+        auto mk_stream = [&](hipStream_t* st, bool critical) {
+            if (!prio_mode) {
+                VIT_HIP(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
+            } else {
+                const bool hi = (prio_mode == 1) == critical;
+                VIT_HIP(hipStreamCreateWithPriority(st, hipStreamNonBlocking, hi ? p_hi : p_lo));
+            }
+        };
+        mk_stream(&s, true);
         VIT_HIP(hipStreamCreateWithFlags(&s_comm, hipStreamNonBlocking));
-        VIT_HIP(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+        mk_stream(&s2, false);
         {
             const char* e = getenv("VIT_BWD_STREAMS");
             two_streams = !(e && atoi(e) == 1);
         }
         for (auto& e : bev) VIT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         ms[0] = s;
-        for (int k = 1; k < MAXMB; k++) VIT_HIP(hipStreamCreateWithFlags(&ms[k], hipStreamNonBlocking));
+        for (int k = 1; k < MAXMB; k++) mk_stream(&ms[k], true);
         for (auto& row : mev)
             for (auto& e : row) VIT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         VIT_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
