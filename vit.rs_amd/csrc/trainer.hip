@@ -568,8 +568,8 @@ struct Trainer {
         // stream priorities (VIT_STREAM_PRIO overrides): 1 = micro-batch streams high, weight-gradient
         // stream low; 2 = the reverse; 0 = all equal.  Measured (bench.py, three interleaved rounds each,
         // profiles/r06_stream_prio.txt): ViT-B/16 bf16 2 vs 0: 7102-7106 vs 7059-7062 img/s (+0.65 %),
-        // 1: -0.2 %; ViT-H/14 fp8 2 vs 0: 1088 vs 1098 img/s (-0.8 %), 1: -2 %.  So 2 in bf16 mode
-        // (the weight gradients, which the next layer's all-reduce chunk waits for, go first), 0 in fp8
+        // 1: -0.2 %; ViT-H/14 fp8 2 vs 0: 1088 vs 1098 img/s (-0.8 %), 1: -2 %.  So 2 in bf16 mode and
+        // 0 in fp8 (a measured choice: which stream's kernels fill the others' partial rounds)
         int prio_mode = prec == VIT_BF16 ? 2 : 0, p_lo = 0, p_hi = 0;
         {
             const char* e = getenv("VIT_STREAM_PRIO");
