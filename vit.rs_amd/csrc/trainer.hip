@@ -576,24 +576,28 @@ struct Trainer {
             if (e) prio_mode = atoi(e);
             if (prio_mode) VIT_HIP(hipDeviceGetStreamPriorityRange(&p_lo, &p_hi));
         }
-        auto mk_stream = [&](hipStream_t* st, bool critical) {
+        // (3 / 4, A/B only: micro-batch stream 0 high and 1 low, the weight-gradient stream high / low)
+        auto mk_stream = [&](hipStream_t* st, int role) {  // role: 0 = micro-batch 0, 1 = other micro-batch, 2 = wgrad
             if (!prio_mode) {
                 VIT_HIP(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
             } else {
-                const bool hi = (prio_mode == 1) == critical;
+                bool hi;
+                if (prio_mode == 1) hi = role != 2;
+                else if (prio_mode == 2) hi = role == 2;
+                else hi = role == 0 || (role == 2 && prio_mode == 3);
                 VIT_HIP(hipStreamCreateWithPriority(st, hipStreamNonBlocking, hi ? p_hi : p_lo));
             }
         };
-        mk_stream(&s, true);
+        mk_stream(&s, 0);
         VIT_HIP(hipStreamCreateWithFlags(&s_comm, hipStreamNonBlocking));
-        mk_stream(&s2, false);
+        mk_stream(&s2, 2);
         {
             const char* e = getenv("VIT_BWD_STREAMS");
             two_streams = !(e && atoi(e) == 1);
         }
         for (auto& e : bev) VIT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         ms[0] = s;
-        for (int k = 1; k < MAXMB; k++) mk_stream(&ms[k], true);
+        for (int k = 1; k < MAXMB; k++) mk_stream(&ms[k], 1);
         for (auto& row : mev)
             for (auto& e : row) VIT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         VIT_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
