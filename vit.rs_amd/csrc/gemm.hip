@@ -1635,12 +1635,31 @@ static void launch_g4(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStre
 // split-K for two-workgroups-per-CU kernels: the smallest split whose last round fills >= 90% of
 // the 512 workgroup slots, keeping >= 32 K-steps per split
 static int choose_split_g4(int tiles, int nk) {
+    // slots the split-K work items are sized for (VIT_G4_SLOTS, A/B): 512 = both workgroups of every CU
+    static const int slots = [] {
+        const char* e = getenv("VIT_G4_SLOTS");
+        const int v = e ? atoi(e) : 512;
+        return v >= 64 && v <= 2048 ? v : 512;
+    }();
+    // r06 rule: the smallest split whose work items fill >= 80 % of the slots in ONE round.  The weight
+    // gradients run on their own stream beside the micro-batch streams, so a partly idle round costs
+    // less than the slab bytes (and the fixed-order reduce) of more splits: ViT-B/16 splits 9/26/7/7 ->
+    // 8/23/6/6 (qkv/proj/fc/fcproj), ViT-H/14 qkv 10 -> 3 (profiles/r06_g4_slots.txt).  VIT_G4_RULE=0:
+    // the round-5 rule below alone (best fill, multi-round allowed, first >= 90 %)
+    static const bool one_round = [] {
+        const char* e = getenv("VIT_G4_RULE");
+        return !(e && e[0] == '0');
+    }();
+    if (one_round) {
+        const int s1 = (int)((0.8 * slots + tiles - 1) / tiles);
+        if (s1 >= 1 && (long long)tiles * s1 <= slots && nk / s1 >= 32) return s1;
+    }
     int best = 1;
     double best_eff = 0.0;
     for (int s = 1; s <= 64 && nk / s >= 32; s++) {
         const int blocks = tiles * s;
-        const int rounds = (blocks + 511) / 512;
-        const double eff = (double)blocks / (rounds * 512.0) * (blocks >= 256 ? 1.0 : blocks / 256.0);
+        const int rounds = (blocks + slots - 1) / slots;
+        const double eff = (double)blocks / (rounds * (double)slots) * (blocks >= slots / 2 ? 1.0 : blocks / (slots / 2.0));
         if (eff > best_eff + 1e-9) { best_eff = eff; best = s; }
         if (eff >= 0.9) break;
     }

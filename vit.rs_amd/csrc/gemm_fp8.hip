@@ -1134,7 +1134,20 @@ void gemm_fp8(const GemmArgs& a, hipStream_t s) {
     GemmArgs b = a;
     float* slab = nullptr;
     if (a.epi == EPI_F32_ATOMIC) {
-        split = a.splitk > 0 ? a.splitk : choose_split_waves(tiles, a.K / f8::KB);
+        // the bf16 weight gradients' r06 rule (gemm.hip choose_split_g4): the smallest split filling
+        // >= 80 % of the 256 slots in one round, before the round-5 rule (ViT-H/14 fp8 qkv wgrad 10 -> 3
+        // splits, proj 10 -> 9: 1094 / 1091 vs 1081 / 1075 img/s, two interleaved rounds,
+        // profiles/r06_g4_slots.txt); VIT_F8_SPLIT_RULE=0: the round-5 rule alone
+        static const bool one_round = [] {
+            const char* e = getenv("VIT_F8_SPLIT_RULE");
+            return !(e && e[0] == '0');
+        }();
+        split = 0;
+        if (a.splitk <= 0 && one_round) {
+            const int nk = a.K / f8::KB, s1 = (int)((0.8 * 256 + tiles - 1) / tiles);
+            if (s1 >= 1 && tiles * s1 <= 256 && nk / s1 >= 16) split = s1;
+        }
+        if (!split) split = a.splitk > 0 ? a.splitk : choose_split_waves(tiles, a.K / f8::KB);
         if (split < 1) split = 1;
         const int kchunk = cdiv(cdiv(a.K, split), f8::KB) * f8::KB;
         split = cdiv(a.K, kchunk);
