@@ -1650,8 +1650,13 @@ static int choose_split_g4(int tiles, int nk) {
         const char* e = getenv("VIT_G4_RULE");
         return !(e && e[0] == '0');
     }();
+    static const double fill = [] {  // (VIT_G4_FILL, percent, A/B)
+        const char* e = getenv("VIT_G4_FILL");
+        const int v = e ? atoi(e) : 80;
+        return (v >= 30 && v <= 100 ? v : 80) / 100.0;
+    }();
     if (one_round) {
-        const int s1 = (int)((0.8 * slots + tiles - 1) / tiles);
+        const int s1 = (int)((fill * slots + tiles - 1) / tiles);
         if (s1 >= 1 && (long long)tiles * s1 <= slots && nk / s1 >= 32) return s1;
     }
     int best = 1;
