@@ -102,6 +102,7 @@ void gemm_set_variant(int v);
 void gemm_set_debug(int flags);
 // compute units of the current device: the persistent engines' grid (one workgroup per CU)
 int gemm_cu_count();
+int gemm_persist_grid();  // workgroups of the persistent engines (VIT_PERSIST_CUS; default gemm_cu_count())
 int gemm_variant_selected();  // the engine variant in effect (VIT_GEMM / gemm_set_variant)
 struct GemmParams;
 // variant 9: the one-wave-per-SIMD persistent engine (gemm_w4.hip) for K-contiguous operands without

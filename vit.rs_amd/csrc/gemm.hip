@@ -1352,6 +1352,15 @@ int gemm_cu_count() {
     }();
     return n;
 }
+// workgroups of the persistent GEMM engines (VIT_PERSIST_CUS, A/B): default one per CU
+int gemm_persist_grid() {
+    static const int n = [] {
+        const char* e = getenv("VIT_PERSIST_CUS");
+        const int v = e ? atoi(e) : 0;
+        return v >= 64 && v <= gemm_cu_count() ? v : gemm_cu_count();
+    }();
+    return n;
+}
 int gemm_variant_selected() { return gemm_variant(); }
 bool gemm_streaming() { return gemm_variant() == 7 || gemm_variant() == 9 || gemm_variant() == 10 || gemm_variant() == 11; }
 void gemm_set_debug(int flags) { g_debug_flags = flags; }
@@ -1551,7 +1560,7 @@ static void launch_g2(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStre
         if ((gemm_variant() == 7 || gemm_variant() == 10 || gemm_variant() == 11) && grid.y == 1 && p.K >= 2 * g2::BK &&
             (long long)p.M * p.lda * 2 < (1LL << 31) &&
             (long long)p.N * p.ldb * 2 < (1LL << 31)) {
-            const int cus = gemm_cu_count();
+            const int cus = gemm_persist_grid();
             const dim3 pg((int)grid.x < cus ? grid.x : cus);
             switch (a.epi) {
 #define VIT_CASE(E) \

@@ -1178,7 +1178,7 @@ void gemm_fp8(const GemmArgs& a, hipStream_t s) {
     if (split == 1 && gemm_streaming() && b.epi != EPI_F32_ACC && !epi_aux16(b.epi) && a.K >= 2 * f8::KB &&
         (long long)a.M * a.lda < (1LL << 31) &&
         (long long)a.N * a.ldb < (1LL << 31)) {
-        const int cus = gemm_cu_count();
+        const int cus = gemm_persist_grid();
         const dim3 pg(tiles < cus ? tiles : cus);
         switch (b.epi) {
 #define VIT_CASE(E) \
