@@ -1142,9 +1142,17 @@ void gemm_fp8(const GemmArgs& a, hipStream_t s) {
             const char* e = getenv("VIT_F8_SPLIT_RULE");
             return !(e && e[0] == '0');
         }();
+        // fill target 45 % (VIT_F8_FILL): ViT-H/14 fp8 80 -> 60 -> 45 -> 35 -> 25 %: 1091 -> 1103 -> 1108 ->
+        // 1103 -> 1092 img/s (interleaved rounds, profiles/r06_f8_fill.txt): half-filled rounds of fewer
+        // splits, the micro-batch streams' kernels beside them
+        static const double fill = [] {
+            const char* e = getenv("VIT_F8_FILL");
+            const int v = e ? atoi(e) : 45;
+            return (v >= 20 && v <= 100 ? v : 45) / 100.0;
+        }();
         split = 0;
         if (a.splitk <= 0 && one_round) {
-            const int nk = a.K / f8::KB, s1 = (int)((0.8 * 256 + tiles - 1) / tiles);
+            const int nk = a.K / f8::KB, s1 = (int)((fill * 256 + tiles - 1) / tiles);
             if (s1 >= 1 && tiles * s1 <= 256 && nk / s1 >= 16) split = s1;
         }
         if (!split) split = a.splitk > 0 ? a.splitk : choose_split_waves(tiles, a.K / f8::KB);
