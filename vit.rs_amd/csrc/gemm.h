@@ -57,6 +57,10 @@ struct GemmArgs {
     int M = 0, N = 0, K = 0;
     int epi = EPI_F32_STORE;
     int splitk = 0;  // 0 = choose automatically (only EPI_F32_ATOMIC may split)
+    // automatic split-K: the share of the engine's slots one round of work items should fill, percent
+    // (0 = the engine's default, 45: a weight gradient beside other streams; the trainer passes 80 when
+    // the kernel has the GPU to itself)
+    int fill_pct = 0;
     // split-K workspace for EPI_F32_ATOMIC on the 256x256 kernel: partials go to fp32 slabs and
     // one reduce kernel adds them into C (no atomics).  nullptr = the calling thread's workspace
     // (ordered on the context stream); the trainer passes its own buffer for its stream.

@@ -1643,7 +1643,7 @@ static void launch_g4(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStre
 
 // split-K for two-workgroups-per-CU kernels: the smallest split whose last round fills >= 90% of
 // the 512 workgroup slots, keeping >= 32 K-steps per split
-static int choose_split_g4(int tiles, int nk) {
+static int choose_split_g4(int tiles, int nk, int fill_pct = 0) {
     // slots the split-K work items are sized for (VIT_G4_SLOTS, A/B): 512 = both workgroups of every CU
     static const int slots = [] {
         const char* e = getenv("VIT_G4_SLOTS");
@@ -1667,7 +1667,8 @@ static int choose_split_g4(int tiles, int nk) {
         return (v >= 20 && v <= 100 ? v : 45) / 100.0;
     }();
     if (one_round) {
-        const int s1 = (int)((fill * slots + tiles - 1) / tiles);
+        const double f = fill_pct > 0 ? fill_pct / 100.0 : fill;
+        const int s1 = (int)((f * slots + tiles - 1) / tiles);
         if (s1 >= 1 && (long long)tiles * s1 <= slots && nk / s1 >= 32) return s1;
     }
     int best = 1;
@@ -1685,7 +1686,7 @@ static int choose_split_g4(int tiles, int nk) {
 static void gemm_bf16_g4(const GemmArgs& a, hipStream_t s) {
     const int tiles = cdiv(a.M, g4::BM) * cdiv(a.N, g4::BN);
     int split = 1;
-    if (a.epi == EPI_F32_ATOMIC) split = a.splitk > 0 ? a.splitk : choose_split_g4(tiles, a.K / g4::KTILE);
+    if (a.epi == EPI_F32_ATOMIC) split = a.splitk > 0 ? a.splitk : choose_split_g4(tiles, a.K / g4::KTILE, a.fill_pct);
     int kchunk = cdiv(cdiv(a.K, split), g4::KTILE) * g4::KTILE;
     split = cdiv(a.K, kchunk);
     GemmArgs b = a;

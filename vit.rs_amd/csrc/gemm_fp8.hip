@@ -1152,7 +1152,8 @@ void gemm_fp8(const GemmArgs& a, hipStream_t s) {
         }();
         split = 0;
         if (a.splitk <= 0 && one_round) {
-            const int nk = a.K / f8::KB, s1 = (int)((fill * 256 + tiles - 1) / tiles);
+            const double f = a.fill_pct > 0 ? a.fill_pct / 100.0 : fill;
+            const int nk = a.K / f8::KB, s1 = (int)((f * 256 + tiles - 1) / tiles);
             if (s1 >= 1 && tiles * s1 <= 256 && nk / s1 >= 16) split = s1;
         }
         if (!split) split = a.splitk > 0 ? a.splitk : choose_split_waves(tiles, a.K / f8::KB);

@@ -1103,6 +1103,10 @@ struct Trainer {
         w.B = inp; w.ldb = Cin; w.b_kcontig = false;
         w.C = dW; w.ldc = Cin; w.M = OC; w.N = Cin; w.K = (int)BT; w.epi = EPI_F32_ATOMIC;
         w.ws = gemm_ws; w.ws_bytes = gemm_ws_bytes;
+        // split-K fill: beside the micro-batch streams (concurrency on) the engine default (45 %: fewer
+        // splits, their half-filled rounds shared); alone on the GPU (concurrency off: the bench's
+        // per-kernel timing pass) 80 % of the slots
+        w.fill_pct = two_streams ? 0 : 80;
         hipStream_t st = two_streams ? s2 : s;
         if (two_streams) {
             for (int mb = 0; mb < nmb; mb++) {
