@@ -1641,8 +1641,9 @@ static void launch_g4(const GemmArgs& a, const GemmParams& p, dim3 grid, hipStre
     }
 }
 
-// split-K for two-workgroups-per-CU kernels: the smallest split whose last round fills >= 90% of
-// the 512 workgroup slots, keeping >= 32 K-steps per split
+// split-K for two-workgroups-per-CU kernels, keeping >= 32 K-steps per split: the one-round rule
+// below (fill_pct > 0: the caller's fill target, else VIT_G4_FILL), falling back to the best fill
+// over any number of rounds of the 512 workgroup slots
 static int choose_split_g4(int tiles, int nk, int fill_pct = 0) {
     // slots the split-K work items are sized for (VIT_G4_SLOTS, A/B): 512 = both workgroups of every CU
     static const int slots = [] {
