@@ -940,6 +940,17 @@ struct Trainer {
     }
 
     // ------------------------------------------------------------------ head (both modes)
+    // split-K of the M = B head GEMMs (bf16 / fp8 modes): about four 16-deep K-steps per work item.
+    // The engine's rule stops at >= 8 K-steps per split (192-256 workgroups of 12-16 dependent
+    // K-steps: 20-47 us per GEMM at B = 256, on the critical path between forward and backward);
+    // bounded by the slab workspace
+    bool head_sk = true;  // option head_splitk (A/B): 0 = the engine's split rule
+    int head_split(int M, int N, int K) const {
+        if (!head_sk) return 0;
+        int sp = std::min(16, std::max(1, K / 64));
+        while (sp > 1 && (size_t)sp * M * N * sizeof(float) > gemm_ws_bytes) sp--;
+        return sp;
+    }
     void head_forward() {
         tbeg(TC_HEAD, 2.0 * B * C * NC);
         // lnf on the CLS row of each image (D15)
@@ -951,10 +962,11 @@ struct Trainer {
         a.bias = P(P_HEADB); a.M = B; a.N = NC; a.K = C; a.epi = EPI_F32_STORE;
         if (lowp()) {
             // fast path: the M = B head GEMMs have 64 output tiles for 256 CUs, so they run
-            // split-K with float atomics onto the bias (fp32 mode keeps the ordered sums)
+            // split-K through fp32 slabs onto the broadcast bias (fp32 mode keeps the ordered sums)
             bcast_rows_k<<<cdiv((long long)B * NC, 256), 256, 0, s>>>(logits, P(P_HEADB), B, NC);
             a.bias = nullptr;
             a.epi = EPI_F32_ATOMIC;
+            a.splitk = head_split(a.M, a.N, a.K);
         }
         a.ws = gemm_ws; a.ws_bytes = gemm_ws_bytes;
         gemm_f32(a, s);
@@ -973,12 +985,14 @@ struct Trainer {
         a.A = dlogits; a.lda = NC; a.a_kcontig = true;
         a.B = P(P_HEADW); a.ldb = C; a.b_kcontig = false;
         a.C = dlnf; a.ldc = C; a.M = B; a.N = C; a.K = NC; a.epi = lowp() ? EPI_F32_ATOMIC : EPI_F32_ACC;
+        if (lowp()) a.splitk = head_split(a.M, a.N, a.K);
         a.ws = gemm_ws; a.ws_bytes = gemm_ws_bytes;
         gemm_f32(a, s);
         GemmArgs w;  // dhead_w += dlogits^T . lnf
         w.A = dlogits; w.lda = NC; w.a_kcontig = false;
         w.B = lnf; w.ldb = C; w.b_kcontig = false;
         w.C = G(P_HEADW); w.ldc = C; w.M = NC; w.N = C; w.K = B; w.epi = lowp() ? EPI_F32_ATOMIC : EPI_F32_ACC;
+        if (lowp()) w.splitk = head_split(w.M, w.N, w.K);
         w.ws = gemm_ws; w.ws_bytes = gemm_ws_bytes;
         gemm_f32(w, s);
         colsum_f32(G(P_HEADB), dlogits, B, NC, NC, s, red_ws);
@@ -1887,6 +1901,8 @@ int vit_trainer_set_option(vit_trainer_t* h, const char* name, int value) {
         t.ln_mx = value != 0;
     } else if (n == "fp8_ln_leftover") {  // fp8: LayerNorm -> MX forward, last partial round as rows (default 0)
         t.ln_left = value != 0;
+    } else if (n == "head_splitk") {  // bf16 / fp8: the head GEMMs' split-K at ~4 K-steps per item (default 1)
+        t.head_sk = value != 0;
     } else if (n == "fp8_lnb_mx") {  // fp8: the residual-gradient LayerNorm backwards write dres' MX forms (default 1)
         t.lnb_mx = value != 0;
     } else if (n == "dp_probe") {
