@@ -945,6 +945,9 @@ struct Trainer {
     // K-steps: 20-47 us per GEMM at B = 256, on the critical path between forward and backward);
     // bounded by the slab workspace
     bool head_sk = true;  // option head_splitk (A/B): 0 = the engine's split rule
+    // option patch_tail (A/B): the patch embedding backward after the join with its weight gradient
+    // split for 80 % of the slots and the small gradients on s2 beside it (0: 45 %, all on s)
+    bool patch_tail = true;
     int head_split(int M, int N, int K) const {
         if (!head_sk) return 0;
         int sp = std::min(16, std::max(1, K / 64));
@@ -1324,6 +1327,15 @@ struct Trainer {
         }
         // patch embedding backward (encoder_backward, train_vit.rs:371 -> ViT)
         tbeg(TC_PATCH_BWD, 2.0 * B * NP * (double)KP * C);
+        // cls / position / patch-bias gradients (psg: three small kernels, 43 us) on s2 beside the
+        // patch weight gradient on s; s waits for them before the chunk is final
+        const bool psg_side = two_streams && lowp() && patch_tail;
+        if (psg_side) {
+            VIT_HIP(hipEventRecord(bev[EV_SG], s));
+            VIT_HIP(hipStreamWaitEvent(s2, bev[EV_SG], 0));
+            patch_small_grads(G(P_CLS), G(P_WPE), G(P_PATCH_B), rbA, loA, B, T, C, s2, pos_sums, psg_part);
+            VIT_HIP(hipEventRecord(bev[EV_JOIN], s2));
+        }
         if (patch_f32) {
             patch_gather_f32(dpatch_f, rbA, loA, B, NP, C, s);
             GemmArgs w;
@@ -1337,6 +1349,9 @@ struct Trainer {
             w.B = patches_bf; w.ldb = KPP; w.b_kcontig = false;
             w.C = G(P_PATCH_W); w.ldc = KP; w.M = C; w.N = KP; w.K = B * NP; w.epi = EPI_F32_ATOMIC;
             w.ws = gemm_ws; w.ws_bytes = gemm_ws_bytes;
+            // after the join nothing but the small-gradient kernels runs beside it: split-K for 80 %
+            // of the slots (the 45 % default leaves half the CUs idle: 102 us with 234 workgroups)
+            w.fill_pct = patch_tail ? 80 : 0;
             if (patch_pad) {  // dW over KPP columns into the scratch, then its first KP columns into G
                 VIT_HIP(hipMemsetAsync(dwpatch_pad, 0, (size_t)C * KPP * 4, s));
                 w.C = dwpatch_pad; w.ldc = KPP; w.N = KPP;
@@ -1345,7 +1360,10 @@ struct Trainer {
             if (patch_pad)
                 add_cols_k<<<grid_for((long long)C * KP, 256), 256, 0, s>>>(G(P_PATCH_W), dwpatch_pad, C, KP, KPP);
         }
-        patch_small_grads(G(P_CLS), G(P_WPE), G(P_PATCH_B), rbA, loA, B, T, C, s, pos_sums, psg_part);
+        if (psg_side)
+            VIT_HIP(hipStreamWaitEvent(s, bev[EV_JOIN], 0));
+        else
+            patch_small_grads(G(P_CLS), G(P_WPE), G(P_PATCH_B), rbA, loA, B, T, C, s, pos_sums, psg_part);
         tend();
         chunk_done(L + 1);
     }
@@ -1901,6 +1919,8 @@ int vit_trainer_set_option(vit_trainer_t* h, const char* name, int value) {
         t.ln_mx = value != 0;
     } else if (n == "fp8_ln_leftover") {  // fp8: LayerNorm -> MX forward, last partial round as rows (default 0)
         t.ln_left = value != 0;
+    } else if (n == "patch_tail") {  // bf16 / fp8: patch embedding backward tail, see Trainer::patch_tail (default 1)
+        t.patch_tail = value != 0;
     } else if (n == "head_splitk") {  // bf16 / fp8: the head GEMMs' split-K at ~4 K-steps per item (default 1)
         t.head_sk = value != 0;
     } else if (n == "fp8_lnb_mx") {  // fp8: the residual-gradient LayerNorm backwards write dres' MX forms (default 1)
