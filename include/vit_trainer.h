@@ -119,6 +119,9 @@ int vit_trainer_set_concurrency(vit_trainer_t* t, int on);
  *      "fp8_lnb_mx" = 1 (default): ... and its residual-gradient LayerNorm backwards those of dres,
  *      "head_splitk" = 1 (default): bf16 / fp8 modes split the classifier head's GEMMs at about
  *      four K-steps per work item (0: the fp32 engine's own split rule),
+ *      "pre_side" = 1 (default): bf16 / fp8 modes with concurrency on clear the gradient arena
+ *      (vit_trainer_zero_grad) and refresh the transposed weight copies on the weight-gradient
+ *      stream beside the forward; the backward (and every host read) waits for them,
  *      "patch_tail" = 1 (default): bf16 / fp8 modes split the patch embedding's weight gradient for
  *      80 % of the GPU and run its small gradients on a second stream beside it (0: one stream, 45 %),
  *      "dp_probe" = 1: every gradient chunk is also copied, on the all-reduce stream right after

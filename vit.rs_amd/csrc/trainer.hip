@@ -232,7 +232,7 @@ struct Trainer {
     // attention kernels of the main stream (they only read activations and write grads)
     hipStream_t s2 = nullptr;
     bool two_streams = true;
-    enum BwdEv { EV_RESA, EV_RESB, EV_DFCH, EV_DQKV, EV_W1, EV_W2, EV_W3, EV_W4, EV_JOIN, EV_SG, EV_COUNT };
+    enum BwdEv { EV_RESA, EV_RESB, EV_DFCH, EV_DQKV, EV_W1, EV_W2, EV_W3, EV_W4, EV_JOIN, EV_SG, EV_PRE_IN, EV_PRE, EV_COUNT };
     hipEvent_t bev[EV_COUNT]{};
     // micro-batches: the batch is processed as NMB row ranges on NMB streams (ms[0] = s), so the
     // kernels of one half (GEMM epilogue bursts, LayerNorm, attention) overlap the other's GEMM
@@ -448,6 +448,7 @@ struct Trainer {
 
     // canonical <-> device copies (host staging)
     void canon_to_device(const float* host, float* dev) {
+        pre_side_wait();  // (the arena clear / transposes on s2 must not race this copy)
         std::vector<float> stage((size_t)arena_elems, 0.f);
         long long c = 0;
         for (int ti = 0; ti < 20; ti++) {
@@ -463,6 +464,7 @@ struct Trainer {
         VIT_HIP(hipStreamSynchronize(s));
     }
     void device_to_canon(const float* dev, float* host) {
+        pre_side_wait();
         std::vector<float> stage((size_t)arena_elems);
         VIT_HIP(hipMemcpyAsync(stage.data(), dev, arena_elems * 4, hipMemcpyDeviceToHost, s));
         VIT_HIP(hipStreamSynchronize(s));
@@ -847,8 +849,30 @@ struct Trainer {
         if (s2) (void)hipStreamDestroy(s2);
     }
 
+    // side pre-work (option pre_side, bf16 / fp8 with two streams, timing off): the gradient-arena
+    // clear and the transposed weight copies run on s2 beside the forward instead of ahead of it on s.
+    // pre_side_begin orders s2 after everything enqueued on s so far; pre_side_end records EV_PRE,
+    // which s waits for before the backward's first gradient write (backward_bf16)
+    bool pre_side = true;
+    bool pre_side_on() const { return pre_side && two_streams && lowp() && !timing && s2; }
+    hipStream_t pre_side_begin() {
+        VIT_HIP(hipEventRecord(bev[EV_PRE_IN], s));
+        VIT_HIP(hipStreamWaitEvent(s2, bev[EV_PRE_IN], 0));
+        return s2;
+    }
+    void pre_side_end() {
+        VIT_HIP(hipEventRecord(bev[EV_PRE], s2));
+        pre_pending = true;
+    }
+    bool pre_pending = false;
+    void pre_side_wait() {
+        if (!pre_pending) return;
+        VIT_HIP(hipStreamWaitEvent(s, bev[EV_PRE], 0));
+        pre_pending = false;
+    }
     void refresh_bf16() {
         if (!lowp()) return;
+        pre_side_wait();  // an earlier refresh's transposes on s2 still read pbf
         to_bf16_k<<<grid_for(arena_elems, 256), 256, 0, s>>>(pbf, params, arena_elems);
         after_launch("params_to_bf16");
         refresh_transposed();
@@ -859,13 +883,18 @@ struct Trainer {
         const int kinds[4] = {P_QKVW, P_ATTPROJW, P_FCW, P_FCPROJW};
         const int rows[4] = {3 * C, C, 4 * C, C}, cols[4] = {C, C, C, 4 * C};
         tbeg(TC_MISC, 0);
+        // only the backward's dgrads read the transposes: with side pre-work on they run on s2 beside
+        // the next forward (s waits for them at the start of the backward)
+        const bool side = pre_side_on() && !(fp8() && wt_cols);
+        hipStream_t ts = side ? pre_side_begin() : s;
         // fp8 mode reads no bf16 transposed copy (refresh_fp8 column-quantizes W for the dgrads)
         for (int k = 0; k < 4 && !(fp8() && wt_cols); k++) {
             const long long stride = L > 1 ? off[kinds[k] * L + 1] - off[kinds[k] * L] : 0;
             // negative stride: pass the lowest-addressed layer (layers are stored in reverse)
             const int l0 = stride < 0 ? L - 1 : 0;
-            transpose_bf16(WT(kinds[k], l0), W(kinds[k], l0), rows[k], cols[k], L, stride < 0 ? -stride : stride, s);
+            transpose_bf16(WT(kinds[k], l0), W(kinds[k], l0), rows[k], cols[k], L, stride < 0 ? -stride : stride, ts);
         }
+        if (side) pre_side_end();
         if (patch_pad)  // the patch weight's padded copy (columns KP .. KPP-1 stay zero)
             VIT_HIP(hipMemcpy2DAsync(wpatch_pad, (size_t)KPP * 2, W(P_PATCH_W), (size_t)KP * 2, (size_t)KP * 2, C,
                                      hipMemcpyDeviceToDevice, s));
@@ -1190,6 +1219,7 @@ struct Trainer {
     }
 
     void backward_bf16() {
+        pre_side_wait();  // the arena clear and the transposed weights (side pre-work on s2)
         // the residual-gradient stream is "bf16 + lo8" (common.h: a bf16 plane, the GEMM operand,
         // plus a byte plane of its rounding residual; a 16-bit significand in 3 bytes): dres3 (the
         // layer output's gradient) in rbA/loA, dres2 in rbB/loB; each LayerNorm backward reads one
@@ -1547,6 +1577,7 @@ struct Trainer {
     // AdamW update t = adam_t + 1 (llm.c's update, which the reference's m/v buffers —
     // train_vit.rs:73-74 — were allocated for; its optimizer_step :737 is SGD)
     void step_adamw(float lr, const vit_adamw_t& hp) {
+        pre_side_wait();
         finish_allreduce();
         if (!ensure_adam()) return;
         adam_t += 1;
@@ -1564,6 +1595,7 @@ struct Trainer {
     }
 
     void step(float lr) {
+        pre_side_wait();
         finish_allreduce();
         tbeg(TC_SGD, 0);
         if (lowp()) {
@@ -1689,7 +1721,13 @@ int vit_trainer_zero_grad(vit_trainer_t* h) {
         VIT_HIP(hipEventRecord(t.comm_done, t.s_comm));
         VIT_HIP(hipStreamWaitEvent(t.s, t.comm_done, 0));
     }
-    VIT_HIP(hipMemsetAsync(t.grads, 0, t.arena_elems * 4, t.s));
+    if (t.pre_side_on()) {  // on s2 beside the forward; the backward waits for it
+        hipStream_t zs = t.pre_side_begin();
+        VIT_HIP(hipMemsetAsync(t.grads, 0, t.arena_elems * 4, zs));
+        t.pre_side_end();
+    } else {
+        VIT_HIP(hipMemsetAsync(t.grads, 0, t.arena_elems * 4, t.s));
+    }
     return vit::has_error();
 }
 int vit_trainer_backward(vit_trainer_t* h) {
@@ -1824,6 +1862,7 @@ int vit_trainer_get_logits(vit_trainer_t* h, float* out) {
     return vit::has_error();
 }
 int vit_trainer_sync(vit_trainer_t* h) {
+    h->t.pre_side_wait();
     VIT_HIP(hipStreamSynchronize(h->t.s_comm));
     VIT_HIP(hipStreamSynchronize(h->t.s));
     return vit::has_error();
@@ -1919,6 +1958,9 @@ int vit_trainer_set_option(vit_trainer_t* h, const char* name, int value) {
         t.ln_mx = value != 0;
     } else if (n == "fp8_ln_leftover") {  // fp8: LayerNorm -> MX forward, last partial round as rows (default 0)
         t.ln_left = value != 0;
+    } else if (n == "pre_side") {  // bf16 / fp8: gradient clear + transposed weights on s2 beside the forward (default 1)
+        t.pre_side_wait();
+        t.pre_side = value != 0;
     } else if (n == "patch_tail") {  // bf16 / fp8: patch embedding backward tail, see Trainer::patch_tail (default 1)
         t.patch_tail = value != 0;
     } else if (n == "head_splitk") {  // bf16 / fp8: the head GEMMs' split-K at ~4 K-steps per item (default 1)
