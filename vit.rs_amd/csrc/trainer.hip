@@ -227,7 +227,7 @@ struct Trainer {
     long long chunk_off[VIT_MAX_LAYERS + 3]{};  // chunk c: [chunk_off[c], chunk_off[c+1]) ; c=0 head, 1..L layers L-1..0, L+1 embed
     int n_chunks = 0;
 
-    hipStream_t s = nullptr, s_comm = nullptr;
+    hipStream_t s = nullptr, s_comm = nullptr, s_opt = nullptr;
     // backward weight-gradient stream: the wgrad GEMMs of a layer run beside the dgrad / LN /
     // attention kernels of the main stream (they only read activations and write grads)
     hipStream_t s2 = nullptr;
@@ -505,6 +505,7 @@ struct Trainer {
         if (recs.empty()) return;
         VIT_HIP(hipStreamSynchronize(s));
         VIT_HIP(hipStreamSynchronize(s2));
+        VIT_HIP(hipStreamSynchronize(s_opt));
         for (int k = 1; k < MAXMB; k++) VIT_HIP(hipStreamSynchronize(ms[k]));
         for (auto& r : recs) {
             float ms = 0.f;
@@ -593,6 +594,7 @@ struct Trainer {
         mk_stream(&s, 0);
         VIT_HIP(hipStreamCreateWithFlags(&s_comm, hipStreamNonBlocking));
         mk_stream(&s2, 2);
+        mk_stream(&s_opt, 1);  // early SGD chunks: the micro-batch streams' priority
         {
             const char* e = getenv("VIT_BWD_STREAMS");
             two_streams = !(e && atoi(e) == 1);
@@ -830,6 +832,7 @@ struct Trainer {
         if (s) (void)hipStreamSynchronize(s);
         if (s_comm) (void)hipStreamSynchronize(s_comm);
         if (s2) (void)hipStreamSynchronize(s2);
+        if (s_opt) (void)hipStreamSynchronize(s_opt);
         for (int k = 1; k < MAXMB; k++) if (ms[k]) (void)hipStreamSynchronize(ms[k]);
         if (comm) ncclCommDestroy(comm);
         for (auto& a : allocs) (void)hipFree(a.p);
@@ -847,6 +850,7 @@ struct Trainer {
         if (s) (void)hipStreamDestroy(s);
         if (s_comm) (void)hipStreamDestroy(s_comm);
         if (s2) (void)hipStreamDestroy(s2);
+        if (s_opt) (void)hipStreamDestroy(s_opt);
     }
 
     // side pre-work (option pre_side, bf16 / fp8 with two streams, timing off): the gradient-arena
@@ -883,9 +887,10 @@ struct Trainer {
         const int kinds[4] = {P_QKVW, P_ATTPROJW, P_FCW, P_FCPROJW};
         const int rows[4] = {3 * C, C, 4 * C, C}, cols[4] = {C, C, C, 4 * C};
         tbeg(TC_MISC, 0);
-        // only the backward's dgrads read the transposes: with side pre-work on they run on s2 beside
-        // the next forward (s waits for them at the start of the backward)
-        const bool side = pre_side_on() && !(fp8() && wt_cols);
+        // bf16 mode: only the backward's dgrads read the transposes, so with side pre-work on they run
+        // on s2 beside the next forward (s waits for them at the start of the backward).  fp8 mode
+        // keeps them on s: refresh_fp8 below row-quantizes them (VIT_FP8_WT_COLS=0) right away
+        const bool side = pre_side_on() && !fp8();
         hipStream_t ts = side ? pre_side_begin() : s;
         // fp8 mode reads no bf16 transposed copy (refresh_fp8 column-quantizes W for the dgrads)
         for (int k = 0; k < 4 && !(fp8() && wt_cols); k++) {
@@ -1486,7 +1491,36 @@ struct Trainer {
     }
 
     // ------------------------------------------------------------------ DP
+    // Early SGD (option early_sgd, one GPU, bf16 / fp8, two streams, the fused train step): chunk c's
+    // gradients are final at chunk_done(c) (the DP overlap's ordering, checked bit-for-bit by the
+    // dp_probe test), and no later backward kernel reads chunk c's weights, so its SGD update runs
+    // on s_opt right there, beside the rest of the backward, instead of one 216 us pass after it.
+    // The update is elementwise: the same bits as the whole-arena pass.  step() then only waits.
+    // Measured (tools/ab_step.py, same process, profiles/r06_early_sgd_ab.txt): on s_comm ViT-B/16
+    // 35.57 vs 35.56 ms/step, ViT-H/14 fp8 114.68 vs 116.08; on its own stream, another box, -1.2 %
+    // on both: box-dependent, within +-1.2 %, so off by default
+    bool early_sgd = false;
+    bool early_on = false, early_done = false;
+    float early_lr = 0.f;
+    void sgd_chunk(int c) {
+        VIT_HIP(hipEventRecord(chunk_ev[c], s));
+        VIT_HIP(hipStreamWaitEvent(s_opt, chunk_ev[c], 0));
+        VIT_HIP(hipEventRecord(chunk_ev2[c], s2));
+        VIT_HIP(hipStreamWaitEvent(s_opt, chunk_ev2[c], 0));
+        for (int k = 1; k < nmb; k++) {
+            hipEvent_t e = chunk_evm[(size_t)c * MAXMB + k];
+            VIT_HIP(hipEventRecord(e, ms[k]));
+            VIT_HIP(hipStreamWaitEvent(s_opt, e, 0));
+        }
+        const long long o = chunk_off[c], n = chunk_off[c + 1] - chunk_off[c];
+        sgd_bf16_k<<<grid_for(n / 4, 256), 256, 0, s_opt>>>(params + o, pbf + o, grads + o, n, early_lr);
+        after_launch("sgd_bf16_chunk");
+    }
     void chunk_done(int c) {
+        if (early_on) {
+            sgd_chunk(c);
+            return;
+        }
         if (!comm || !overlap) return;
         VIT_HIP(hipEventRecord(chunk_ev[c], s));
         VIT_HIP(hipStreamWaitEvent(s_comm, chunk_ev[c], 0));
@@ -1596,6 +1630,13 @@ struct Trainer {
 
     void step(float lr) {
         pre_side_wait();
+        if (early_done) {  // every chunk already updated on s_opt (train_step with early SGD)
+            early_done = false;
+            VIT_HIP(hipEventRecord(comm_done, s_opt));
+            VIT_HIP(hipStreamWaitEvent(s, comm_done, 0));
+            refresh_transposed();
+            return;
+        }
         finish_allreduce();
         tbeg(TC_SGD, 0);
         if (lowp()) {
@@ -1744,9 +1785,15 @@ int vit_trainer_step(vit_trainer_t* h, float lr) {
     return vit::has_error();
 }
 int vit_trainer_train_step(vit_trainer_t* h, float lr, int b_global) {
+    auto& t = h->t;
     vit_trainer_zero_grad(h);
     vit_trainer_forward(h, b_global);
+    // the fused step knows lr before the backward: SGD per finished chunk (Trainer::early_sgd)
+    t.early_on = t.early_sgd && t.lowp() && !t.comm && t.two_streams && !t.timing && t.s2 && t.has_targets;
+    t.early_lr = lr;
     vit_trainer_backward(h);
+    t.early_done = t.early_on && !vit::has_error();
+    t.early_on = false;
     vit_trainer_step(h, lr);
     return vit::has_error();
 }
@@ -1958,6 +2005,8 @@ int vit_trainer_set_option(vit_trainer_t* h, const char* name, int value) {
         t.ln_mx = value != 0;
     } else if (n == "fp8_ln_leftover") {  // fp8: LayerNorm -> MX forward, last partial round as rows (default 0)
         t.ln_left = value != 0;
+    } else if (n == "early_sgd") {  // bf16 / fp8, one GPU: SGD per finished gradient chunk inside train_step (default 0)
+        t.early_sgd = value != 0;
     } else if (n == "pre_side") {  // bf16 / fp8: gradient clear + transposed weights on s2 beside the forward (default 1)
         t.pre_side_wait();
         t.pre_side = value != 0;
