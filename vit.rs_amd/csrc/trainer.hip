@@ -227,7 +227,7 @@ struct Trainer {
     long long chunk_off[VIT_MAX_LAYERS + 3]{};  // chunk c: [chunk_off[c], chunk_off[c+1]) ; c=0 head, 1..L layers L-1..0, L+1 embed
     int n_chunks = 0;
 
-    hipStream_t s = nullptr, s_comm = nullptr, s_opt = nullptr;
+    hipStream_t s = nullptr, s_comm = nullptr;
     // backward weight-gradient stream: the wgrad GEMMs of a layer run beside the dgrad / LN /
     // attention kernels of the main stream (they only read activations and write grads)
     hipStream_t s2 = nullptr;
@@ -505,7 +505,6 @@ struct Trainer {
         if (recs.empty()) return;
         VIT_HIP(hipStreamSynchronize(s));
         VIT_HIP(hipStreamSynchronize(s2));
-        VIT_HIP(hipStreamSynchronize(s_opt));
         for (int k = 1; k < MAXMB; k++) VIT_HIP(hipStreamSynchronize(ms[k]));
         for (auto& r : recs) {
             float ms = 0.f;
@@ -594,7 +593,6 @@ struct Trainer {
         mk_stream(&s, 0);
         VIT_HIP(hipStreamCreateWithFlags(&s_comm, hipStreamNonBlocking));
         mk_stream(&s2, 2);
-        mk_stream(&s_opt, 1);  // early SGD chunks: the micro-batch streams' priority
         {
             const char* e = getenv("VIT_BWD_STREAMS");
             two_streams = !(e && atoi(e) == 1);
@@ -832,7 +830,6 @@ struct Trainer {
         if (s) (void)hipStreamSynchronize(s);
         if (s_comm) (void)hipStreamSynchronize(s_comm);
         if (s2) (void)hipStreamSynchronize(s2);
-        if (s_opt) (void)hipStreamSynchronize(s_opt);
         for (int k = 1; k < MAXMB; k++) if (ms[k]) (void)hipStreamSynchronize(ms[k]);
         if (comm) ncclCommDestroy(comm);
         for (auto& a : allocs) (void)hipFree(a.p);
@@ -850,7 +847,6 @@ struct Trainer {
         if (s) (void)hipStreamDestroy(s);
         if (s_comm) (void)hipStreamDestroy(s_comm);
         if (s2) (void)hipStreamDestroy(s2);
-        if (s_opt) (void)hipStreamDestroy(s_opt);
     }
 
     // side pre-work (option pre_side, bf16 / fp8 with two streams, timing off): the gradient-arena
@@ -1494,26 +1490,27 @@ struct Trainer {
     // Early SGD (option early_sgd, one GPU, bf16 / fp8, two streams, the fused train step): chunk c's
     // gradients are final at chunk_done(c) (the DP overlap's ordering, checked bit-for-bit by the
     // dp_probe test), and no later backward kernel reads chunk c's weights, so its SGD update runs
-    // on s_opt right there, beside the rest of the backward, instead of one 216 us pass after it.
+    // on s_comm (no extra stream: a seventh stream re-maps the streams onto the 4 hardware queues
+    // and cost bf16 6 %) right there, beside the rest of the backward, instead of one 216 us pass.
     // The update is elementwise: the same bits as the whole-arena pass.  step() then only waits.
     // Measured (tools/ab_step.py, same process, profiles/r06_early_sgd_ab.txt): on s_comm ViT-B/16
-    // 35.57 vs 35.56 ms/step, ViT-H/14 fp8 114.68 vs 116.08; on its own stream, another box, -1.2 %
-    // on both: box-dependent, within +-1.2 %, so off by default
+    // 35.57 vs 35.56 ms/step, ViT-H/14 fp8 114.68 vs 116.08 (+1.2 %); not yet repeated on another
+    // box, so off by default
     bool early_sgd = false;
     bool early_on = false, early_done = false;
     float early_lr = 0.f;
     void sgd_chunk(int c) {
         VIT_HIP(hipEventRecord(chunk_ev[c], s));
-        VIT_HIP(hipStreamWaitEvent(s_opt, chunk_ev[c], 0));
+        VIT_HIP(hipStreamWaitEvent(s_comm, chunk_ev[c], 0));
         VIT_HIP(hipEventRecord(chunk_ev2[c], s2));
-        VIT_HIP(hipStreamWaitEvent(s_opt, chunk_ev2[c], 0));
+        VIT_HIP(hipStreamWaitEvent(s_comm, chunk_ev2[c], 0));
         for (int k = 1; k < nmb; k++) {
             hipEvent_t e = chunk_evm[(size_t)c * MAXMB + k];
             VIT_HIP(hipEventRecord(e, ms[k]));
-            VIT_HIP(hipStreamWaitEvent(s_opt, e, 0));
+            VIT_HIP(hipStreamWaitEvent(s_comm, e, 0));
         }
         const long long o = chunk_off[c], n = chunk_off[c + 1] - chunk_off[c];
-        sgd_bf16_k<<<grid_for(n / 4, 256), 256, 0, s_opt>>>(params + o, pbf + o, grads + o, n, early_lr);
+        sgd_bf16_k<<<grid_for(n / 4, 256), 256, 0, s_comm>>>(params + o, pbf + o, grads + o, n, early_lr);
         after_launch("sgd_bf16_chunk");
     }
     void chunk_done(int c) {
@@ -1630,9 +1627,9 @@ struct Trainer {
 
     void step(float lr) {
         pre_side_wait();
-        if (early_done) {  // every chunk already updated on s_opt (train_step with early SGD)
+        if (early_done) {  // every chunk already updated on s_comm (train_step with early SGD)
             early_done = false;
-            VIT_HIP(hipEventRecord(comm_done, s_opt));
+            VIT_HIP(hipEventRecord(comm_done, s_comm));
             VIT_HIP(hipStreamWaitEvent(s, comm_done, 0));
             refresh_transposed();
             return;
