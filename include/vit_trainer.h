@@ -119,7 +119,7 @@ int vit_trainer_set_concurrency(vit_trainer_t* t, int on);
  *      "fp8_lnb_mx" = 1 (default): ... and its residual-gradient LayerNorm backwards those of dres,
  *      "head_splitk" = 1 (default): bf16 / fp8 modes split the classifier head's GEMMs at about
  *      four K-steps per work item (0: the fp32 engine's own split rule),
- *      "early_sgd" = 0 (default; 1 = measured neutral within +-1.2 %, box-dependent): one GPU, bf16 / fp8, concurrency on: vit_trainer_train_step
+ *      "early_sgd" = -1 (default: on in fp8 mode, off in bf16; measured per dtype): one GPU, bf16 / fp8, concurrency on: vit_trainer_train_step
  *      updates each gradient chunk (head, layer L-1 .. 0, embedding) as soon as the backward has
  *      finished it, on a side stream beside the rest of the backward (same bits as one pass),
  *      "pre_side" = 1 (default): bf16 / fp8 modes with concurrency on clear the gradient arena

@@ -1494,9 +1494,10 @@ struct Trainer {
     // and cost bf16 6 %) right there, beside the rest of the backward, instead of one 216 us pass.
     // The update is elementwise: the same bits as the whole-arena pass.  step() then only waits.
     // Measured (tools/ab_step.py, same process, profiles/r06_early_sgd_ab.txt): on s_comm ViT-B/16
-    // 35.57 vs 35.56 ms/step, ViT-H/14 fp8 114.68 vs 116.08 (+1.2 %); not yet repeated on another
-    // box, so off by default
-    bool early_sgd = false;
+    // 35.57 vs 35.56 and 35.65 vs 35.54 ms/step (-0.2 %), ViT-L/16 114.47 vs 114.79 (+0.3 %), ViT-H/14
+    // fp8 114.68 vs 116.08 and 114.99 vs 115.72 (+1.2 / +0.6 %) on two boxes: on in fp8 mode (-1: auto)
+    int early_sgd = -1;
+    bool early_sgd_on() const { return early_sgd < 0 ? fp8() : early_sgd != 0; }
     bool early_on = false, early_done = false;
     float early_lr = 0.f;
     void sgd_chunk(int c) {
@@ -1786,7 +1787,7 @@ int vit_trainer_train_step(vit_trainer_t* h, float lr, int b_global) {
     vit_trainer_zero_grad(h);
     vit_trainer_forward(h, b_global);
     // the fused step knows lr before the backward: SGD per finished chunk (Trainer::early_sgd)
-    t.early_on = t.early_sgd && t.lowp() && !t.comm && t.two_streams && !t.timing && t.s2 && t.has_targets;
+    t.early_on = t.early_sgd_on() && t.lowp() && !t.comm && t.two_streams && !t.timing && t.s2 && t.has_targets;
     t.early_lr = lr;
     vit_trainer_backward(h);
     t.early_done = t.early_on && !vit::has_error();
@@ -2002,8 +2003,8 @@ int vit_trainer_set_option(vit_trainer_t* h, const char* name, int value) {
         t.ln_mx = value != 0;
     } else if (n == "fp8_ln_leftover") {  // fp8: LayerNorm -> MX forward, last partial round as rows (default 0)
         t.ln_left = value != 0;
-    } else if (n == "early_sgd") {  // bf16 / fp8, one GPU: SGD per finished gradient chunk inside train_step (default 0)
-        t.early_sgd = value != 0;
+    } else if (n == "early_sgd") {  // one GPU: SGD per finished gradient chunk inside train_step (default: fp8 mode only)
+        t.early_sgd = value < 0 ? -1 : value != 0;
     } else if (n == "pre_side") {  // bf16 / fp8: gradient clear + transposed weights on s2 beside the forward (default 1)
         t.pre_side_wait();
         t.pre_side = value != 0;
